@@ -1,0 +1,203 @@
+/*
+ * zombsole_mi355x.h — C ABI of the MI355X-native batched zombsole step engine.
+ *
+ * The reference (jvstinian/libzombsole) has no FFI: its boundary is the Python
+ * class surface ZombsoleGymEnv / MultiagentZombsoleEnv, whose per-tick work is
+ * `World.step` plus the env glue.  This header is the seam
+ * a maintainer binds from that surface (see INTEGRATION.md for the ctypes
+ * stub).  Each entry point names the reference code it replaces:
+ *
+ *   zs_create      <- ZombsoleGymEnv.__init__ / MultiagentZombsoleEnv.__init__
+ *                     (zombsole/gym_env.py:49-83, zombsole/gym/multiagent_env.py:25-78)
+ *                     + Game.__init__ (zombsole/game.py:115-140), N envs at once
+ *   zs_seed        <- random.seed(s) on the process-global CPython MT19937 the
+ *                     reference draws from (/usr/lib/python3.10/random.py:128-168);
+ *                     here one independent stream per env
+ *   zs_reset       <- env.reset() -> Game.__initialize_world__ + reward reset + obs
+ *                     (gym_env.py:148-164, gym/multiagent_env.py:173-184, game.py:151-169)
+ *   zs_step        <- env.step(action) (gym_env.py:99-145, gym/multiagent_env.py:111-171):
+ *                     set_action, World.step (core.py:72-78), rewards (gym/reward.py),
+ *                     respawn (game.py:196-201), observation (gym/observation.py),
+ *                     rules (zombsole/rules/{...}.py)
+ *   zs_get_state / zs_set_state
+ *                  <- the test pokes env.game.world.things, env.game.agents[i].life = x
+ *                     (tests/test_game.py:55,105, tests/test_multiagent_env.py:108)
+ *   zs_gen_actions <- (bench/parity only) the uniform discrete policy of SURVEY.md §8(d)
+ *
+ * Conventions: plain C types only; device buffers are raw HIP device pointers,
+ * `stream` is a hipStream_t passed as void*.  The engine owns its device
+ * state; the caller owns every output buffer.  All calls on one handle are
+ * serialized on the stream they are given.  Return value 0 = ok, otherwise a
+ * ZS_E* code with a message in zs_last_error() (thread-local).
+ */
+#ifndef ZOMBSOLE_MI355X_H
+#define ZOMBSOLE_MI355X_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes (mapped to Python exceptions by the wrapper) --------- */
+#define ZS_OK 0
+#define ZS_EINVAL 1    /* -> ValueError                                   */
+#define ZS_ENOSPACE 2  /* -> Exception('Not enough space to spawn ...') core.py:62-64 */
+#define ZS_EHIP 3      /* -> RuntimeError (HIP failure)                    */
+#define ZS_ESTATE 4    /* -> RuntimeError (bad call order / index)         */
+
+/* ---- thing kinds: the observation codes of gym/observation.py:18-26 ---- */
+#define ZS_THING_NONE 0
+#define ZS_THING_BOX 1
+#define ZS_THING_DEADBODY 2
+#define ZS_THING_OBJECTIVE 3
+#define ZS_THING_WALL 4
+#define ZS_THING_ZOMBIE 5
+#define ZS_THING_PLAYER 6 /* scripted bot (players/{...}.py)          */
+#define ZS_THING_AGENT 7  /* RL agent (players/agent.py)          */
+
+/* ---- weapons: the codes of gym/observation.py:27-34; table weapons.py:18-25 */
+#define ZS_WEAPON_NONE 0
+#define ZS_WEAPON_CLAWS 1
+#define ZS_WEAPON_KNIFE 10
+#define ZS_WEAPON_AXE 11
+#define ZS_WEAPON_GUN 12
+#define ZS_WEAPON_RIFLE 13
+#define ZS_WEAPON_SHOTGUN 14
+#define ZS_WEAPON_RANDOM 255 /* WeaponFactory 'random' (weapons.py:43-44) */
+
+/* ---- scripted bots (players/{...}.py) -------------------------------------- */
+#define ZS_BOT_TERMINATOR 1 /* players/terminator.py */
+#define ZS_BOT_SNIPER 2     /* players/sniper.py     */
+#define ZS_BOT_TROLL 3      /* players/troll.py      */
+#define ZS_BOT_HAMSTER 4    /* players/hamster.py    */
+#define ZS_BOT_RANDOMAN 5   /* players/randoman.py   */
+
+/* ---- rules (rules/factory.py:9-19) -------------------------------------- */
+#define ZS_RULES_EXTERMINATION 0
+#define ZS_RULES_SURVIVAL 1
+#define ZS_RULES_EVACUATION 2
+#define ZS_RULES_SAFEHOUSE 3
+
+/* ---- agent action kinds (int32 triple kind,dx,dy per agent) ------------- */
+#define ZS_ACT_IDLE 0
+#define ZS_ACT_MOVE 1
+#define ZS_ACT_ATTACK 2
+#define ZS_ACT_ATTACK_CLOSEST 3
+#define ZS_ACT_HEAL 4
+#define ZS_ACT_HEAL_CLOSEST 5
+#define ZS_ACT_CONFUSED 6
+
+/* ---- env surface / observation ------------------------------------------ */
+#define ZS_REWARD_SINGLE 0 /* AgentRewards, include_life_in_reward=True (gym/reward.py:19-47) */
+#define ZS_REWARD_MULTI 1  /* MultiAgentRewards (gym/reward.py:67-98)                         */
+#define ZS_OBS_WORLD 0
+#define ZS_OBS_SURROUNDINGS 1
+#define ZS_ENC_SIMPLE 0
+#define ZS_ENC_CHANNELS 1
+#define ZS_DTYPE_I32 0
+#define ZS_DTYPE_I64 1
+#define ZS_DTYPE_I16 2 /* compact internal form; values fit int16 */
+
+#define ZS_FLAG_AUTORESET 1u /* next-step autoreset: an env that ended is reset by the next zs_step */
+
+/* ---- map description (parsed by the host; zombsole/game.py:45-97) ------- */
+typedef struct zs_map_desc {
+    int32_t width, height;
+    int32_t n_obstacles;          /* boxes+walls in map-file (dict insertion) order */
+    const int32_t* obstacle_xy;   /* [n_obstacles][2]                               */
+    const uint8_t* obstacle_kind; /* ZS_THING_BOX / ZS_THING_WALL                   */
+    int32_t n_objectives;
+    const int32_t* objective_xy;  /* [n][2], map-file order                          */
+    int32_t n_player_spawns;
+    const int32_t* player_spawn_xy;
+    int32_t n_zombie_spawns;      /* 0 => every cell, x-major (core.py:44-47)        */
+    const int32_t* zombie_spawn_xy;
+} zs_map_desc;
+
+typedef struct zs_config {
+    int32_t num_envs;
+    zs_map_desc map;
+    int32_t rules;                /* ZS_RULES_*                                     */
+    int32_t num_agents;
+    const int32_t* agent_weapons; /* [num_agents] ZS_WEAPON_* or ZS_WEAPON_RANDOM    */
+    const int32_t* agent_codes;   /* [num_agents] channels code = 8 + int(agent_id)  */
+    int32_t num_bots;
+    const int32_t* bot_types;     /* [num_bots] ZS_BOT_* in player_names order       */
+    int32_t initial_zombies;
+    int32_t minimum_zombies;
+    int32_t reward_mode;          /* ZS_REWARD_*                                     */
+    int32_t obs_scope;            /* ZS_OBS_*                                        */
+    int32_t obs_encoding;         /* ZS_ENC_*                                        */
+    int32_t obs_width;            /* surroundings width (odd, > 1)                   */
+    int32_t obs_dtype;            /* ZS_DTYPE_*                                      */
+    int32_t max_episode_steps;    /* 0 = none; else TimeLimit-style truncation       */
+    uint32_t flags;               /* ZS_FLAG_*                                       */
+} zs_config;
+
+typedef struct zs_handle zs_handle;
+
+/* Thread-local message for the last failing call on this thread. */
+const char* zs_last_error(void);
+
+/* Validate `cfg`, allocate device state for cfg->num_envs envs on `device`. */
+int zs_create(const zs_config* cfg, int device, zs_handle** out);
+int zs_destroy(zs_handle* h);
+
+/* Per-env observation shape: out[0] = observations per env (1 for the single
+ * surface, num_agents for the multi surface), out[1..3] = C, H, W. */
+int zs_obs_shape(const zs_handle* h, int32_t out[4]);
+
+/* CPython random.seed(int) semantics per env, for envs [env0, env0+n).  Host
+ * array of n seeds.  Also records the seed as the env's action-stream seed. */
+int zs_seed(zs_handle* h, int32_t env0, int32_t n, const uint64_t* seeds_host, void* stream);
+
+/* Reset the envs whose byte in env_mask_dev is nonzero (NULL = all) and write
+ * their reset observations into obs_dev (other envs' slices untouched). */
+int zs_reset(zs_handle* h, const uint8_t* env_mask_dev, void* obs_dev, void* stream);
+
+/* One lock-step tick for every env.
+ *   actions_dev      int32 [N][num_agents][3]  (kind, dx, dy)
+ *   obs_dev          [N][obs_per_env][C][H][W] of cfg->obs_dtype
+ *   rewards_dev      float64 [N][num_agents]   (single surface: [N][1])
+ *   done_dev, trunc_dev   uint8 [N]
+ *   listed_dev       uint8 [N][num_agents]: agent was in env.agents before the
+ *                    step (multi surface: the keys of the returned dicts)
+ *   reset_dev        uint8 [N]: 1 when this call reset the env (autoreset)
+ * Any output pointer except obs/rewards/done/trunc may be NULL. */
+int zs_step(zs_handle* h, const int32_t* actions_dev, void* obs_dev, double* rewards_dev,
+            uint8_t* done_dev, uint8_t* trunc_dev, uint8_t* listed_dev, uint8_t* reset_dev,
+            void* stream);
+
+/* Bench / parity action stream: actions_dev[e][a] = DISCRETE table entry
+ * splitmix64(splitmix64(splitmix64(seed_e) ^ step) ^ a) % n_discrete
+ * (libzombsole_amd/actions.py).  n_discrete = 6 or 7. */
+int zs_gen_actions(zs_handle* h, uint64_t step, int32_t n_discrete, int32_t* actions_dev,
+                   void* stream);
+
+/* Host view of one env's state as a flat int32 record (layout below). */
+int zs_state_size(const zs_handle* h, int32_t* n_words);
+int zs_get_state(zs_handle* h, int32_t env, int32_t* buf_host, void* stream);
+int zs_set_state(zs_handle* h, int32_t env, const int32_t* buf_host, void* stream);
+
+/* Flat state record, int32 words:
+ *   [0]  t (World.t)          [1] deaths            [2] zombie_deaths
+ *   [3]  episode_steps        [4] n_order (things with ask_for_actions + ... present, dict order)
+ *   [5]  needs_reset          [6] n_entities (E)    [7] n_obstacles (O)
+ *   [8]  width                [9] height            [10] reward prev zombie_deaths
+ *   [11] n_zombies_present    [12..15] reserved
+ *   [16 .. 16+8E)  entity records: kind, present, x, y, life, weapon, extra, spawn_serial
+ *                  (slots: agents [0,A), bots [A,A+P), zombies [A+P,E))
+ *   [.. +E)        order: entity slot ids in dict order (first n_order valid)
+ *   [.. +O)        obstacle life      [.. +O) obstacle present (0/1)
+ *   [.. +A)        reward tracker previous life per agent
+ *   [.. +A)        listed (agent in env.agents) per agent
+ *   [.. +ceil(W*H/32)) dead-body bitmap, bit (y*W+x)
+ */
+#define ZS_STATE_HEADER 16
+#define ZS_STATE_ENTITY_WORDS 8
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ZOMBSOLE_MI355X_H */
