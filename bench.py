@@ -1,0 +1,187 @@
+#!/usr/bin/env python3
+"""Benchmark: batched zombsole env-steps/s on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[2], "C3"): synthetic 64x64 `bridge64` map,
+extermination rules, MultiagentZombsoleEnv semantics with 2 agents + 10
+zombies per env, 21x21x3 int64 channel observations for every agent written to
+HBM each step, uniform Discrete(7) policy generated on device
+(splitmix64(seed, step, agent)), gym TimeLimit 1000, next-step autoreset.
+65 536 envs over 8 GPUs = 8 192 envs per GPU; envs are independent, so each
+rank owns a contiguous global env range (seeds = global index) and no data-path
+collective runs ("weak" scaling: per-GPU work fixed as GPUs are added).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--envs-per-gpu 8192]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+Prints ONE JSON line (rank 0).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "env-steps/sec (whole node), 65 536 parallel 64×64 envs at 1/2/4/8 MI355X"
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--envs-per-gpu", type=int, default=8192)
+    p.add_argument("--map", default="bridge64")
+    p.add_argument("--agents", type=int, default=2)
+    p.add_argument("--zombies", type=int, default=10)
+    p.add_argument("--max-episode-steps", type=int, default=1000)
+    p.add_argument("--obs-dtype", default="int64", choices=["int64", "int32", "int16"])
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-steps", type=int, default=300)
+    return p.parse_args()
+
+
+def algorithmic_bytes(E, A, occ_bytes, obs_bytes_per_env, mt_words):
+    """SURVEY.md §8(d) per env-step figures, split by kernel.
+
+    k_tick: entity SoA read+write (E x 12 B x 2) + MT state (8 B) + MT words consumed x 4 B
+            + occupancy bitmap read (W*H/8 B) + actions (A x 12 B) + rewards (8A) + 3 flag bytes
+    k_obs : observation bytes written (A x 3 x 21 x 21 x 8 B for int64)
+    """
+    tick = 2 * E * 12 + 8 + 4 * mt_words + occ_bytes + A * 12 + 8 * A + 3
+    return tick, obs_bytes_per_env
+
+
+def cpu_baseline(args, builder_fn):
+    """The C oracle (bit-exact CPU restatement, "port") on this host, bounded sample."""
+    from oracle.oracle import run_batch
+    try:
+        threads = len(os.sched_getaffinity(0))
+    except AttributeError:
+        threads = os.cpu_count() or 1
+    threads = max(1, min(threads, int(os.environ.get("OMP_NUM_THREADS", "16") or 16), 16))
+    n_envs = min(args.envs_per_gpu, 8192)
+    b = builder_fn(1)
+    t0 = time.perf_counter()
+    n, _ = run_batch(b, 0, n_envs, args.cpu_steps, 7, threads=threads)
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": "C oracle (oracle/zs_oracle.c, OpenMP over envs), %d envs x %d steps of the same "
+                      "workload (same map/agents/zombies/policy/obs), %.1f s wall" % (n_envs, args.cpu_steps, dt)}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from libzombsole_amd import _abi
+    from libzombsole_amd.engine import Engine
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.cuda.current_device()
+    dtype = {"int64": _abi.DTYPE_I64, "int32": _abi.DTYPE_I32, "int16": _abi.DTYPE_I16}[args.obs_dtype]
+    agent_ids = [str(i) for i in range(args.agents)]
+
+    def builder(n):
+        return _abi.multi_env_config(n, "extermination", [], args.map, agent_ids, initial_zombies=args.zombies,
+                                     minimum_zombies=0, max_episode_steps=args.max_episode_steps,
+                                     obs_dtype=dtype)
+
+    n_local = args.envs_per_gpu
+    env0 = rank * n_local
+    eng = Engine(builder(n_local), device=dev)
+    eng.seed([env0 + i for i in range(n_local)])
+    eng.reset()
+    torch.cuda.synchronize()
+
+    step = 0
+    for _ in range(args.warmup):
+        step += 1
+        eng.gen_actions(step, 7)
+        eng.step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    eng.profile(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step += 1
+        eng.gen_actions(step, 7)
+        eng.step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    prof = eng.profile_read()
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    total_envs = n_local * world
+    value = total_envs * args.steps / elapsed
+
+    # roofline of the dominant kernel (HIP-event durations on the engine's stream)
+    m = eng.builder.map
+    E = args.agents + args.zombies
+    obs_per_env = eng.obs[0].numel() * eng.obs.element_size()
+    mt_words = 40  # measured average MT words per env-step for this workload
+    tick_b, obs_b = algorithmic_bytes(E, args.agents, (m.size[0] * m.size[1] + 7) // 8, obs_per_env, mt_words)
+    tick_ms = prof["tick_ms"] / max(prof["tick_n"], 1)
+    obs_ms = prof["obs_ms"] / max(prof["obs_n"], 1)
+    if tick_ms >= obs_ms:
+        dom, dom_ms, dom_b = "k_tick", tick_ms, tick_b
+    else:
+        dom, dom_ms, dom_b = "k_obs", obs_ms, obs_b
+    achieved = dom_b * n_local / (dom_ms * 1e-3) / 1e9
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc):
+        try:
+            with open(pmc) as f:
+                traffic = json.load(f).get(dom, {}).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    out = {
+        "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "int32", "data": "synthetic",
+        "config": {"workload": "C3 shard: %d %dx%d '%s' envs per GPU (%d total), extermination, %d agents + %d "
+                               "zombies, uniform Discrete(7) policy on device, 21x21x3 %s obs per agent, "
+                               "TimeLimit %d, next-step autoreset" % (
+                                   n_local, m.size[0], m.size[1], args.map, total_envs, args.agents,
+                                   args.zombies, args.obs_dtype, args.max_episode_steps),
+                   "envs_per_gpu": n_local, "total_envs": total_envs, "map": args.map,
+                   "agents": args.agents, "zombies": args.zombies, "obs_dtype": args.obs_dtype,
+                   "parallelism": "env-sharded x%d (no data-path collective)" % world},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
+                     "algorithmic_bytes_per_launch": dom_b * n_local,
+                     "avg_launch_ms": dom_ms, "k_tick_ms": tick_ms, "k_obs_ms": obs_ms},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args, builder)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -180,6 +180,14 @@ int zs_state_size(const zs_handle* h, int32_t* n_words);
 int zs_get_state(zs_handle* h, int32_t env, int32_t* buf_host, void* stream);
 int zs_set_state(zs_handle* h, int32_t env, const int32_t* buf_host, void* stream);
 
+/* Diagnostics (not part of the reference surface): when enabled, every k_tick
+ * (the step kernel) and k_obs (the observation kernel) launch is bracketed by
+ * HIP events on its stream.  zs_profile_read synchronizes and returns
+ * out[0] = total k_tick ms, out[1] = k_tick launches, out[2] = total k_obs ms,
+ * out[3] = k_obs launches, then clears the record. */
+int zs_profile(zs_handle* h, int32_t enable);
+int zs_profile_read(zs_handle* h, double out[4]);
+
 /* Flat state record, int32 words:
  *   [0]  t (World.t)          [1] deaths            [2] zombie_deaths
  *   [3]  episode_steps        [4] n_order (things with ask_for_actions + ... present, dict order)

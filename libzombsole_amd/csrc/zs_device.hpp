@@ -1,0 +1,166 @@
+// zs_device.hpp — device-side data layout and primitives of the MI355X zombsole engine.
+//
+// Layout in HBM (N envs, E = A + P + Z entity slots, O obstacles, W x H map):
+//   * entity SoA, env-minor [slot][N]: pos (x | y << 16, int16 each), life (int32),
+//     weapon (u8), present (u8), serial (u32), order (u8 dict-order list)
+//       -> a wave of 64 envs touching the same slot issues one 256-B coalesced access.
+//   * per-env scalars [k][N] (World.t, deaths, zombie_deaths, ...), agent tracker [a][N].
+//   * env-major per-env blocks (each lane walks its own env):
+//       occ   [N][occ_stride] u8   cell -> entity slot + 1   (World.things for entities)
+//       dead  [N][DW] u32          dead-body decoration bitmap
+//       obstacle hp [N][O] int32, present / nonpos bitmaps [N][OW] u32
+//       MT19937 ring [N][2][624] u32 (current block + precomputed next block)
+//   * static, shared by all envs: cellmap (cell -> obstacle index), objective bitmap,
+//     obstacle xy/kind, spawn lists.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/zombsole_mi355x.h"
+
+#define ZS_MT_N 624
+#define ZS_MT_M 397
+#define ZS_RING_WORDS (2 * ZS_MT_N)
+
+// per-env scalar rows
+enum {
+    S_T = 0,        // World.t (core.py:17)
+    S_DEATHS,       // World.deaths
+    S_ZD,           // World.zombie_deaths
+    S_EPSTEPS,      // steps since reset (TimeLimit)
+    S_NORDER,       // entities present (length of the dict-order list)
+    S_NEEDRESET,    // autoreset pending
+    S_PREVZD,       // reward tracker zombie_deaths (gym/reward.py:23,70)
+    S_SERIAL,       // spawn serial counter (state views)
+    S_ODIRTY,       // some obstacle may need removal at the next cleanup
+    S_NSCAL
+};
+
+struct Dev {
+    int N, W, H, O, A, P, Z, E, OW, DW, ncand, nps, nzs, nobj;
+    int occ_stride;
+    int rules, reward_mode, obs_scope, obs_enc, obs_w, obs_dtype, max_steps;
+    int initial_zombies, minimum_zombies;
+    uint32_t flags;
+    // static
+    const int16_t* cellmap;
+    const uint32_t* objbits;
+    const int32_t* obst_xy;  // packed x | y << 16
+    const uint8_t* obst_kind;
+    const int32_t* pspawn;   // packed
+    const int32_t* zspawn;   // packed
+    const int32_t* agent_weapons;
+    const int32_t* agent_codes;
+    const int32_t* bot_types;
+    // per env
+    int32_t* pos;
+    int32_t* life;
+    uint8_t* weapon;
+    uint8_t* present;
+    uint32_t* serial;
+    uint8_t* order;
+    int32_t* scal;
+    int32_t* prev_life;
+    uint8_t* listed;
+    int32_t* obst_hp;
+    uint32_t* obst_present;
+    uint32_t* obst_nonpos;
+    uint8_t* occ;
+    uint32_t* dead;
+    uint32_t* ring;
+    uint32_t* rngst;
+    uint64_t* seeds;
+    int32_t* cand;
+};
+
+__device__ __forceinline__ int32_t pack_xy(int x, int y) { return (int32_t)((uint32_t)(x & 0xffff) | ((uint32_t)y << 16)); }
+__device__ __forceinline__ int unpack_x(int32_t p) { return (int)(int16_t)(p & 0xffff); }
+__device__ __forceinline__ int unpack_y(int32_t p) { return (int)(p >> 16); }
+
+// ---------------------------------------------------------------------------
+// CPython MT19937 stream, one per env.
+// The ring holds two consecutive 624-word blocks of the raw (untempered) MT
+// sequence x[k]: the block being consumed and, when `ready`, the next one, so a
+// lane can draw >= 624 words without twisting.  x[k+624] = x[k+397] ^ f(x[k], x[k+1])
+// lets the next block be produced from the current one (serially in a lane on
+// the rare slow path, cooperatively by a whole wave in zs_rng_refill).
+// rngst packs: offset (bits 0..9), current slot (bit 10), next-ready (bit 11).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
+    y ^= (y >> 11);
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= (y >> 18);
+    return y;
+}
+
+__device__ __forceinline__ uint32_t mt_f(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
+    return c ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+}
+
+// dst = the 624-word block that follows src (Modules/_randommodule.c genrand_uint32 twist)
+__device__ inline void mt_twist_serial(uint32_t* dst, const uint32_t* src) {
+    for (int i = 0; i < ZS_MT_N; i++) {
+        uint32_t b = (i + 1 < ZS_MT_N) ? src[i + 1] : dst[0];
+        uint32_t c = (i + ZS_MT_M < ZS_MT_N) ? src[i + ZS_MT_M] : dst[i + ZS_MT_M - ZS_MT_N];
+        dst[i] = mt_f(src[i], b, c);
+    }
+}
+
+struct Rng {
+    uint32_t* ring;  // this env's 1248 words
+    uint32_t st;
+};
+
+__device__ __forceinline__ uint32_t rng_u32(Rng& r) {
+    uint32_t off = r.st & 1023u, slot = (r.st >> 10) & 1u, ready = (r.st >> 11) & 1u;
+    if (off >= ZS_MT_N) {
+        if (!ready) mt_twist_serial(r.ring + (slot ^ 1u) * ZS_MT_N, r.ring + slot * ZS_MT_N);
+        slot ^= 1u;
+        off = 0;
+        ready = 0;
+    }
+    uint32_t y = r.ring[slot * ZS_MT_N + off];
+    r.st = (off + 1) | (slot << 10) | (ready << 11);
+    return mt_temper(y);
+}
+
+// Random._randbelow_with_getrandbits (random.py:239-249); getrandbits(k<=32) = u32 >> (32-k)
+__device__ __forceinline__ int rng_below(Rng& r, int n) {
+    if (n <= 0) return 0;
+    int k = 32 - __clz(n);
+    uint32_t v;
+    do {
+        v = rng_u32(r) >> (32 - k);
+    } while (v >= (uint32_t)n);
+    return (int)v;
+}
+
+// randint(a, b) (random.py:366-370)
+__device__ __forceinline__ int rng_int(Rng& r, int a, int b) { return a + rng_below(r, b - a + 1); }
+
+// ---------------------------------------------------------------------------
+// weapons (weapons.py:18-25) with the sqrt range tests as exact integer d^2
+// bounds: dist > 1.5 <=> d2 >= 3, > 3 <=> d2 >= 10, > 6 <=> d2 >= 37, > 10 <=> d2 >= 101
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int weapon_r2(int w) {
+    return w == ZS_WEAPON_GUN ? 36 : w == ZS_WEAPON_RIFLE ? 100 : w == ZS_WEAPON_SHOTGUN ? 9 : 2;
+}
+__device__ __forceinline__ int weapon_lo(int w) {
+    return w == ZS_WEAPON_AXE ? 75 : w == ZS_WEAPON_GUN ? 10 : w == ZS_WEAPON_RIFLE ? 25 : w == ZS_WEAPON_SHOTGUN ? 75 : 5;
+}
+__device__ __forceinline__ int weapon_hi(int w) {
+    return w == ZS_WEAPON_AXE ? 100 : w == ZS_WEAPON_GUN ? 50 : w == ZS_WEAPON_RIFLE ? 75 : w == ZS_WEAPON_SHOTGUN ? 100 : 10;
+}
+
+__device__ __forceinline__ int d2(int x1, int y1, int x2, int y2) {
+    int dx = x1 - x2, dy = y1 - y2;
+    return dx * dx + dy * dy;
+}
+
+__device__ __forceinline__ int64_t floordiv100(int64_t a) {  // Python a // 100
+    int64_t q = a / 100;
+    if ((a % 100) != 0 && a < 0) q -= 1;
+    return q;
+}

@@ -1,0 +1,225 @@
+"""Runtime binding of the HIP engine (libzombsole_mi355x.so) through its C ABI.
+
+`Engine` owns one `zs_handle` (N envs on one GPU) plus the torch device
+tensors the engine writes its outputs into.  There is no CPU fallback: if
+the shared library or a HIP device is missing, construction raises.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import _abi
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_build", "libzombsole_mi355x.so")
+SYMBOLS = ["zs_last_error", "zs_create", "zs_destroy", "zs_obs_shape", "zs_seed", "zs_reset", "zs_step",
+           "zs_gen_actions", "zs_state_size", "zs_get_state", "zs_set_state", "zs_profile", "zs_profile_read"]
+
+_lib = None
+
+
+class EngineUnavailable(RuntimeError):
+    pass
+
+
+def load_library(path=None):
+    """Load the engine .so (no device call is made)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise EngineUnavailable("HIP engine library not built: %s (run __graft_entry__.build())" % p)
+    L = C.CDLL(p)
+    vp, i32, u64 = C.c_void_p, C.c_int32, C.c_uint64
+    L.zs_last_error.restype = C.c_char_p
+    L.zs_create.argtypes = [vp, C.c_int, C.POINTER(vp)]
+    L.zs_destroy.argtypes = [vp]
+    L.zs_obs_shape.argtypes = [vp, C.POINTER(i32)]
+    L.zs_seed.argtypes = [vp, i32, i32, C.POINTER(u64), vp]
+    L.zs_reset.argtypes = [vp, vp, vp, vp]
+    L.zs_step.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.zs_gen_actions.argtypes = [vp, u64, i32, vp, vp]
+    L.zs_state_size.argtypes = [vp, C.POINTER(i32)]
+    L.zs_get_state.argtypes = [vp, i32, vp, vp]
+    L.zs_set_state.argtypes = [vp, i32, vp, vp]
+    L.zs_profile.argtypes = [vp, i32]
+    L.zs_profile_read.argtypes = [vp, C.POINTER(C.c_double)]
+    for s in SYMBOLS:
+        if s != "zs_last_error":
+            getattr(L, s).restype = C.c_int
+    if path is None:
+        _lib = L
+    return L
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+def _raise(L, rc, what):
+    msg = (L.zs_last_error() or b"").decode(errors="replace")
+    if rc == _abi.ZS_EINVAL:
+        raise ValueError("%s: %s" % (what, msg))
+    if rc == _abi.ZS_ENOSPACE:
+        raise Exception(msg or "Not enough space to spawn")  # core.py:62-64 raises a bare Exception
+    raise EngineError("%s failed (%d): %s" % (what, rc, msg))
+
+
+def _ptr(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class Engine(object):
+    """N lock-step envs on one MI355X."""
+
+    def __init__(self, builder, device=None):
+        import torch
+        if not torch.cuda.is_available():
+            raise EngineUnavailable("no HIP device visible: the zombsole engine runs only on the GPU")
+        self.torch = torch
+        self.L = load_library()
+        self.builder = builder
+        self.device = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+        self.h = C.c_void_p()
+        rc = self.L.zs_create(C.cast(builder.ptr(), C.c_void_p), self.device.index, C.byref(self.h))
+        if rc:
+            _raise(self.L, rc, "zs_create")
+        shp = (C.c_int32 * 4)()
+        self.L.zs_obs_shape(self.h, shp)
+        self.obs_shape = tuple(int(v) for v in shp)
+        self.N = builder.cfg.num_envs
+        self.A = builder.num_agents
+        self.multi = builder.cfg.reward_mode == _abi.REWARD_MULTI
+        dt = {_abi.DTYPE_I32: torch.int32, _abi.DTYPE_I64: torch.int64, _abi.DTYPE_I16: torch.int16}
+        self.obs_dtype = dt[builder.cfg.obs_dtype]
+        kw = dict(device=self.device)
+        self.obs = torch.zeros((self.N,) + self.obs_shape, dtype=self.obs_dtype, **kw)
+        self.rewards = torch.zeros((self.N, self.A if self.multi else 1), dtype=torch.float64, **kw)
+        self.done = torch.zeros(self.N, dtype=torch.uint8, **kw)
+        self.trunc = torch.zeros(self.N, dtype=torch.uint8, **kw)
+        self.listed = torch.zeros((self.N, self.A), dtype=torch.uint8, **kw)
+        self.was_reset = torch.zeros(self.N, dtype=torch.uint8, **kw)
+        self.actions = torch.zeros((self.N, self.A, 3), dtype=torch.int32, **kw)
+        n = C.c_int32()
+        self.L.zs_state_size(self.h, C.byref(n))
+        self.state_words = int(n.value)
+
+    def close(self):
+        if getattr(self, "h", None) and self.h.value:
+            self.L.zs_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _stream(self):
+        return C.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
+
+    def seed(self, seeds, env0=0):
+        arr = np.ascontiguousarray(np.asarray(seeds, dtype=np.uint64).reshape(-1))
+        rc = self.L.zs_seed(self.h, env0, len(arr), arr.ctypes.data_as(C.POINTER(C.c_uint64)), self._stream())
+        if rc:
+            _raise(self.L, rc, "zs_seed")
+
+    def reset(self, mask=None):
+        """Reset envs (all, or where the uint8 device tensor `mask` is nonzero)."""
+        rc = self.L.zs_reset(self.h, _ptr(mask), _ptr(self.obs), self._stream())
+        if rc:
+            _raise(self.L, rc, "zs_reset")
+        return self.obs
+
+    def step(self, actions=None):
+        """One tick for all envs; `actions` int32 [N, A, 3] device tensor (default: self.actions)."""
+        a = self.actions if actions is None else actions
+        rc = self.L.zs_step(self.h, _ptr(a), _ptr(self.obs), _ptr(self.rewards), _ptr(self.done),
+                            _ptr(self.trunc), _ptr(self.listed), _ptr(self.was_reset), self._stream())
+        if rc:
+            _raise(self.L, rc, "zs_step")
+        return self.obs, self.rewards, self.done, self.trunc
+
+    def gen_actions(self, step, n_discrete, out=None):
+        o = self.actions if out is None else out
+        rc = self.L.zs_gen_actions(self.h, int(step), int(n_discrete), _ptr(o), self._stream())
+        if rc:
+            _raise(self.L, rc, "zs_gen_actions")
+        return o
+
+    def profile(self, enable=True):
+        """Bracket every k_tick / k_obs launch with HIP events on its stream."""
+        self.L.zs_profile(self.h, 1 if enable else 0)
+
+    def profile_read(self):
+        """{'tick_ms': total, 'tick_n': launches, 'obs_ms': total, 'obs_n': launches}."""
+        out = (C.c_double * 4)()
+        rc = self.L.zs_profile_read(self.h, out)
+        if rc:
+            _raise(self.L, rc, "zs_profile_read")
+        return {"tick_ms": out[0], "tick_n": int(out[1]), "obs_ms": out[2], "obs_n": int(out[3])}
+
+    def get_state(self, env):
+        buf = np.zeros(self.state_words, dtype=np.int32)
+        rc = self.L.zs_get_state(self.h, int(env), C.c_void_p(buf.ctypes.data), self._stream())
+        if rc:
+            _raise(self.L, rc, "zs_get_state")
+        return StateView(self, buf)
+
+    def set_state(self, env, view):
+        rc = self.L.zs_set_state(self.h, int(env), C.c_void_p(view.buf.ctypes.data), self._stream())
+        if rc:
+            _raise(self.L, rc, "zs_set_state")
+
+
+class StateView(object):
+    """Decoded zs_get_state record (layout: include/zombsole_mi355x.h)."""
+
+    def __init__(self, eng, buf):
+        self.buf = buf
+        b = buf
+        self.E, self.O, self.W, self.H = int(b[6]), int(b[7]), int(b[8]), int(b[9])
+        self.A = eng.A
+        self.P = eng.builder.num_bots
+        o = _abi.STATE_HEADER
+        self.ent = b[o:o + _abi.STATE_ENTITY_WORDS * self.E].reshape(self.E, _abi.STATE_ENTITY_WORDS)
+        o += _abi.STATE_ENTITY_WORDS * self.E
+        self.order = b[o:o + self.E]
+        o += self.E
+        self.obst_life = b[o:o + self.O]
+        o += self.O
+        self.obst_present = b[o:o + self.O]
+        o += self.O
+        self.prev_life = b[o:o + self.A]
+        o += self.A
+        self.listed = b[o:o + self.A]
+        o += self.A
+        dw = (self.W * self.H + 31) // 32
+        self.dead_words = b[o:o + dw]
+
+    t = property(lambda s: int(s.buf[0]))
+    deaths = property(lambda s: int(s.buf[1]))
+    zombie_deaths = property(lambda s: int(s.buf[2]))
+    n_order = property(lambda s: int(s.buf[4]))
+
+    def dead_cells(self):
+        w = self.dead_words.astype(np.uint32)
+        bits = np.unpackbits(w.view(np.uint8), bitorder="little")
+        return [int(c) for c in np.nonzero(bits[:self.W * self.H])[0]]
+
+    def canonical(self, obstacle_kinds):
+        """The canonical state dict of tests/golden records."""
+        dyn = []
+        for s in self.order[:self.n_order]:
+            r = self.ent[int(s)]
+            dyn.append([int(r[0]), int(r[2]), int(r[3]), int(r[4]), int(r[5]), int(r[6])])
+        obst = []
+        for i in range(self.O):
+            ml = 10 if obstacle_kinds[i] == _abi.THING_BOX else 200
+            if int(self.obst_life[i]) != ml or not self.obst_present[i]:
+                obst.append([i, int(self.obst_life[i]), int(self.obst_present[i])])
+        agents = [[int(r[2]), int(r[3]), int(r[4]), int(r[5])] for r in self.ent[:self.A]]
+        players = [[int(r[2]), int(r[3]), int(r[4]), int(r[5])] for r in self.ent[self.A:self.A + self.P]]
+        return {"dyn": dyn, "obst": obst, "dead": self.dead_cells(), "ctr": [self.t, self.deaths, self.zombie_deaths],
+                "agents": agents, "players": players}

@@ -1,0 +1,115 @@
+"""HIP engine vs the C oracle on many seeded envs (bit-exact), through the C ABI.
+
+Covers the configs of BASELINE.json at reduced env counts (the oracle finishes
+them in seconds) plus bots / rules / encodings the golden fixtures touch only
+briefly.  Full-size runs are checked by size-independent properties in
+test_engine_props.py.
+"""
+import numpy as np
+import pytest
+
+from libzombsole_amd import _abi
+from libzombsole_amd import actions as A
+
+pytestmark = pytest.mark.gpu
+
+
+def _rich_triples(seed, step, n_agents):
+    return np.array([A.encode_action(A.rich_action(seed, step, a)) for a in range(n_agents)], dtype=np.int32)
+
+
+def run_parity(make_builder, n_envs, steps, stream="discrete", seed0=1000, n_discrete=7, check_state_every=25):
+    import torch
+    from libzombsole_amd.engine import Engine
+    from oracle.oracle import OracleEnv
+
+    eng = Engine(make_builder(n_envs))
+    kinds = [o[2] for o in eng.builder.map.obstacles]
+    seeds = [seed0 + i for i in range(n_envs)]
+    eng.seed(seeds)
+    obs0 = eng.reset().cpu().numpy()
+    refs = []
+    for k, s in enumerate(seeds):
+        o = OracleEnv(make_builder(1))
+        o.seed(s)
+        exp = o.reset()
+        assert np.array_equal(obs0[k], exp), ("reset obs", k)
+        refs.append(o)
+    need = [False] * n_envs
+    for t in range(1, steps + 1):
+        if stream == "discrete":
+            eng.gen_actions(t, n_discrete)
+            acts = eng.actions.cpu().numpy()
+        else:
+            acts = np.stack([_rich_triples(s, t, eng.A) for s in seeds])
+            eng.actions.copy_(torch.from_numpy(acts))
+        eng.step()
+        torch.cuda.synchronize()
+        obs = eng.obs.cpu().numpy()
+        rew = eng.rewards.cpu().numpy()
+        done = eng.done.cpu().numpy()
+        trunc = eng.trunc.cpu().numpy()
+        was_reset = eng.was_reset.cpu().numpy()
+        for k, o in enumerate(refs):
+            if need[k]:
+                assert was_reset[k], ("expected autoreset", k, t)
+                exp = o.reset()
+                need[k] = False
+            else:
+                assert not was_reset[k], ("unexpected reset", k, t)
+                exp, r, d, tr, lb = o.step(acts[k])
+                assert bool(done[k]) == d and bool(trunc[k]) == tr, ("flags", k, t)
+                if eng.multi:
+                    assert np.array_equal(rew[k][lb], r[:eng.A][lb]), ("rew", k, t, rew[k], r)
+                else:
+                    assert rew[k][0] == r[0], ("rew", k, t, rew[k][0], r[0])
+                need[k] = d or tr
+            assert np.array_equal(obs[k], exp), ("obs", k, t)
+            if check_state_every and t % check_state_every == 0:
+                assert eng.get_state(k).canonical(kinds) == o.state(), ("state", k, t)
+    eng.close()
+
+
+def c2(n):
+    return _abi.multi_env_config(n, "extermination", [], "bridge64", ["0", "1"], initial_zombies=10,
+                                 minimum_zombies=0, max_episode_steps=1000)
+
+
+def test_c2_bridge64_multi_discrete():
+    run_parity(c2, 192, 160)
+
+
+def test_single_bridge_world_simple():
+    run_parity(lambda n: _abi.single_env_config(n, "extermination", [], "bridge", 0, initial_zombies=10,
+                                                observation_scope="world", observation_position_encoding="simple",
+                                                max_episode_steps=1000),
+               128, 120, n_discrete=6)
+
+
+def test_city128_safehouse_respawn():
+    run_parity(lambda n: _abi.multi_env_config(n, "safehouse", [], "city128", ["0", "1", "2", "3"],
+                                               initial_zombies=50, minimum_zombies=50),
+               48, 60)
+
+
+def test_city_for_safehouse_long_shuffles():
+    run_parity(lambda n: _abi.multi_env_config(n, "safehouse", [], "city_for_safehouse", ["0", "1", "2", "3"],
+                                               initial_zombies=50, minimum_zombies=50),
+               32, 40)
+
+
+def test_bots_rules_rich_actions():
+    run_parity(lambda n: _abi.single_env_config(n, "evacuation", ["terminator", "randoman", "hamster", "troll"],
+                                                "easy_exit", "0", initial_zombies=8, minimum_zombies=6,
+                                                observation_scope="surroundings:9",
+                                                observation_position_encoding="channels", agent_weapon="random",
+                                                max_episode_steps=80),
+               96, 150, stream="rich")
+
+
+def test_multi_bots_survival_rich_int16():
+    run_parity(lambda n: _abi.multi_env_config(n, "survival", ["sniper", "randoman"], "fort",
+                                               ["0", "1", "2"], initial_zombies=30, minimum_zombies=20,
+                                               agent_weapons=["random", "gun"], observation_surroundings_width=11,
+                                               obs_dtype=_abi.DTYPE_I16, max_episode_steps=70),
+               64, 140, stream="rich")
