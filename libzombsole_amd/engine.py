@@ -81,6 +81,10 @@ class Engine(object):
         self.L = load_library()
         self.builder = builder
         self.device = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+        # Initialise torch's HIP runtime on this device first: the engine .so binds to the same
+        # libamdhip64 torch loaded (one runtime per process), and a bare is_available() leaves
+        # that runtime without a device context (hipSetDevice then reports no device).
+        torch.zeros(1, device=self.device)
         self.h = C.c_void_p()
         rc = self.L.zs_create(C.cast(builder.ptr(), C.c_void_p), self.device.index, C.byref(self.h))
         if rc:
