@@ -30,6 +30,10 @@ def load_library(path=None):
     p = path or LIB_PATH
     if not os.path.exists(p):
         raise EngineUnavailable("HIP engine library not built: %s (run __graft_entry__.build())" % p)
+    # torch ships its own libamdhip64.so.7 / libhsa-runtime64.so.1; load it first so the engine
+    # binds to that same runtime (same SONAME) instead of pulling a second HIP runtime from
+    # /opt/rocm into the process, which cannot open the device once torch's runtime owns it.
+    import torch  # noqa: F401
     L = C.CDLL(p)
     vp, i32, u64 = C.c_void_p, C.c_int32, C.c_uint64
     L.zs_last_error.restype = C.c_char_p
