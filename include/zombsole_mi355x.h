@@ -133,6 +133,7 @@ typedef struct zs_config {
     int32_t obs_dtype;            /* ZS_DTYPE_*                                      */
     int32_t max_episode_steps;    /* 0 = none; else TimeLimit-style truncation       */
     uint32_t flags;               /* ZS_FLAG_*                                       */
+    int32_t lanes_per_env;        /* k_tick lanes per env (1..64, power of 2); 0 = auto */
 } zs_config;
 
 typedef struct zs_handle zs_handle;

@@ -56,7 +56,7 @@ class zs_config(C.Structure):
                 ("initial_zombies", C.c_int32), ("minimum_zombies", C.c_int32),
                 ("reward_mode", C.c_int32), ("obs_scope", C.c_int32), ("obs_encoding", C.c_int32),
                 ("obs_width", C.c_int32), ("obs_dtype", C.c_int32),
-                ("max_episode_steps", C.c_int32), ("flags", C.c_uint32)]
+                ("max_episode_steps", C.c_int32), ("flags", C.c_uint32), ("lanes_per_env", C.c_int32)]
 
 
 def rules_id(rules_name):
@@ -138,7 +138,7 @@ class ConfigBuilder(object):
 
     def __init__(self, num_envs, map_, rules, agent_weapons, agent_codes, bot_types, initial_zombies,
                  minimum_zombies, reward_mode, obs_scope, obs_encoding, obs_width, obs_dtype,
-                 max_episode_steps=0, autoreset=True):
+                 max_episode_steps=0, autoreset=True, lanes_per_env=0):
         m = map_ if isinstance(map_, Map) else load_map(map_)
         self.map = m
 
@@ -162,7 +162,8 @@ class ConfigBuilder(object):
         self.cfg = zs_config(int(num_envs), md, int(rules), len(self._aw), p32(self._aw), p32(self._ac),
                              len(self._bt), p32(self._bt), int(initial_zombies), int(minimum_zombies),
                              int(reward_mode), int(obs_scope), int(obs_encoding), int(obs_width),
-                             int(obs_dtype), int(max_episode_steps), FLAG_AUTORESET if autoreset else 0)
+                             int(obs_dtype), int(max_episode_steps), FLAG_AUTORESET if autoreset else 0,
+                             int(lanes_per_env))
 
     @property
     def num_agents(self):
@@ -189,7 +190,8 @@ class ConfigBuilder(object):
 
 def single_env_config(num_envs, rules_name, player_names, map_name, agent_id, initial_zombies=0,
                       minimum_zombies=0, observation_scope="world", observation_position_encoding="simple",
-                      agent_weapon="rifle", max_episode_steps=0, obs_dtype=DTYPE_I32, autoreset=True):
+                      agent_weapon="rifle", max_episode_steps=0, obs_dtype=DTYPE_I32, autoreset=True,
+                      lanes_per_env=0):
     """zs_config for the ZombsoleGymEnv surface (gym_env.py:49-83): one agent + bots."""
     m = load_map(map_name)
     rules = rules_id(rules_name)
@@ -199,13 +201,13 @@ def single_env_config(num_envs, rules_name, player_names, map_name, agent_id, in
     enc = parse_encoding(observation_position_encoding)
     return ConfigBuilder(num_envs, m, rules, weapons, [agent_code(agent_id)], bots, initial_zombies,
                          minimum_zombies, REWARD_SINGLE, scope, enc, width, obs_dtype, max_episode_steps,
-                         autoreset)
+                         autoreset, lanes_per_env)
 
 
 def multi_env_config(num_envs, rules_name, player_names, map_name, agent_ids, initial_zombies=0,
                      minimum_zombies=0, observation_surroundings_width=21,
                      observation_position_encoding_style="channels", agent_weapons="rifle",
-                     max_episode_steps=0, obs_dtype=DTYPE_I64, autoreset=True):
+                     max_episode_steps=0, obs_dtype=DTYPE_I64, autoreset=True, lanes_per_env=0):
     """zs_config for the MultiagentZombsoleEnv surface (gym/multiagent_env.py:25-78)."""
     w = int(observation_surroundings_width)
     if (w % 2 == 0) or (w <= 1):
@@ -219,4 +221,4 @@ def multi_env_config(num_envs, rules_name, player_names, map_name, agent_ids, in
     weapons = [weapon_id(n) for n in names]
     return ConfigBuilder(num_envs, m, rules, weapons, [agent_code(a) for a in ids], bots, initial_zombies,
                          minimum_zombies, REWARD_MULTI, OBS_SURROUNDINGS, enc, w, obs_dtype,
-                         max_episode_steps, autoreset)
+                         max_episode_steps, autoreset, lanes_per_env)

@@ -1,17 +1,17 @@
 // zs_device.hpp — device-side data layout and primitives of the MI355X zombsole engine.
 //
-// Layout in HBM (N envs, E = A + P + Z entity slots, O obstacles, W x H map):
+// Layout in HBM (N envs, E = A + P + Z entity slots, O obstacles, W x H map, DW = ceil(W*H/32)):
 //   * entity SoA, env-minor [slot][N]: pos (x | y << 16, int16 each), life (int32),
 //     weapon (u8), present (u8), serial (u32), order (u8 dict-order list)
-//       -> a wave of 64 envs touching the same slot issues one 256-B coalesced access.
+//       -> lanes touching the same slot of consecutive envs issue coalesced accesses.
 //   * per-env scalars [k][N] (World.t, deaths, zombie_deaths, ...), agent tracker [a][N].
-//   * env-major per-env blocks (each lane walks its own env):
-//       occ   [N][occ_stride] u8   cell -> entity slot + 1   (World.things for entities)
-//       dead  [N][DW] u32          dead-body decoration bitmap
+//   * env-major per-env blocks (a lane group walks its own env):
+//       occ_bits [N][DW] u32       occupancy bitmap: cell holds an entity or a present obstacle
+//       dead     [N][DW] u32       dead-body decoration bitmap
 //       obstacle hp [N][O] int32, present / nonpos bitmaps [N][OW] u32
 //       MT19937 ring [N][2][624] u32 (current block + precomputed next block)
-//   * static, shared by all envs: cellmap (cell -> obstacle index), objective bitmap,
-//     obstacle xy/kind, spawn lists.
+//   * static, shared by all envs: cellmap (cell -> obstacle index), obstacle occupancy bitmap,
+//     objective bitmap, obstacle xy/kind, spawn lists.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -38,12 +38,15 @@ enum {
 
 struct Dev {
     int N, W, H, O, A, P, Z, E, OW, DW, ncand, nps, nzs, nobj;
-    int occ_stride;
+    int rw_cap;      // RNG window words staged in LDS per env (tick kernel)
+    int rw_step;     // words prefetched for a plain step (resets prefetch rw_cap)
+    int cand_cap;    // spawn-candidate entries staged in LDS per env (0 = global scratch)
     int rules, reward_mode, obs_scope, obs_enc, obs_w, obs_dtype, max_steps;
     int initial_zombies, minimum_zombies;
     uint32_t flags;
     // static
     const int16_t* cellmap;
+    const uint32_t* obstbits;  // static obstacle occupancy bitmap [DW]
     const uint32_t* objbits;
     const int32_t* obst_xy;  // packed x | y << 16
     const uint8_t* obst_kind;
@@ -65,7 +68,7 @@ struct Dev {
     int32_t* obst_hp;
     uint32_t* obst_present;
     uint32_t* obst_nonpos;
-    uint8_t* occ;
+    uint32_t* occ_bits;
     uint32_t* dead;
     uint32_t* ring;
     uint32_t* rngst;
@@ -108,37 +111,21 @@ __device__ inline void mt_twist_serial(uint32_t* dst, const uint32_t* src) {
     }
 }
 
-struct Rng {
-    uint32_t* ring;  // this env's 1248 words
-    uint32_t st;
-};
+__device__ __forceinline__ uint32_t st_pack(uint32_t off, uint32_t slot, uint32_t ready) {
+    return off | (slot << 10) | (ready << 11);
+}
 
-__device__ __forceinline__ uint32_t rng_u32(Rng& r) {
-    uint32_t off = r.st & 1023u, slot = (r.st >> 10) & 1u, ready = (r.st >> 11) & 1u;
-    if (off >= ZS_MT_N) {
-        if (!ready) mt_twist_serial(r.ring + (slot ^ 1u) * ZS_MT_N, r.ring + slot * ZS_MT_N);
+// ring state after consuming n more words from st (n <= 624; when the words cross into the
+// other slot that slot held the next block, i.e. st was `ready`)
+__device__ __forceinline__ uint32_t st_advance(uint32_t st, uint32_t n) {
+    uint32_t off = (st & 1023u) + n, slot = (st >> 10) & 1u, ready = (st >> 11) & 1u;
+    if (off > ZS_MT_N) {
         slot ^= 1u;
-        off = 0;
+        off -= ZS_MT_N;
         ready = 0;
     }
-    uint32_t y = r.ring[slot * ZS_MT_N + off];
-    r.st = (off + 1) | (slot << 10) | (ready << 11);
-    return mt_temper(y);
+    return st_pack(off, slot, ready);
 }
-
-// Random._randbelow_with_getrandbits (random.py:239-249); getrandbits(k<=32) = u32 >> (32-k)
-__device__ __forceinline__ int rng_below(Rng& r, int n) {
-    if (n <= 0) return 0;
-    int k = 32 - __clz(n);
-    uint32_t v;
-    do {
-        v = rng_u32(r) >> (32 - k);
-    } while (v >= (uint32_t)n);
-    return (int)v;
-}
-
-// randint(a, b) (random.py:366-370)
-__device__ __forceinline__ int rng_int(Rng& r, int a, int b) { return a + rng_below(r, b - a + 1); }
 
 // ---------------------------------------------------------------------------
 // weapons (weapons.py:18-25) with the sqrt range tests as exact integer d^2

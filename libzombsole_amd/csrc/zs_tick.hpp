@@ -1,0 +1,978 @@
+// zs_tick.hpp — the step kernel (k_tick): one env per group of G lanes, state staged in LDS.
+//
+// A tick of the reference is strictly sequential per env (World.step, core.py:72-78: decide
+// in dict order -> random.shuffle -> execute one by one -> clean dead things), followed by the
+// env glue (rewards, zombie respawn, rules).  Mapping to CDNA4:
+//   * a 64-lane wave holds NE = 64/G envs; every env's hot state sits in LDS for the whole
+//     tick: occupancy bitmap (1 bit per cell), entity table, dict-order list, a window of
+//     pre-tempered MT19937 words and the spawn-candidate list, so the serial chain issues no
+//     dependent global loads;
+//   * the G lanes of an env stage state in/out and take the decisions in parallel (every
+//     decision reads start-of-tick state only; the few RNG-consuming ones — wandering zombies,
+//     hamster, randoman — are deferred to the leader and taken in dict order);
+//   * the leader lane runs the order-dependent part: shuffle, execution, cleanup, rewards,
+//     respawn, rules;
+//   * at the end the wave twists, cooperatively, the next MT block of every env that crossed one.
+// The sqrt range tests of the reference are replaced by exact integer d^2 tests.
+#pragma once
+#include "zs_device.hpp"
+
+#define NOTHING ((int)0x80000000)
+
+enum { K_NONE = 0, K_MOVE = 1, K_ATTACK = 2, K_HEAL = 3, K_DEFER = 4 };
+enum { MODE_STEP = 0, MODE_RESET = 1 };
+
+// adjacent_positions order (utils.py:34-44)
+__constant__ int c_adj_dx[4] = {0, 0, 1, -1};
+__constant__ int c_adj_dy[4] = {1, -1, 0, 0};
+
+// LDS footprint of one workgroup (host and device agree on this layout)
+struct TickLayout {
+    int ne;                                  // envs per workgroup
+    int off_lst, off_bm, off_rw, off_cand;   // byte offsets
+    int off_pos, off_life, off_tgt;
+    int off_weap, off_pres, off_order, off_rank, off_kind, off_perm, off_moved;
+    int bytes;
+};
+
+__host__ __device__ inline TickLayout tick_layout(int ne, int E, int DW, int rw_cap, int cand_cap) {
+    TickLayout L;
+    L.ne = ne;
+    int o = 0;
+    L.off_lst = o;
+    o += ne * 4;
+    int region = o;
+    L.off_bm = o;
+    o += DW * ne * 4;
+    L.off_rw = o;
+    o += rw_cap * ne * 4;
+    L.off_pos = o;
+    o += E * ne * 4;
+    L.off_life = o;
+    o += E * ne * 4;
+    L.off_tgt = o;
+    o += E * ne * 4;
+    L.off_cand = o;
+    o += ((cand_cap * ne * 2 + 3) / 4) * 4;
+    L.off_weap = o;
+    o += E * ne;
+    L.off_pres = o;
+    o += E * ne;
+    L.off_order = o;
+    o += E * ne;
+    L.off_rank = o;
+    o += E * ne;
+    L.off_kind = o;
+    o += E * ne;
+    L.off_perm = o;
+    o += E * ne;
+    L.off_moved = o;
+    o += E * ne;
+    o = ((o + 15) / 16) * 16;
+    // the MT twist buffer (2 x 624 words) aliases the per-env region after state is stored
+    if (o - region < 2 * ZS_MT_N * 4) o = region + 2 * ZS_MT_N * 4;
+    L.bytes = o;
+    return L;
+}
+
+// one env as seen by one lane of its group
+struct Grp {
+    int e, g, j, ne;
+    uint32_t* bm;
+    uint32_t* rw;
+    uint16_t* cand;
+    int32_t* lpos;
+    int32_t* llife;
+    int32_t* ltgt;
+    uint8_t* lweap;
+    uint8_t* lpres;
+    uint8_t* lorder;
+    uint8_t* lrank;
+    uint8_t* lkind;
+    uint8_t* lperm;
+    uint8_t* lmoved;
+    // leader registers
+    uint32_t st0;  // ring state at the start of the LDS window
+    int wpos, wlen;
+    int n_order, t, deaths, zd, epsteps, prevzd, serial, odirty;
+};
+
+#define IX(c, k) ((k) * (c).ne + (c).g)
+#define LP(c, s) (c).lpos[IX(c, s)]
+#define LL(c, s) (c).llife[IX(c, s)]
+#define LT(c, s) (c).ltgt[IX(c, s)]
+#define LW(c, s) (c).lweap[IX(c, s)]
+#define LPR(c, s) (c).lpres[IX(c, s)]
+#define LO(c, s) (c).lorder[IX(c, s)]
+#define LR(c, s) (c).lrank[IX(c, s)]
+#define LK(c, s) (c).lkind[IX(c, s)]
+#define LPE(c, s) (c).lperm[IX(c, s)]
+#define LM(c, s) (c).lmoved[IX(c, s)]
+
+// ---------------------------------------------------------------------------
+// RNG: the leader draws pre-tempered words from the LDS window; when it runs dry it reloads
+// the next rw_cap words from the ring by itself (twisting serially if the ring is behind).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void rng_reload(const Dev& d, Grp& c) {
+    uint32_t st = st_advance(c.st0, c.wlen);
+    uint32_t off = st & 1023u, slot = (st >> 10) & 1u, ready = (st >> 11) & 1u;
+    uint32_t* ring = d.ring + (size_t)c.e * ZS_RING_WORDS;
+    if (off >= ZS_MT_N) {
+        if (!ready) mt_twist_serial(ring + (slot ^ 1u) * ZS_MT_N, ring + slot * ZS_MT_N);
+        slot ^= 1u;
+        off = 0;
+        ready = 0;
+    }
+    int n = d.rw_cap;
+    if ((int)off + n > ZS_MT_N && !ready) {
+        mt_twist_serial(ring + (slot ^ 1u) * ZS_MT_N, ring + slot * ZS_MT_N);
+        ready = 1;
+    }
+    for (int i = 0; i < n; i++) {
+        uint32_t q = off + i;
+        uint32_t w = q < ZS_MT_N ? ring[slot * ZS_MT_N + q] : ring[(slot ^ 1u) * ZS_MT_N + q - ZS_MT_N];
+        c.rw[IX(c, i)] = mt_temper(w);
+    }
+    c.st0 = st_pack(off, slot, ready);
+    c.wpos = 0;
+    c.wlen = n;
+}
+
+__device__ __forceinline__ uint32_t rng_u32(const Dev& d, Grp& c) {
+    if (c.wpos >= c.wlen) rng_reload(d, c);
+    return c.rw[IX(c, c.wpos++)];
+}
+
+// Random._randbelow_with_getrandbits (random.py:239-249); getrandbits(k<=32) = u32 >> (32-k)
+__device__ __forceinline__ int rng_below(const Dev& d, Grp& c, int n) {
+    if (n <= 0) return 0;
+    int k = 32 - __clz(n);
+    uint32_t v;
+    do {
+        v = rng_u32(d, c) >> (32 - k);
+    } while (v >= (uint32_t)n);
+    return (int)v;
+}
+
+// randint(a, b) (random.py:366-370)
+__device__ __forceinline__ int rng_int(const Dev& d, Grp& c, int a, int b) { return a + rng_below(d, c, b - a + 1); }
+
+// ---------------------------------------------------------------------------
+// World.things queries on the LDS image
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool in_bounds(const Dev& d, int x, int y) { return x >= 0 && y >= 0 && x < d.W && y < d.H; }
+
+__device__ __forceinline__ bool bm_test(const Grp& c, int cell) { return (c.bm[IX(c, cell >> 5)] >> (cell & 31)) & 1u; }
+__device__ __forceinline__ void bm_set(Grp& c, int cell) { c.bm[IX(c, cell >> 5)] |= 1u << (cell & 31); }
+__device__ __forceinline__ void bm_clr(Grp& c, int cell) { c.bm[IX(c, cell >> 5)] &= ~(1u << (cell & 31)); }
+
+// things.get(position) is not None
+__device__ __forceinline__ bool occupied(const Dev& d, const Grp& c, int x, int y) {
+    return in_bounds(d, x, y) && bm_test(c, y * d.W + x);
+}
+
+// things.get(position): entity slot (>= 0), obstacle -(index+1), or NOTHING
+__device__ int thing_at(const Dev& d, const Grp& c, int x, int y) {
+    if (!occupied(d, c, x, y)) return NOTHING;
+    int32_t pk = pack_xy(x, y);
+    for (int s = 0; s < d.E; s++)
+        if (LPR(c, s) && LP(c, s) == pk) return s;
+    return -((int)d.cellmap[y * d.W + x] + 1);
+}
+
+__device__ __forceinline__ int32_t target_pos(const Dev& d, const Grp& c, int tgt) {
+    return tgt >= 0 ? LP(c, tgt) : d.obst_xy[-tgt - 1];
+}
+__device__ __forceinline__ int target_maxlife(const Dev& d, int tgt) {
+    if (tgt >= 0) return 100;  // Zombie / Player / Agent MAX_LIFE (things.py:62,109)
+    return d.obst_kind[-tgt - 1] == ZS_THING_BOX ? 10 : 200;
+}
+__device__ __forceinline__ int target_life(const Dev& d, const Grp& c, int tgt) {
+    return tgt >= 0 ? LL(c, tgt) : d.obst_hp[(size_t)c.e * d.O + (-tgt - 1)];
+}
+__device__ __forceinline__ void set_target_life(const Dev& d, Grp& c, int tgt, int v) {
+    if (tgt >= 0) {
+        LL(c, tgt) = v;
+        return;
+    }
+    int oi = -tgt - 1;
+    d.obst_hp[(size_t)c.e * d.O + oi] = v;
+    uint32_t* w = &d.obst_nonpos[(size_t)c.e * d.OW + (oi >> 5)];
+    uint32_t bit = 1u << (oi & 31);
+    *w = v <= 0 ? (*w | bit) : (*w & ~bit);
+    c.odirty = 1;
+}
+
+// closest(...) over present slots [s0, s1) \ {excl}: the first minimum in dict order
+__device__ __forceinline__ int closest_in(const Dev& d, const Grp& c, int fx, int fy, int s0, int s1, int excl) {
+    int best = -1, bd = 0, br = 0;
+    for (int s = s0; s < s1; s++) {
+        if (!LPR(c, s) || s == excl) continue;
+        int p = LP(c, s);
+        int dd = d2(fx, fy, unpack_x(p), unpack_y(p));
+        int rk = LR(c, s);
+        if (best < 0 || dd < bd || (dd == bd && rk < br)) {
+            best = s;
+            bd = dd;
+            br = rk;
+        }
+    }
+    return best;
+}
+
+// ---------------------------------------------------------------------------
+// spawning (leader)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void place(const Dev& d, Grp& c, int s, int cell) {
+    LP(c, s) = pack_xy(cell % d.W, cell / d.W);
+    LPR(c, s) = 1;
+    bm_set(c, cell);
+    LO(c, c.n_order) = (uint8_t)s;
+    c.n_order++;
+    d.serial[(size_t)s * d.N + c.e] = (uint32_t)(++c.serial);
+}
+
+// World.spawn_in_random (core.py:40-66) for the k slots listed in LM(c, 0..k).  Only the first
+// k Fisher-Yates iterations can move the k cells that get popped; the rest are replayed for
+// their RNG draws alone.
+__device__ int spawn_in_random(const Dev& d, Grp& c, int k, const int32_t* list, int nlist, int fail_if_cant) {
+    const int total = nlist ? nlist : d.W * d.H;
+    const bool lds = total <= d.cand_cap;
+    int32_t* gc = d.cand + (size_t)c.e * d.ncand;
+#define CGET(i) (lds ? (int)c.cand[IX(c, i)] : gc[i])
+#define CSET(i, v)                              \
+    do {                                        \
+        if (lds) c.cand[IX(c, i)] = (uint16_t)(v); \
+        else gc[i] = (v);                       \
+    } while (0)
+    int n = 0;
+    if (nlist == 0) {  // every cell, x-major (core.py:45-47)
+        for (int x = 0; x < d.W; x++)
+            for (int y = 0; y < d.H; y++) {
+                int cell = y * d.W + x;
+                if (!bm_test(c, cell)) {
+                    CSET(n, cell);
+                    n++;
+                }
+            }
+    } else {
+        for (int i = 0; i < nlist; i++) {
+            int32_t p = list[i];
+            int cell = unpack_y(p) * d.W + unpack_x(p);
+            if (!bm_test(c, cell)) {
+                CSET(n, cell);
+                n++;
+            }
+        }
+    }
+    int lim = n - k;
+    for (int i = n - 1; i >= 1; i--) {
+        int j = rng_below(d, c, i + 1);
+        if (i >= lim) {
+            int a = CGET(i), b = CGET(j);
+            CSET(i, b);
+            CSET(j, a);
+        }
+    }
+    for (int m = 0; m < k; m++) {
+        int s = LM(c, m);
+        if (m < n) {
+            place(d, c, s, CGET(n - 1 - m));
+        } else {
+            if (fail_if_cant) return ZS_ENOSPACE;
+            for (int q = m; q < k; q++) LPR(c, LM(c, q)) = 0;  // dropped (game.py:192-194)
+            return ZS_OK;
+        }
+    }
+#undef CGET
+#undef CSET
+    return ZS_OK;
+}
+
+// Game.spawn_zombies(count) into free zombie slots (game.py:189-194); every Zombie() draws
+// randint(50, 100) before the spawn shuffle (things.py:61-68).
+__device__ void spawn_zombies(const Dev& d, Grp& c, int count) {
+    int k = 0;
+    for (int s = d.A + d.P; s < d.E && k < count; s++)
+        if (!LPR(c, s)) LM(c, k++) = (uint8_t)s;
+    for (int i = 0; i < k; i++) {
+        int s = LM(c, i);
+        LL(c, s) = rng_int(d, c, 50, 100);
+        LW(c, s) = ZS_WEAPON_CLAWS;
+    }
+    spawn_in_random(d, c, k, d.zspawn, d.nzs, 0);
+}
+
+// Game.__initialize_world__ (game.py:151-169) after the group has laid the map obstacles into
+// the bitmap and cleared the entity table; plus the reward-tracker / env.agents reset.
+__device__ int env_reset_leader(const Dev& d, Grp& c) {
+    c.t = -1;
+    c.deaths = 0;
+    c.zd = 0;
+    c.n_order = 0;
+    // the map's obstacles re-enter the world with their carried-over HP (game.py:154-155)
+    int any_nonpos = 0;
+    for (int w = 0; w < d.OW; w++) {
+        int nb = min(32, d.O - 32 * w);
+        d.obst_present[(size_t)c.e * d.OW + w] = nb == 32 ? 0xffffffffu : ((1u << nb) - 1u);
+        any_nonpos |= d.obst_nonpos[(size_t)c.e * d.OW + w] != 0;
+    }
+    c.odirty = any_nonpos;
+    // players: Player() picks a random weapon unless its module gives one (things.py:113-116)
+    for (int p = 0; p < d.P; p++) {
+        int s = d.A + p, w;
+        int bt = d.bot_types[p];
+        if (bt == ZS_BOT_TERMINATOR) w = ZS_WEAPON_SHOTGUN;  // terminator.py:40-42
+        else if (bt == ZS_BOT_SNIPER) w = ZS_WEAPON_RIFLE;   // sniper.py:22-24
+        else {                                               // choice([Gun, Shotgun, Rifle, Knife, Axe])
+            int k = rng_below(d, c, 5);
+            w = k == 0 ? ZS_WEAPON_GUN : k == 1 ? ZS_WEAPON_SHOTGUN : k == 2 ? ZS_WEAPON_RIFLE : k == 3 ? ZS_WEAPON_KNIFE : ZS_WEAPON_AXE;
+        }
+        LW(c, s) = (uint8_t)w;
+        LL(c, s) = 100;
+    }
+    // agents: WeaponFactory.create_player_weapon (weapons.py:28-45)
+    for (int a = 0; a < d.A; a++) {
+        int w = d.agent_weapons[a];
+        if (w == ZS_WEAPON_RANDOM) {  // choice([Knife(), Axe(), Gun(), Rifle(), Shotgun()])
+            int k = rng_below(d, c, 5);
+            w = k == 0 ? ZS_WEAPON_KNIFE : k == 1 ? ZS_WEAPON_AXE : k == 2 ? ZS_WEAPON_GUN : k == 3 ? ZS_WEAPON_RIFLE : ZS_WEAPON_SHOTGUN;
+        }
+        LW(c, a) = (uint8_t)w;
+        LL(c, a) = 100;
+    }
+    for (int p = 0; p < d.P; p++) LM(c, p) = (uint8_t)(d.A + p);
+    int rc = spawn_in_random(d, c, d.P, d.pspawn, d.nps, 1);
+    if (rc) return rc;
+    for (int a = 0; a < d.A; a++) LM(c, a) = (uint8_t)a;
+    rc = spawn_in_random(d, c, d.A, d.pspawn, d.nps, 1);
+    if (rc) return rc;
+    spawn_zombies(d, c, d.initial_zombies);
+    c.prevzd = 0;
+    for (int a = 0; a < d.A; a++) {
+        d.prev_life[(size_t)a * d.N + c.e] = LL(c, a);
+        d.listed[(size_t)a * d.N + c.e] = 1;
+    }
+    c.epsteps = 0;
+    return ZS_OK;
+}
+
+// ---------------------------------------------------------------------------
+// decisions on the start-of-tick state.  With rng == false a decision that would draw
+// from the RNG returns K_DEFER instead (the leader re-takes it in dict order).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int pick_bit(int mask, int j) {  // j-th set bit (ascending)
+    int k = 0;
+    for (; k < 4; k++)
+        if ((mask >> k) & 1) {
+            if (j == 0) break;
+            j--;
+        }
+    return k;
+}
+
+// Zombie.next_step (things.py:70-105)
+__device__ void decide_zombie(const Dev& d, Grp& c, int s, bool rng, int& kind, int& tgt) {
+    int p = LP(c, s), x = unpack_x(p), y = unpack_y(p);
+    int freemask = 0;
+    for (int k = 0; k < 4; k++)  // possible_moves: not in things, not bounds-checked (utils.py:47-52)
+        if (!occupied(d, c, x + c_adj_dx[k], y + c_adj_dy[k])) freemask |= 1 << k;
+    int h = closest_in(d, c, x, y, 0, d.A + d.P, -1);
+    if (h >= 0) {
+        int hp = LP(c, h), hx = unpack_x(hp), hy = unpack_y(hp);
+        if (d2(x, y, hx, hy) <= 2) {  // distance < 1.5
+            kind = K_ATTACK;
+            tgt = h;
+            return;
+        }
+        if (freemask) {  // closest(target, positions)
+            int bk = -1, bd = 0;
+            for (int k = 0; k < 4; k++) {
+                if (!((freemask >> k) & 1)) continue;
+                int dd = d2(hx, hy, x + c_adj_dx[k], y + c_adj_dy[k]);
+                if (bk < 0 || dd < bd) {
+                    bk = k;
+                    bd = dd;
+                }
+            }
+            kind = K_MOVE;
+            tgt = pack_xy(x + c_adj_dx[bk], y + c_adj_dy[bk]);
+            return;
+        }
+        // blocked: first Box/Wall in sort_by_distance(target, adjacent_positions(self))
+        int dd[4];
+        for (int k = 0; k < 4; k++) dd[k] = d2(hx, hy, x + c_adj_dx[k], y + c_adj_dy[k]);
+        int used = 0;
+        for (int r = 0; r < 4; r++) {
+            int bk = -1;
+            for (int k = 0; k < 4; k++)
+                if (!((used >> k) & 1) && (bk < 0 || dd[k] < dd[bk])) bk = k;
+            used |= 1 << bk;
+            int th = thing_at(d, c, x + c_adj_dx[bk], y + c_adj_dy[bk]);
+            if (th != NOTHING && th < 0) {
+                kind = K_ATTACK;
+                tgt = th;
+                return;
+            }
+        }
+        kind = K_NONE;
+        return;
+    }
+    if (freemask) {  // wander: random.choice(positions)
+        if (!rng) {
+            kind = K_DEFER;
+            return;
+        }
+        int k = pick_bit(freemask, rng_below(d, c, __popc(freemask)));
+        kind = K_MOVE;
+        tgt = pack_xy(x + c_adj_dx[k], y + c_adj_dy[k]);
+        return;
+    }
+    kind = K_NONE;
+}
+
+__device__ __forceinline__ int clamp16(int v) { return v < -16384 ? -16384 : (v > 16383 ? 16383 : v); }
+
+// Agent.next_step (players/agent.py:28-96) on the action triple
+__device__ void decide_agent(const Dev& d, const Grp& c, int s, const int32_t* act, int& kind, int& tgt) {
+    int p = LP(c, s), x = unpack_x(p), y = unpack_y(p);
+    int ak = act[0], dx = clamp16(act[1]), dy = clamp16(act[2]);
+    kind = K_NONE;
+    if (ak == ZS_ACT_MOVE) {
+        kind = K_MOVE;
+        tgt = pack_xy(x + dx, y + dy);
+    } else if (ak == ZS_ACT_ATTACK_CLOSEST) {
+        int z = closest_in(d, c, x, y, d.A + d.P, d.E, -1);
+        if (z >= 0) {
+            kind = K_ATTACK;
+            tgt = z;
+        }
+    } else if (ak == ZS_ACT_ATTACK) {
+        int th = thing_at(d, c, x + dx, y + dy);
+        if (th != NOTHING) {
+            kind = K_ATTACK;
+            tgt = th;
+        }
+    } else if (ak == ZS_ACT_HEAL) {
+        if (dx == 0 && dy == 0) {
+            kind = K_HEAL;
+            tgt = s;
+        } else {
+            int th = thing_at(d, c, x + dx, y + dy);
+            if (th != NOTHING && (th < 0 || th < d.A + d.P)) {  // Player, Box or Wall; never a Zombie
+                kind = K_HEAL;
+                tgt = th;
+            }
+        }
+    } else if (ak == ZS_ACT_HEAL_CLOSEST) {
+        int q = closest_in(d, c, x, y, 0, d.A + d.P, s);
+        kind = K_HEAL;
+        tgt = q >= 0 ? q : s;
+    }
+}
+
+// scripted bots (players/{terminator,sniper,troll,hamster,randoman}.py)
+__device__ void decide_bot(const Dev& d, Grp& c, int s, bool rng, int& kind, int& tgt) {
+    int p = LP(c, s), x = unpack_x(p), y = unpack_y(p);
+    int bt = d.bot_types[s - d.A];
+    kind = K_NONE;
+    if (bt == ZS_BOT_TERMINATOR) {  // terminator.py:9-37
+        int z = closest_in(d, c, x, y, d.A + d.P, d.E, -1);
+        if (z < 0) {
+            kind = K_HEAL;
+            tgt = s;
+            return;
+        }
+        int zp = LP(c, z), zx = unpack_x(zp), zy = unpack_y(zp);
+        if (d2(x, y, zx, zy) > weapon_r2(LW(c, s))) {
+            int bk = 0, bd = d2(zx, zy, x + c_adj_dx[0], y + c_adj_dy[0]);
+            for (int k = 1; k < 4; k++) {
+                int dd = d2(zx, zy, x + c_adj_dx[k], y + c_adj_dy[k]);
+                if (dd < bd) {
+                    bk = k;
+                    bd = dd;
+                }
+            }
+            int bx = x + c_adj_dx[bk], by = y + c_adj_dy[bk];
+            int th = thing_at(d, c, bx, by);
+            if (th != NOTHING) {
+                kind = (th >= 0 && th < d.A + d.P) ? K_HEAL : K_ATTACK;
+                tgt = th;
+            } else {
+                kind = K_MOVE;
+                tgt = pack_xy(bx, by);
+            }
+        } else {
+            kind = K_ATTACK;
+            tgt = z;
+        }
+    } else if (bt == ZS_BOT_SNIPER) {  // sniper.py:9-19
+        int z = closest_in(d, c, x, y, d.A + d.P, d.E, -1);
+        if (z >= 0) {
+            kind = K_ATTACK;
+            tgt = z;
+        }
+    } else if (bt == ZS_BOT_TROLL) {  // troll.py:10-12
+        kind = K_HEAL;
+        tgt = s;
+    } else if (bt == ZS_BOT_HAMSTER) {  // hamster.py:10-14
+        int freemask = 0;
+        for (int k = 0; k < 4; k++)
+            if (!occupied(d, c, x + c_adj_dx[k], y + c_adj_dy[k])) freemask |= 1 << k;
+        if (freemask) {
+            if (!rng) {
+                kind = K_DEFER;
+                return;
+            }
+            int k = pick_bit(freemask, rng_below(d, c, __popc(freemask)));
+            kind = K_MOVE;
+            tgt = pack_xy(x + c_adj_dx[k], y + c_adj_dy[k]);
+        }
+    } else if (bt == ZS_BOT_RANDOMAN) {  // randoman.py:9-21
+        if (!rng) {
+            kind = K_DEFER;
+            return;
+        }
+        int a = rng_below(d, c, 3);  // choice(('move', 'attack', 'heal'))
+        if (a != 0) {
+            // choice(list(things.values())): present obstacles (map order), then dynamic things
+            const uint32_t* pres = d.obst_present + (size_t)c.e * d.OW;
+            int npo = 0;
+            for (int w = 0; w < d.OW; w++) npo += __popc(pres[w]);
+            int k = rng_below(d, c, npo + c.n_order);
+            if (k < npo) {
+                int w = 0;
+                while (k >= (int)__popc(pres[w])) {
+                    k -= __popc(pres[w]);
+                    w++;
+                }
+                uint32_t m = pres[w];
+                for (; k > 0; k--) m &= m - 1;
+                tgt = -(32 * w + __ffs(m) - 1 + 1);
+            } else {
+                tgt = LO(c, k - npo);
+            }
+            kind = a == 1 ? K_ATTACK : K_HEAL;
+        } else {
+            int axis = rng_below(d, c, 2);            // target[choice((0, 1))]
+            int delta = rng_below(d, c, 2) ? 1 : -1;  //   += choice((-1, 1))
+            kind = K_MOVE;
+            tgt = axis == 0 ? pack_xy(x + delta, y) : pack_xy(x, y + delta);
+        }
+    }
+}
+
+__device__ __forceinline__ void decide(const Dev& d, Grp& c, int s, const int32_t* actions, bool rng, int& kind,
+                                       int& tgt) {
+    kind = K_NONE;
+    tgt = 0;
+    if (s < d.A) decide_agent(d, c, s, actions + ((size_t)c.e * d.A + s) * 3, kind, tgt);
+    else if (s < d.A + d.P) decide_bot(d, c, s, rng, kind, tgt);
+    else decide_zombie(d, c, s, rng, kind, tgt);
+}
+
+// ---------------------------------------------------------------------------
+// rules (rules/{extermination,survival,safehouse,evacuation}.py)
+// ---------------------------------------------------------------------------
+__device__ void rules_check(const Dev& d, const Grp& c, int& ended, int& won) {
+    int pa = 0;  // Rules.players_alive (rules.py:6-11)
+    for (int s = 0; s < d.A + d.P; s++) pa |= LL(c, s) > 0;
+    if (d.rules == ZS_RULES_EXTERMINATION) {
+        int za = 0;
+        for (int s = d.A + d.P; s < d.E; s++) za |= LPR(c, s) && LL(c, s) > 0;
+        ended = !pa || !za;
+        won = pa;
+    } else if (d.rules == ZS_RULES_SURVIVAL) {
+        ended = !pa;
+        won = pa;
+    } else if (d.rules == ZS_RULES_SAFEHOUSE) {
+        if (pa) {
+            int all_in = 1;
+            for (int s = 0; s < d.A + d.P; s++) {
+                if (LL(c, s) <= 0) continue;
+                int p = LP(c, s), cell = unpack_y(p) * d.W + unpack_x(p);
+                if (!((d.objbits[cell >> 5] >> (cell & 31)) & 1u)) all_in = 0;
+            }
+            ended = all_in;
+        } else {
+            ended = 1;
+        }
+        won = pa;
+    } else {  // evacuation: alive >= half of the team and alive players 4-connected
+        int total = d.A + d.P;
+        unsigned long long alive = 0;
+        int na = 0;
+        for (int s = 0; s < total; s++)
+            if (LL(c, s) > 0) {
+                alive |= 1ull << s;
+                na++;
+            }
+        int half = 2 * na >= total;
+        if (half) {
+            int first = -1;  // alive_players[0]: first alive bot, else first alive agent
+            for (int s = d.A; s < total && first < 0; s++)
+                if ((alive >> s) & 1ull) first = s;
+            for (int s = 0; s < d.A && first < 0; s++)
+                if ((alive >> s) & 1ull) first = s;
+            unsigned long long together = 0, frontier = 0;
+            if (first >= 0) together = frontier = 1ull << first;
+            while (frontier) {
+                int s = __ffsll((long long)frontier) - 1;
+                frontier &= frontier - 1;
+                int p = LP(c, s), x = unpack_x(p), y = unpack_y(p);
+                for (int q = 0; q < total; q++) {
+                    if (!((alive >> q) & 1ull) || ((together >> q) & 1ull)) continue;
+                    int pq = LP(c, q);
+                    int dx = unpack_x(pq) - x, dy = unpack_y(pq) - y;
+                    if ((dx == 0 && (dy == 1 || dy == -1)) || (dy == 0 && (dx == 1 || dx == -1))) {
+                        together |= 1ull << q;
+                        frontier |= 1ull << q;
+                    }
+                }
+            }
+            ended = __popcll(together) == na;
+        } else {
+            ended = 1;
+        }
+        won = half;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// leader: the order-dependent rest of the tick (gym_env.py:99-145 / multiagent_env.py:111-171)
+// ---------------------------------------------------------------------------
+__device__ void env_step_leader(const Dev& d, Grp& c, const int32_t* actions, double* rew, uint8_t* done_out,
+                                uint8_t* trunc_out, uint8_t* listed_out) {
+    const int A = d.A, E = d.E, N = d.N;
+    // World.get_actions (core.py:80-101): deferred (RNG-drawing) decisions in dict order
+    int nact = 0;
+    for (int k = 0; k < c.n_order; k++) {
+        int s = LO(c, k);
+        if (LK(c, s) == K_DEFER) {
+            int kind, tgt;
+            decide(d, c, s, actions, true, kind, tgt);
+            LK(c, s) = (uint8_t)kind;
+            LT(c, s) = tgt;
+        }
+        if (LK(c, s) != K_NONE) LPE(c, nact++) = (uint8_t)s;
+    }
+    // random.shuffle(actions) (core.py:76)
+    for (int i = nact - 1; i >= 1; i--) {
+        int j = rng_below(d, c, i + 1);
+        uint8_t tmp = LPE(c, i);
+        LPE(c, i) = LPE(c, j);
+        LPE(c, j) = tmp;
+    }
+    // execute_actions (core.py:103-119)
+    int nmoved = 0;
+    for (int i = 0; i < nact; i++) {
+        int s = LPE(c, i), kind = LK(c, s), tgt = LT(c, s);
+        int p = LP(c, s), x = unpack_x(p), y = unpack_y(p);
+        if (kind == K_MOVE) {  // thing_move (core.py:140-166)
+            int tx = unpack_x(tgt), ty = unpack_y(tgt);
+            if (in_bounds(d, tx, ty) && !bm_test(c, ty * d.W + tx) && d2(x, y, tx, ty) <= 1) {
+                bm_clr(c, y * d.W + x);
+                bm_set(c, ty * d.W + tx);
+                LP(c, s) = tgt;
+                LM(c, nmoved++) = (uint8_t)s;
+                LR(c, s) = 255;  // re-inserted at the end of the dict
+            }
+        } else if (kind == K_ATTACK) {  // thing_attack (core.py:168-184)
+            int tp = target_pos(d, c, tgt);
+            int w = LW(c, s);
+            if (d2(x, y, unpack_x(tp), unpack_y(tp)) <= weapon_r2(w)) {
+                int dmg = rng_int(d, c, weapon_lo(w), weapon_hi(w));
+                set_target_life(d, c, tgt, target_life(d, c, tgt) - dmg);
+            }
+        } else {  // thing_heal (core.py:186-202), HEALING_RANGE = 3
+            int tp = target_pos(d, c, tgt);
+            if (d2(x, y, unpack_x(tp), unpack_y(tp)) <= 9) {
+                int ml = target_maxlife(d, tgt);
+                int hl = rng_int(d, c, ml / 10, ml / 4);
+                set_target_life(d, c, tgt, min(ml, target_life(d, c, tgt) + hl));
+            }
+        }
+    }
+    {  // dict order after the tick's moves: unmoved in old order, then movers in execution order
+        int m = 0;
+        for (int k = 0; k < c.n_order; k++) {
+            int s = LO(c, k);
+            if (LR(c, s) != 255) LO(c, m++) = (uint8_t)s;
+        }
+        for (int j = 0; j < nmoved; j++) LO(c, m++) = LM(c, j);
+    }
+    // clean_dead_things (core.py:121-138)
+    if (c.odirty) {
+        for (int w = 0; w < d.OW; w++) {
+            uint32_t* pw = &d.obst_present[(size_t)c.e * d.OW + w];
+            uint32_t dead = *pw & d.obst_nonpos[(size_t)c.e * d.OW + w];
+            if (dead) {
+                *pw &= ~dead;
+                c.deaths += __popc(dead);
+                while (dead) {
+                    int oi = 32 * w + __ffs(dead) - 1;
+                    dead &= dead - 1;
+                    int32_t op = d.obst_xy[oi];
+                    bm_clr(c, unpack_y(op) * d.W + unpack_x(op));
+                }
+            }
+        }
+        c.odirty = 0;
+    }
+    {
+        uint32_t* deadbits = d.dead + (size_t)c.e * d.DW;
+        int m = 0;
+        for (int k = 0; k < c.n_order; k++) {
+            int s = LO(c, k);
+            if (LL(c, s) <= 0) {
+                int p = LP(c, s), cell = unpack_y(p) * d.W + unpack_x(p);
+                deadbits[cell >> 5] |= 1u << (cell & 31);  // DeadBody decoration
+                bm_clr(c, cell);
+                LPR(c, s) = 0;
+                c.deaths++;
+                if (s >= A + d.P) c.zd++;
+            } else {
+                LO(c, m++) = (uint8_t)s;
+            }
+        }
+        c.n_order = m;
+    }
+    // reward_tracker.update (gym/reward.py:30-35, 77-86)
+    double rs = 0.0;
+    if (d.reward_mode == ZS_REWARD_SINGLE) {
+        long long sp = 0, sc = 0;
+        for (int a = 0; a < A; a++) {
+            sp += d.prev_life[(size_t)a * N + c.e];
+            sc += LL(c, a);
+        }
+        double prev = (double)c.prevzd + (double)sp / 100.0;
+        double cur = (double)c.zd + (double)sc / 100.0;
+        rs = cur - prev;
+    } else {
+        for (int a = 0; a < A; a++) {
+            double prev = (double)c.prevzd + (double)d.prev_life[(size_t)a * N + c.e] / 100.0;
+            double cur = (double)c.zd + (double)LL(c, a) / 100.0;
+            rew[(size_t)c.e * A + a] = cur - prev;
+        }
+    }
+    for (int a = 0; a < A; a++) d.prev_life[(size_t)a * N + c.e] = LL(c, a);
+    c.prevzd = c.zd;
+    // spawn_zombies_to_maintain_minimum (game.py:196-201)
+    {
+        int nz = 0;
+        for (int s = A + d.P; s < E; s++) nz += LPR(c, s);
+        if (nz < d.minimum_zombies) spawn_zombies(d, c, d.minimum_zombies - nz);
+    }
+    // rules and end-of-game reward (gym_env.py:130-141, gym/multiagent_env.py:143-162)
+    int ended, won, tr = 0;
+    rules_check(d, c, ended, won);
+    double end_reward = 0.0;
+    if (ended) {
+        end_reward = won ? 10.0 : -10.0;
+    } else {
+        int aa = 0;
+        for (int a = 0; a < A; a++) aa |= LL(c, a) > 0;
+        if (!aa) {
+            tr = 1;
+            end_reward = -10.0;
+        }
+    }
+    if (d.reward_mode == ZS_REWARD_SINGLE) {
+        if (ended || tr) rs += end_reward;
+        rew[c.e] = rs;
+        if (listed_out)
+            for (int a = 0; a < A; a++) listed_out[(size_t)c.e * A + a] = d.listed[(size_t)a * N + c.e];
+    } else {
+        for (int a = 0; a < A; a++) {
+            uint8_t was = d.listed[(size_t)a * N + c.e];
+            if (listed_out) listed_out[(size_t)c.e * A + a] = was;
+            double r = rew[(size_t)c.e * A + a];
+            if (!was) r = 0.0;
+            else if (LL(c, a) > 0) r = r + end_reward;
+            rew[(size_t)c.e * A + a] = r;
+            d.listed[(size_t)a * N + c.e] = LL(c, a) > 0;
+        }
+    }
+    c.epsteps++;
+    if (d.max_steps > 0 && c.epsteps >= d.max_steps) tr = 1;
+    done_out[c.e] = (uint8_t)ended;
+    trunc_out[c.e] = (uint8_t)tr;
+}
+
+// ---------------------------------------------------------------------------
+// wave-cooperative MT19937 refill: every env of the workgroup whose next block is not ready
+// gets it twisted by all 64 lanes (3 dependency phases over the 624-word block).
+// ---------------------------------------------------------------------------
+__device__ void coop_refill(const Dev& d, int base, int count, const uint32_t* lst, uint32_t* tw) {
+    const int tid = threadIdx.x, nt = blockDim.x;
+    for (int i = 0; i < count; i++) {
+        uint32_t st = lst[i];
+        if ((st >> 11) & 1u) continue;
+        uint32_t slot = (st >> 10) & 1u;
+        uint32_t* ring = d.ring + (size_t)(base + i) * ZS_RING_WORDS;
+        const uint32_t* src = ring + slot * ZS_MT_N;
+        uint32_t* dst = ring + (slot ^ 1u) * ZS_MT_N;
+        for (int k = tid; k < ZS_MT_N; k += nt) tw[k] = src[k];
+        __syncthreads();
+        uint32_t* nw = tw + ZS_MT_N;
+        for (int k = tid; k < ZS_MT_N - ZS_MT_M; k += nt) nw[k] = mt_f(tw[k], tw[k + 1], tw[k + ZS_MT_M]);
+        __syncthreads();
+        for (int k = (ZS_MT_N - ZS_MT_M) + tid; k < 2 * (ZS_MT_N - ZS_MT_M); k += nt)
+            nw[k] = mt_f(tw[k], tw[k + 1], nw[k + ZS_MT_M - ZS_MT_N]);
+        __syncthreads();
+        for (int k = 2 * (ZS_MT_N - ZS_MT_M) + tid; k < ZS_MT_N; k += nt)
+            nw[k] = mt_f(tw[k], k + 1 < ZS_MT_N ? tw[k + 1] : nw[0], nw[k + ZS_MT_M - ZS_MT_N]);
+        __syncthreads();
+        for (int k = tid; k < ZS_MT_N; k += nt) dst[k] = nw[k];
+        if (tid == 0) d.rngst[base + i] = st | (1u << 11);
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_tick: one workgroup = one wave = 64/G envs
+// ---------------------------------------------------------------------------
+template <int G>
+__global__ void __launch_bounds__(64) k_tick(Dev d, int mode, const uint8_t* mask, const int32_t* actions,
+                                             double* rew, uint8_t* done_out, uint8_t* trunc_out,
+                                             uint8_t* listed_out, uint8_t* reset_out, int* err_out) {
+    extern __shared__ __align__(16) uint8_t smem[];
+    constexpr int NE = 64 / G;
+    const int lane = threadIdx.x, g = lane / G, j = lane - g * G;
+    const int base = blockIdx.x * NE, e = base + g, N = d.N, E = d.E;
+    const bool active = e < N;
+    const bool leader = j == 0;
+    const TickLayout L = tick_layout(NE, E, d.DW, d.rw_cap, d.cand_cap);
+    uint32_t* lst = (uint32_t*)(smem + L.off_lst);
+    Grp c;
+    c.e = e;
+    c.g = g;
+    c.j = j;
+    c.ne = NE;
+    c.bm = (uint32_t*)(smem + L.off_bm);
+    c.rw = (uint32_t*)(smem + L.off_rw);
+    c.cand = (uint16_t*)(smem + L.off_cand);
+    c.lpos = (int32_t*)(smem + L.off_pos);
+    c.llife = (int32_t*)(smem + L.off_life);
+    c.ltgt = (int32_t*)(smem + L.off_tgt);
+    c.lweap = smem + L.off_weap;
+    c.lpres = smem + L.off_pres;
+    c.lorder = smem + L.off_order;
+    c.lrank = smem + L.off_rank;
+    c.lkind = smem + L.off_kind;
+    c.lperm = smem + L.off_perm;
+    c.lmoved = smem + L.off_moved;
+
+    int do_reset = 0, n_order = 0;
+    uint32_t st0 = 0;
+    int wlen = 0;
+    if (active) {
+        int needs_reset = d.scal[S_NEEDRESET * N + e];
+        do_reset = mode == MODE_RESET ? (mask == nullptr || mask[e]) : needs_reset;
+        n_order = d.scal[S_NORDER * N + e];
+        // stage the entity table
+        for (int s = j; s < E; s += G) {
+            LP(c, s) = d.pos[(size_t)s * N + e];
+            LL(c, s) = d.life[(size_t)s * N + e];
+            LW(c, s) = d.weapon[(size_t)s * N + e];
+            LPR(c, s) = do_reset ? 0 : d.present[(size_t)s * N + e];
+            LO(c, s) = d.order[(size_t)s * N + e];
+        }
+        // occupancy bitmap: persisted one, or the map's obstacles for a new World
+        const uint32_t* src = do_reset ? d.obstbits : d.occ_bits + (size_t)e * d.DW;
+        for (int w = j; w < d.DW; w += G) c.bm[IX(c, w)] = src[w];
+        if (do_reset)
+            for (int w = j; w < d.DW; w += G) d.dead[(size_t)e * d.DW + w] = 0;
+        // RNG window: the next words of this env's stream, tempered
+        uint32_t st = d.rngst[e];
+        uint32_t off = st & 1023u, slot = (st >> 10) & 1u, ready = (st >> 11) & 1u;
+        if (off >= ZS_MT_N && ready) {
+            slot ^= 1u;
+            off = 0;
+            ready = 0;
+        }
+        int maxw = off >= ZS_MT_N ? 0 : (ready ? d.rw_cap : min(d.rw_cap, ZS_MT_N - (int)off));
+        wlen = min(do_reset ? d.rw_cap : d.rw_step, maxw);
+        const uint32_t* ring = d.ring + (size_t)e * ZS_RING_WORDS;
+        for (int i = j; i < wlen; i += G) {
+            uint32_t q = off + i;
+            uint32_t w = q < ZS_MT_N ? ring[slot * ZS_MT_N + q] : ring[(slot ^ 1u) * ZS_MT_N + q - ZS_MT_N];
+            c.rw[IX(c, i)] = mt_temper(w);
+        }
+        st0 = st_pack(off, slot, ready);
+    }
+    __syncthreads();
+    if (active && !do_reset && mode == MODE_STEP) {
+        // dict-order ranks for closest() tie-breaks
+        for (int k = j; k < n_order; k += G) LR(c, LO(c, k)) = (uint8_t)k;
+    }
+    __syncthreads();
+    if (active && !do_reset && mode == MODE_STEP) {
+        // decisions (start-of-tick state), the group's lanes over the actors
+        for (int k = j; k < n_order; k += G) {
+            int s = LO(c, k), kind, tgt;
+            decide(d, c, s, actions, false, kind, tgt);
+            LK(c, s) = (uint8_t)kind;
+            LT(c, s) = tgt;
+        }
+    }
+    __syncthreads();
+    if (active && leader) {
+        c.st0 = st0;
+        c.wpos = 0;
+        c.wlen = wlen;
+        c.n_order = n_order;
+        c.t = d.scal[S_T * N + e];
+        c.deaths = d.scal[S_DEATHS * N + e];
+        c.zd = d.scal[S_ZD * N + e];
+        c.epsteps = d.scal[S_EPSTEPS * N + e];
+        c.prevzd = d.scal[S_PREVZD * N + e];
+        c.serial = d.scal[S_SERIAL * N + e];
+        c.odirty = d.scal[S_ODIRTY * N + e];
+        int needs_reset = 0;
+        if (do_reset) {
+            int rc = env_reset_leader(d, c);
+            if (rc && err_out) atomicMax(err_out, rc);
+            if (mode == MODE_STEP) {
+                int nr = d.reward_mode == ZS_REWARD_SINGLE ? 1 : d.A;
+                for (int a = 0; a < nr; a++) rew[(size_t)e * nr + a] = 0.0;
+                done_out[e] = 0;
+                trunc_out[e] = 0;
+                if (listed_out)
+                    for (int a = 0; a < d.A; a++) listed_out[(size_t)e * d.A + a] = 1;
+            }
+        } else if (mode == MODE_STEP) {
+            c.t += 1;
+            env_step_leader(d, c, actions, rew, done_out, trunc_out, listed_out);
+            if ((done_out[e] || trunc_out[e]) && (d.flags & ZS_FLAG_AUTORESET)) needs_reset = 1;
+        } else {
+            needs_reset = d.scal[S_NEEDRESET * N + e];
+        }
+        if (mode == MODE_STEP && reset_out) reset_out[e] = (uint8_t)do_reset;
+        d.scal[S_T * N + e] = c.t;
+        d.scal[S_DEATHS * N + e] = c.deaths;
+        d.scal[S_ZD * N + e] = c.zd;
+        d.scal[S_EPSTEPS * N + e] = c.epsteps;
+        d.scal[S_NORDER * N + e] = c.n_order;
+        d.scal[S_PREVZD * N + e] = c.prevzd;
+        d.scal[S_SERIAL * N + e] = c.serial;
+        d.scal[S_ODIRTY * N + e] = c.odirty;
+        d.scal[S_NEEDRESET * N + e] = needs_reset;
+        uint32_t stf = st_advance(c.st0, c.wpos);
+        d.rngst[e] = stf;
+        lst[g] = stf;
+    }
+    __syncthreads();
+    if (active) {
+        for (int s = j; s < E; s += G) {
+            d.pos[(size_t)s * N + e] = LP(c, s);
+            d.life[(size_t)s * N + e] = LL(c, s);
+            d.weapon[(size_t)s * N + e] = LW(c, s);
+            d.present[(size_t)s * N + e] = LPR(c, s);
+            d.order[(size_t)s * N + e] = LO(c, s);
+        }
+        for (int w = j; w < d.DW; w += G) d.occ_bits[(size_t)e * d.DW + w] = c.bm[IX(c, w)];
+    }
+    __syncthreads();
+    coop_refill(d, base, min(NE, N - base), lst, (uint32_t*)(smem + L.off_bm));
+}
