@@ -188,6 +188,9 @@ int zs_set_state(zs_handle* h, int32_t env, const int32_t* buf_host, void* strea
  * out[3] = k_obs launches, then clears the record. */
 int zs_profile(zs_handle* h, int32_t enable);
 int zs_profile_read(zs_handle* h, double out[4]);
+/* Diagnostic builds compiled with -DZS_STAMPS only (the product .so returns ZS_ESTATE):
+ * per-phase k_tick cycle sums / maxima over all workgroup launches since the last call. */
+int zs_debug_stamps(zs_handle* h, uint64_t* sum_out, uint64_t* max_out, int32_t n);
 
 /* Flat state record, int32 words:
  *   [0]  t (World.t)          [1] deaths            [2] zombie_deaths

@@ -759,3 +759,23 @@ extern "C" int zs_profile_read(zs_handle* h, double* out) {
     h->ev_next = 0;
     return ZS_OK;
 }
+
+// ---------------------------------------------------------------------------
+// diagnostic build (-DZS_STAMPS): per-phase k_tick cycle sums since the last read
+// ---------------------------------------------------------------------------
+extern "C" int zs_debug_stamps(zs_handle* h, uint64_t* sum_out, uint64_t* max_out, int32_t n) {
+#ifdef ZS_STAMPS
+    if (!h || !sum_out || n > ZS_NPHASE) return fail(ZS_EINVAL, "bad argument");
+    HIPCHK(hipSetDevice(h->device));
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpyFromSymbol(sum_out, HIP_SYMBOL(g_stamp_sum), sizeof(uint64_t) * n));
+    if (max_out) HIPCHK(hipMemcpyFromSymbol(max_out, HIP_SYMBOL(g_stamp_max), sizeof(uint64_t) * n));
+    unsigned long long z[ZS_NPHASE] = {0};
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_sum), z, sizeof(z)));
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_max), z, sizeof(z)));
+    return ZS_OK;
+#else
+    (void)h; (void)sum_out; (void)max_out; (void)n;
+    return fail(ZS_ESTATE, "not a ZS_STAMPS diagnostic build");
+#endif
+}

@@ -20,6 +20,28 @@
 #define NOTHING ((int)0x80000000)
 
 enum { K_NONE = 0, K_MOVE = 1, K_ATTACK = 2, K_HEAL = 3, K_DEFER = 4 };
+
+// Diagnostic build only (-DZS_STAMPS, never the product .so): lane 0 of every workgroup adds the
+// s_memtime cycles each k_tick phase took into g_stamp_sum (phase k) and counts launches.
+#ifdef ZS_STAMPS
+#define ZS_NPHASE 8
+__device__ unsigned long long g_stamp_sum[ZS_NPHASE];
+__device__ unsigned long long g_stamp_max[ZS_NPHASE];
+#define STAMP_DECL unsigned long long _st_prev = 0;
+#define STAMP(k)                                                                          \
+    do {                                                                                  \
+        unsigned long long _t;                                                            \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");      \
+        if ((k) > 0 && threadIdx.x == 0) {                                                \
+            atomicAdd(&g_stamp_sum[(k)-1], _t - _st_prev);                                \
+            atomicMax(&g_stamp_max[(k)-1], _t - _st_prev);                                \
+        }                                                                                 \
+        _st_prev = _t;                                                                    \
+    } while (0)
+#else
+#define STAMP_DECL
+#define STAMP(k)
+#endif
 enum { MODE_STEP = 0, MODE_RESET = 1 };
 
 // adjacent_positions order (utils.py:34-44)
@@ -863,6 +885,8 @@ __global__ void __launch_bounds__(64) k_tick(Dev d, int mode, const uint8_t* mas
     c.lperm = smem + L.off_perm;
     c.lmoved = smem + L.off_moved;
 
+    STAMP_DECL
+    STAMP(0);
     int do_reset = 0, n_order = 0;
     uint32_t st0 = 0;
     int wlen = 0;
@@ -902,11 +926,13 @@ __global__ void __launch_bounds__(64) k_tick(Dev d, int mode, const uint8_t* mas
         st0 = st_pack(off, slot, ready);
     }
     __syncthreads();
+    STAMP(1);
     if (active && !do_reset && mode == MODE_STEP) {
         // dict-order ranks for closest() tie-breaks
         for (int k = j; k < n_order; k += G) LR(c, LO(c, k)) = (uint8_t)k;
     }
     __syncthreads();
+    STAMP(2);
     if (active && !do_reset && mode == MODE_STEP) {
         // decisions (start-of-tick state), the group's lanes over the actors
         for (int k = j; k < n_order; k += G) {
@@ -917,6 +943,7 @@ __global__ void __launch_bounds__(64) k_tick(Dev d, int mode, const uint8_t* mas
         }
     }
     __syncthreads();
+    STAMP(3);
     if (active && leader) {
         c.st0 = st0;
         c.wpos = 0;
@@ -963,6 +990,7 @@ __global__ void __launch_bounds__(64) k_tick(Dev d, int mode, const uint8_t* mas
         lst[g] = stf;
     }
     __syncthreads();
+    STAMP(4);
     if (active) {
         for (int s = j; s < E; s += G) {
             d.pos[(size_t)s * N + e] = LP(c, s);
@@ -974,5 +1002,7 @@ __global__ void __launch_bounds__(64) k_tick(Dev d, int mode, const uint8_t* mas
         for (int w = j; w < d.DW; w += G) d.occ_bits[(size_t)e * d.DW + w] = c.bm[IX(c, w)];
     }
     __syncthreads();
+    STAMP(5);
     coop_refill(d, base, min(NE, N - base), lst, (uint32_t*)(smem + L.off_bm));
+    STAMP(6);
 }

@@ -13,7 +13,8 @@ from . import _abi
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_build", "libzombsole_mi355x.so")
 SYMBOLS = ["zs_last_error", "zs_create", "zs_destroy", "zs_obs_shape", "zs_seed", "zs_reset", "zs_step",
-           "zs_gen_actions", "zs_state_size", "zs_get_state", "zs_set_state", "zs_profile", "zs_profile_read"]
+           "zs_gen_actions", "zs_state_size", "zs_get_state", "zs_set_state", "zs_profile", "zs_profile_read",
+           "zs_debug_stamps"]
 
 _lib = None
 
@@ -27,7 +28,8 @@ def load_library(path=None):
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = path or LIB_PATH
+    # ZS_ENGINE_LIB selects a diagnostic build of the same sources (tools/stamps.py)
+    p = path or os.environ.get("ZS_ENGINE_LIB") or LIB_PATH
     if not os.path.exists(p):
         raise EngineUnavailable("HIP engine library not built: %s (run __graft_entry__.build())" % p)
     # torch ships its own libamdhip64.so.7 / libhsa-runtime64.so.1; load it first so the engine
@@ -49,6 +51,7 @@ def load_library(path=None):
     L.zs_set_state.argtypes = [vp, i32, vp, vp]
     L.zs_profile.argtypes = [vp, i32]
     L.zs_profile_read.argtypes = [vp, C.POINTER(C.c_double)]
+    L.zs_debug_stamps.argtypes = [vp, vp, vp, i32]
     for s in SYMBOLS:
         if s != "zs_last_error":
             getattr(L, s).restype = C.c_int
@@ -167,6 +170,15 @@ class Engine(object):
         if rc:
             _raise(self.L, rc, "zs_profile_read")
         return {"tick_ms": out[0], "tick_n": int(out[1]), "obs_ms": out[2], "obs_n": int(out[3])}
+
+    def debug_stamps(self, n=6):
+        """Per-phase k_tick cycle sums / maxima (diagnostic -DZS_STAMPS build only)."""
+        ssum = np.zeros(n, dtype=np.uint64)
+        smax = np.zeros(n, dtype=np.uint64)
+        rc = self.L.zs_debug_stamps(self.h, C.c_void_p(ssum.ctypes.data), C.c_void_p(smax.ctypes.data), n)
+        if rc:
+            _raise(self.L, rc, "zs_debug_stamps")
+        return ssum, smax
 
     def get_state(self, env):
         buf = np.zeros(self.state_words, dtype=np.int32)

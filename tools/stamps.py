@@ -1,0 +1,53 @@
+#!/usr/bin/env python3
+"""Diagnostic: where do k_tick's cycles go?  Builds a -DZS_STAMPS copy of the engine and
+reports, per phase, the mean and max s_memtime cycles per workgroup launch for the bench
+workload at several lanes-per-env settings.  Never used by the product or the bench."""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+SO = os.path.join(ROOT, "libzombsole_amd", "_build", "libzombsole_mi355x_stamps.so")
+PHASES = ["stage-in", "ranks", "decide", "leader", "stage-out", "mt-refill"]
+
+
+def main():
+    import __graft_entry__ as ge
+    if not os.path.exists(SO) or "--rebuild" in sys.argv:
+        subprocess.check_call([ge._hipcc()] + ge.HIPCC_FLAGS + ["-DZS_STAMPS", "-o", SO,
+                                                                 os.path.join(ge.CSRC, "engine.hip")])
+    os.environ["ZS_ENGINE_LIB"] = SO
+    import torch
+    from libzombsole_amd import _abi
+    from libzombsole_amd.engine import Engine
+    n_envs = int(os.environ.get("N_ENVS", "8192"))
+    for G in [int(g) for g in os.environ.get("GS", "1,2,4,8,16").split(",")]:
+        b = _abi.multi_env_config(n_envs, "extermination", [], "bridge64", ["0", "1"], initial_zombies=10,
+                                  minimum_zombies=0, max_episode_steps=1000, lanes_per_env=G)
+        eng = Engine(b)
+        eng.seed(list(range(n_envs)))
+        eng.reset()
+        for t in range(1, 31):
+            eng.gen_actions(t, 7)
+            eng.step()
+        torch.cuda.synchronize()
+        eng.debug_stamps()
+        eng.profile(True)
+        steps = 50
+        for t in range(31, 31 + steps):
+            eng.gen_actions(t, 7)
+            eng.step()
+        torch.cuda.synchronize()
+        prof = eng.profile_read()
+        ssum, smax = eng.debug_stamps()
+        wgs = (n_envs + 64 // G - 1) // (64 // G)
+        print("G=%2d  k_tick %.1f us  k_obs %.1f us" % (G, 1e3 * prof["tick_ms"] / prof["tick_n"],
+                                                       1e3 * prof["obs_ms"] / prof["obs_n"]))
+        for k, name in enumerate(PHASES):
+            print("   %-10s mean %9.0f cyc   max %9d cyc" % (name, ssum[k] / (wgs * steps), smax[k]))
+        eng.close()
+
+
+if __name__ == "__main__":
+    main()
