@@ -404,14 +404,16 @@ static int choose_layout(zs_handle* h, int want_g) {
     for (int G = g0; G <= 64; G *= 2) {
         int ne = 64 / G;
         int cand_full = (d.W * d.H <= 65535) ? d.ncand : 0;
+        int lists = (d.nps + d.nzs <= 4096) ? d.nps + d.nzs : 0;
         for (int cand : {cand_full, 0}) {
             for (int rw : {512, 256, 128, 64}) {
-                TickLayout L = tick_layout(ne, d.E, d.DW, rw, cand);
+                TickLayout L = tick_layout(ne, d.E, d.DW, rw, cand, lists, d.A);
                 if (L.bytes <= kMax) {
                     h->G = G;
                     d.rw_cap = rw;
                     d.rw_step = std::min(rw, 64);
                     d.cand_cap = cand;
+                    d.lists_cap = lists;
                     h->lds = L.bytes;
                     return ZS_OK;
                 }
@@ -768,11 +770,20 @@ extern "C" int zs_debug_stamps(zs_handle* h, uint64_t* sum_out, uint64_t* max_ou
     if (!h || !sum_out || n > ZS_NPHASE) return fail(ZS_EINVAL, "bad argument");
     HIPCHK(hipSetDevice(h->device));
     HIPCHK(hipDeviceSynchronize());
-    HIPCHK(hipMemcpyFromSymbol(sum_out, HIP_SYMBOL(g_stamp_sum), sizeof(uint64_t) * n));
-    if (max_out) HIPCHK(hipMemcpyFromSymbol(max_out, HIP_SYMBOL(g_stamp_max), sizeof(uint64_t) * n));
-    unsigned long long z[ZS_NPHASE] = {0};
-    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_sum), z, sizeof(z)));
-    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_max), z, sizeof(z)));
+    std::vector<unsigned long long> buf((size_t)ZS_STAMP_WGS * ZS_NPHASE);
+    HIPCHK(hipMemcpyFromSymbol(buf.data(), HIP_SYMBOL(g_stamp_wg), buf.size() * sizeof(unsigned long long)));
+    for (int k = 0; k < n; k++) {
+        sum_out[k] = 0;
+        if (max_out) max_out[k] = 0;
+    }
+    for (size_t w = 0; w < (size_t)ZS_STAMP_WGS; w++)
+        for (int k = 0; k < n; k++) {
+            unsigned long long v = buf[w * ZS_NPHASE + k];
+            sum_out[k] += v;
+            if (max_out && v > max_out[k]) max_out[k] = v;
+        }
+    std::fill(buf.begin(), buf.end(), 0ull);
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_wg), buf.data(), buf.size() * sizeof(unsigned long long)));
     return ZS_OK;
 #else
     (void)h; (void)sum_out; (void)max_out; (void)n;

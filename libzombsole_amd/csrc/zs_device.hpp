@@ -41,6 +41,7 @@ struct Dev {
     int rw_cap;      // RNG window words staged in LDS per env (tick kernel)
     int rw_step;     // words prefetched for a plain step (resets prefetch rw_cap)
     int cand_cap;    // spawn-candidate entries staged in LDS per env (0 = global scratch)
+    int lists_cap;   // static spawn-list entries staged in LDS per workgroup (0 = read from global)
     int rules, reward_mode, obs_scope, obs_enc, obs_w, obs_dtype, max_steps;
     int initial_zombies, minimum_zombies;
     uint32_t flags;

@@ -22,20 +22,19 @@
 enum { K_NONE = 0, K_MOVE = 1, K_ATTACK = 2, K_HEAL = 3, K_DEFER = 4 };
 
 // Diagnostic build only (-DZS_STAMPS, never the product .so): lane 0 of every workgroup adds the
-// s_memtime cycles each k_tick phase took into g_stamp_sum (phase k) and counts launches.
+// s_memtime ticks each k_tick phase took into its own slot g_stamp_wg[block][phase] (plain
+// stores, no contended atomics); zs_debug_stamps sums / maxes the slots on the host.
 #ifdef ZS_STAMPS
 #define ZS_NPHASE 8
-__device__ unsigned long long g_stamp_sum[ZS_NPHASE];
-__device__ unsigned long long g_stamp_max[ZS_NPHASE];
+#define ZS_STAMP_WGS 65536
+__device__ unsigned long long g_stamp_wg[ZS_STAMP_WGS * ZS_NPHASE];
 #define STAMP_DECL unsigned long long _st_prev = 0;
 #define STAMP(k)                                                                          \
     do {                                                                                  \
         unsigned long long _t;                                                            \
         asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");      \
-        if ((k) > 0 && threadIdx.x == 0) {                                                \
-            atomicAdd(&g_stamp_sum[(k)-1], _t - _st_prev);                                \
-            atomicMax(&g_stamp_max[(k)-1], _t - _st_prev);                                \
-        }                                                                                 \
+        if ((k) > 0 && threadIdx.x == 0 && blockIdx.x < ZS_STAMP_WGS)                     \
+            g_stamp_wg[blockIdx.x * ZS_NPHASE + (k)-1] += _t - _st_prev;                  \
         _st_prev = _t;                                                                    \
     } while (0)
 #else
@@ -51,16 +50,26 @@ __constant__ int c_adj_dy[4] = {1, -1, 0, 0};
 // LDS footprint of one workgroup (host and device agree on this layout)
 struct TickLayout {
     int ne;                                  // envs per workgroup
+    int off_lists;                           // static spawn lists (player then zombie), shared by the WG
+    int off_misc;                            // per-env scalars / tracker, [MISC_*][ne] int32
     int off_lst, off_bm, off_rw, off_cand;   // byte offsets
     int off_pos, off_life, off_tgt;
     int off_weap, off_pres, off_order, off_rank, off_kind, off_perm, off_moved;
     int bytes;
 };
 
-__host__ __device__ inline TickLayout tick_layout(int ne, int E, int DW, int rw_cap, int cand_cap) {
+// per-env LDS scalars (MISC rows); rows MISC_N.. hold prev_life[A] then listed[A]
+enum { MISC_T = 0, MISC_DEATHS, MISC_ZD, MISC_EPSTEPS, MISC_PREVZD, MISC_SERIAL, MISC_ODIRTY, MISC_NONPOS, MISC_N };
+
+__host__ __device__ inline TickLayout tick_layout(int ne, int E, int DW, int rw_cap, int cand_cap, int lists_cap,
+                                                  int A) {
     TickLayout L;
     L.ne = ne;
     int o = 0;
+    L.off_lists = o;
+    o += lists_cap * 4;
+    L.off_misc = o;
+    o += (MISC_N + 2 * A) * ne * 4;
     L.off_lst = o;
     o += ne * 4;
     int region = o;
@@ -100,6 +109,9 @@ __host__ __device__ inline TickLayout tick_layout(int ne, int E, int DW, int rw_
 // one env as seen by one lane of its group
 struct Grp {
     int e, g, j, ne;
+    const int32_t* pspawn;  // spawn lists (LDS copy when they fit, else global)
+    const int32_t* zspawn;
+    int32_t* misc;
     uint32_t* bm;
     uint32_t* rw;
     uint16_t* cand;
@@ -130,6 +142,7 @@ struct Grp {
 #define LK(c, s) (c).lkind[IX(c, s)]
 #define LPE(c, s) (c).lperm[IX(c, s)]
 #define LM(c, s) (c).lmoved[IX(c, s)]
+#define MISC(c, f) (c).misc[IX(c, f)]
 
 // ---------------------------------------------------------------------------
 // RNG: the leader draws pre-tempered words from the LDS window; when it runs dry it reloads
@@ -322,7 +335,7 @@ __device__ void spawn_zombies(const Dev& d, Grp& c, int count) {
         LL(c, s) = rng_int(d, c, 50, 100);
         LW(c, s) = ZS_WEAPON_CLAWS;
     }
-    spawn_in_random(d, c, k, d.zspawn, d.nzs, 0);
+    spawn_in_random(d, c, k, c.zspawn, d.nzs, 0);
 }
 
 // Game.__initialize_world__ (game.py:151-169) after the group has laid the map obstacles into
@@ -332,14 +345,9 @@ __device__ int env_reset_leader(const Dev& d, Grp& c) {
     c.deaths = 0;
     c.zd = 0;
     c.n_order = 0;
-    // the map's obstacles re-enter the world with their carried-over HP (game.py:154-155)
-    int any_nonpos = 0;
-    for (int w = 0; w < d.OW; w++) {
-        int nb = min(32, d.O - 32 * w);
-        d.obst_present[(size_t)c.e * d.OW + w] = nb == 32 ? 0xffffffffu : ((1u << nb) - 1u);
-        any_nonpos |= d.obst_nonpos[(size_t)c.e * d.OW + w] != 0;
-    }
-    c.odirty = any_nonpos;
+    // the map's obstacles re-entered the world with their carried-over HP (game.py:154-155):
+    // the group set every present bit in the prologue and flagged carried-over dead ones
+    c.odirty = MISC(c, MISC_NONPOS);
     // players: Player() picks a random weapon unless its module gives one (things.py:113-116)
     for (int p = 0; p < d.P; p++) {
         int s = d.A + p, w;
@@ -364,16 +372,16 @@ __device__ int env_reset_leader(const Dev& d, Grp& c) {
         LL(c, a) = 100;
     }
     for (int p = 0; p < d.P; p++) LM(c, p) = (uint8_t)(d.A + p);
-    int rc = spawn_in_random(d, c, d.P, d.pspawn, d.nps, 1);
+    int rc = spawn_in_random(d, c, d.P, c.pspawn, d.nps, 1);
     if (rc) return rc;
     for (int a = 0; a < d.A; a++) LM(c, a) = (uint8_t)a;
-    rc = spawn_in_random(d, c, d.A, d.pspawn, d.nps, 1);
+    rc = spawn_in_random(d, c, d.A, c.pspawn, d.nps, 1);
     if (rc) return rc;
     spawn_zombies(d, c, d.initial_zombies);
     c.prevzd = 0;
     for (int a = 0; a < d.A; a++) {
-        d.prev_life[(size_t)a * d.N + c.e] = LL(c, a);
-        d.listed[(size_t)a * d.N + c.e] = 1;
+        MISC(c, MISC_N + a) = LL(c, a);
+        MISC(c, MISC_N + d.A + a) = 1;
     }
     c.epsteps = 0;
     return ZS_OK;
@@ -764,7 +772,7 @@ __device__ void env_step_leader(const Dev& d, Grp& c, const int32_t* actions, do
     if (d.reward_mode == ZS_REWARD_SINGLE) {
         long long sp = 0, sc = 0;
         for (int a = 0; a < A; a++) {
-            sp += d.prev_life[(size_t)a * N + c.e];
+            sp += MISC(c, MISC_N + a);
             sc += LL(c, a);
         }
         double prev = (double)c.prevzd + (double)sp / 100.0;
@@ -772,12 +780,12 @@ __device__ void env_step_leader(const Dev& d, Grp& c, const int32_t* actions, do
         rs = cur - prev;
     } else {
         for (int a = 0; a < A; a++) {
-            double prev = (double)c.prevzd + (double)d.prev_life[(size_t)a * N + c.e] / 100.0;
+            double prev = (double)c.prevzd + (double)MISC(c, MISC_N + a) / 100.0;
             double cur = (double)c.zd + (double)LL(c, a) / 100.0;
             rew[(size_t)c.e * A + a] = cur - prev;
         }
     }
-    for (int a = 0; a < A; a++) d.prev_life[(size_t)a * N + c.e] = LL(c, a);
+    for (int a = 0; a < A; a++) MISC(c, MISC_N + a) = LL(c, a);
     c.prevzd = c.zd;
     // spawn_zombies_to_maintain_minimum (game.py:196-201)
     {
@@ -803,16 +811,16 @@ __device__ void env_step_leader(const Dev& d, Grp& c, const int32_t* actions, do
         if (ended || tr) rs += end_reward;
         rew[c.e] = rs;
         if (listed_out)
-            for (int a = 0; a < A; a++) listed_out[(size_t)c.e * A + a] = d.listed[(size_t)a * N + c.e];
+            for (int a = 0; a < A; a++) listed_out[(size_t)c.e * A + a] = (uint8_t)MISC(c, MISC_N + A + a);
     } else {
         for (int a = 0; a < A; a++) {
-            uint8_t was = d.listed[(size_t)a * N + c.e];
+            uint8_t was = (uint8_t)MISC(c, MISC_N + A + a);
             if (listed_out) listed_out[(size_t)c.e * A + a] = was;
             double r = rew[(size_t)c.e * A + a];
             if (!was) r = 0.0;
             else if (LL(c, a) > 0) r = r + end_reward;
             rew[(size_t)c.e * A + a] = r;
-            d.listed[(size_t)a * N + c.e] = LL(c, a) > 0;
+            MISC(c, MISC_N + A + a) = LL(c, a) > 0;
         }
     }
     c.epsteps++;
@@ -861,16 +869,17 @@ __global__ void __launch_bounds__(64) k_tick(Dev d, int mode, const uint8_t* mas
     extern __shared__ __align__(16) uint8_t smem[];
     constexpr int NE = 64 / G;
     const int lane = threadIdx.x, g = lane / G, j = lane - g * G;
-    const int base = blockIdx.x * NE, e = base + g, N = d.N, E = d.E;
+    const int base = blockIdx.x * NE, e = base + g, N = d.N, E = d.E, A = d.A;
     const bool active = e < N;
     const bool leader = j == 0;
-    const TickLayout L = tick_layout(NE, E, d.DW, d.rw_cap, d.cand_cap);
+    const TickLayout L = tick_layout(NE, E, d.DW, d.rw_cap, d.cand_cap, d.lists_cap, A);
     uint32_t* lst = (uint32_t*)(smem + L.off_lst);
     Grp c;
     c.e = e;
     c.g = g;
     c.j = j;
     c.ne = NE;
+    c.misc = (int32_t*)(smem + L.off_misc);
     c.bm = (uint32_t*)(smem + L.off_bm);
     c.rw = (uint32_t*)(smem + L.off_rw);
     c.cand = (uint16_t*)(smem + L.off_cand);
@@ -884,6 +893,15 @@ __global__ void __launch_bounds__(64) k_tick(Dev d, int mode, const uint8_t* mas
     c.lkind = smem + L.off_kind;
     c.lperm = smem + L.off_perm;
     c.lmoved = smem + L.off_moved;
+    if (d.lists_cap) {  // the static spawn lists, staged once per workgroup
+        int32_t* ll = (int32_t*)(smem + L.off_lists);
+        for (int i = lane; i < d.nps + d.nzs; i += 64) ll[i] = i < d.nps ? d.pspawn[i] : d.zspawn[i - d.nps];
+        c.pspawn = ll;
+        c.zspawn = ll + d.nps;
+    } else {
+        c.pspawn = d.pspawn;
+        c.zspawn = d.zspawn;
+    }
 
     STAMP_DECL
     STAMP(0);
@@ -902,11 +920,32 @@ __global__ void __launch_bounds__(64) k_tick(Dev d, int mode, const uint8_t* mas
             LPR(c, s) = do_reset ? 0 : d.present[(size_t)s * N + e];
             LO(c, s) = d.order[(size_t)s * N + e];
         }
+        // per-env scalars and the reward tracker / env.agents rows
+        for (int f = j; f < MISC_N + 2 * A; f += G) {
+            int v;
+            if (f == MISC_T) v = d.scal[S_T * N + e];
+            else if (f == MISC_DEATHS) v = d.scal[S_DEATHS * N + e];
+            else if (f == MISC_ZD) v = d.scal[S_ZD * N + e];
+            else if (f == MISC_EPSTEPS) v = d.scal[S_EPSTEPS * N + e];
+            else if (f == MISC_PREVZD) v = d.scal[S_PREVZD * N + e];
+            else if (f == MISC_SERIAL) v = d.scal[S_SERIAL * N + e];
+            else if (f == MISC_ODIRTY) v = d.scal[S_ODIRTY * N + e];
+            else if (f == MISC_NONPOS) v = 0;
+            else if (f < MISC_N + A) v = d.prev_life[(size_t)(f - MISC_N) * N + e];
+            else v = d.listed[(size_t)(f - MISC_N - A) * N + e];
+            MISC(c, f) = v;
+        }
         // occupancy bitmap: persisted one, or the map's obstacles for a new World
         const uint32_t* src = do_reset ? d.obstbits : d.occ_bits + (size_t)e * d.DW;
         for (int w = j; w < d.DW; w += G) c.bm[IX(c, w)] = src[w];
-        if (do_reset)
+        if (do_reset) {
             for (int w = j; w < d.DW; w += G) d.dead[(size_t)e * d.DW + w] = 0;
+            // every map obstacle re-enters the dict (game.py:154-155); flag carried-over dead ones
+            for (int w = j; w < d.OW; w += G) {
+                int nb = min(32, d.O - 32 * w);
+                d.obst_present[(size_t)e * d.OW + w] = nb == 32 ? 0xffffffffu : ((1u << nb) - 1u);
+            }
+        }
         // RNG window: the next words of this env's stream, tempered
         uint32_t st = d.rngst[e];
         uint32_t off = st & 1023u, slot = (st >> 10) & 1u, ready = (st >> 11) & 1u;
@@ -926,13 +965,15 @@ __global__ void __launch_bounds__(64) k_tick(Dev d, int mode, const uint8_t* mas
         st0 = st_pack(off, slot, ready);
     }
     __syncthreads();
-    STAMP(1);
+    if (active && do_reset)
+        for (int w = j; w < d.OW; w += G)
+            if (d.obst_nonpos[(size_t)e * d.OW + w]) MISC(c, MISC_NONPOS) = 1;
     if (active && !do_reset && mode == MODE_STEP) {
         // dict-order ranks for closest() tie-breaks
         for (int k = j; k < n_order; k += G) LR(c, LO(c, k)) = (uint8_t)k;
     }
     __syncthreads();
-    STAMP(2);
+    STAMP(1);
     if (active && !do_reset && mode == MODE_STEP) {
         // decisions (start-of-tick state), the group's lanes over the actors
         for (int k = j; k < n_order; k += G) {
@@ -943,30 +984,30 @@ __global__ void __launch_bounds__(64) k_tick(Dev d, int mode, const uint8_t* mas
         }
     }
     __syncthreads();
-    STAMP(3);
+    STAMP(2);
     if (active && leader) {
         c.st0 = st0;
         c.wpos = 0;
         c.wlen = wlen;
         c.n_order = n_order;
-        c.t = d.scal[S_T * N + e];
-        c.deaths = d.scal[S_DEATHS * N + e];
-        c.zd = d.scal[S_ZD * N + e];
-        c.epsteps = d.scal[S_EPSTEPS * N + e];
-        c.prevzd = d.scal[S_PREVZD * N + e];
-        c.serial = d.scal[S_SERIAL * N + e];
-        c.odirty = d.scal[S_ODIRTY * N + e];
+        c.t = MISC(c, MISC_T);
+        c.deaths = MISC(c, MISC_DEATHS);
+        c.zd = MISC(c, MISC_ZD);
+        c.epsteps = MISC(c, MISC_EPSTEPS);
+        c.prevzd = MISC(c, MISC_PREVZD);
+        c.serial = MISC(c, MISC_SERIAL);
+        c.odirty = MISC(c, MISC_ODIRTY);
         int needs_reset = 0;
         if (do_reset) {
             int rc = env_reset_leader(d, c);
             if (rc && err_out) atomicMax(err_out, rc);
             if (mode == MODE_STEP) {
-                int nr = d.reward_mode == ZS_REWARD_SINGLE ? 1 : d.A;
+                int nr = d.reward_mode == ZS_REWARD_SINGLE ? 1 : A;
                 for (int a = 0; a < nr; a++) rew[(size_t)e * nr + a] = 0.0;
                 done_out[e] = 0;
                 trunc_out[e] = 0;
                 if (listed_out)
-                    for (int a = 0; a < d.A; a++) listed_out[(size_t)e * d.A + a] = 1;
+                    for (int a = 0; a < A; a++) listed_out[(size_t)e * A + a] = 1;
             }
         } else if (mode == MODE_STEP) {
             c.t += 1;
@@ -976,21 +1017,21 @@ __global__ void __launch_bounds__(64) k_tick(Dev d, int mode, const uint8_t* mas
             needs_reset = d.scal[S_NEEDRESET * N + e];
         }
         if (mode == MODE_STEP && reset_out) reset_out[e] = (uint8_t)do_reset;
-        d.scal[S_T * N + e] = c.t;
-        d.scal[S_DEATHS * N + e] = c.deaths;
-        d.scal[S_ZD * N + e] = c.zd;
-        d.scal[S_EPSTEPS * N + e] = c.epsteps;
+        MISC(c, MISC_T) = c.t;
+        MISC(c, MISC_DEATHS) = c.deaths;
+        MISC(c, MISC_ZD) = c.zd;
+        MISC(c, MISC_EPSTEPS) = c.epsteps;
+        MISC(c, MISC_PREVZD) = c.prevzd;
+        MISC(c, MISC_SERIAL) = c.serial;
+        MISC(c, MISC_ODIRTY) = c.odirty;
         d.scal[S_NORDER * N + e] = c.n_order;
-        d.scal[S_PREVZD * N + e] = c.prevzd;
-        d.scal[S_SERIAL * N + e] = c.serial;
-        d.scal[S_ODIRTY * N + e] = c.odirty;
         d.scal[S_NEEDRESET * N + e] = needs_reset;
         uint32_t stf = st_advance(c.st0, c.wpos);
         d.rngst[e] = stf;
         lst[g] = stf;
     }
     __syncthreads();
-    STAMP(4);
+    STAMP(3);
     if (active) {
         for (int s = j; s < E; s += G) {
             d.pos[(size_t)s * N + e] = LP(c, s);
@@ -999,10 +1040,23 @@ __global__ void __launch_bounds__(64) k_tick(Dev d, int mode, const uint8_t* mas
             d.present[(size_t)s * N + e] = LPR(c, s);
             d.order[(size_t)s * N + e] = LO(c, s);
         }
+        for (int f = j; f < MISC_N + 2 * A; f += G) {
+            int v = MISC(c, f);
+            if (f == MISC_T) d.scal[S_T * N + e] = v;
+            else if (f == MISC_DEATHS) d.scal[S_DEATHS * N + e] = v;
+            else if (f == MISC_ZD) d.scal[S_ZD * N + e] = v;
+            else if (f == MISC_EPSTEPS) d.scal[S_EPSTEPS * N + e] = v;
+            else if (f == MISC_PREVZD) d.scal[S_PREVZD * N + e] = v;
+            else if (f == MISC_SERIAL) d.scal[S_SERIAL * N + e] = v;
+            else if (f == MISC_ODIRTY) d.scal[S_ODIRTY * N + e] = v;
+            else if (f == MISC_NONPOS) {
+            } else if (f < MISC_N + A) d.prev_life[(size_t)(f - MISC_N) * N + e] = v;
+            else d.listed[(size_t)(f - MISC_N - A) * N + e] = (uint8_t)v;
+        }
         for (int w = j; w < d.DW; w += G) d.occ_bits[(size_t)e * d.DW + w] = c.bm[IX(c, w)];
     }
     __syncthreads();
-    STAMP(5);
+    STAMP(4);
     coop_refill(d, base, min(NE, N - base), lst, (uint32_t*)(smem + L.off_bm));
-    STAMP(6);
+    STAMP(5);
 }

@@ -171,7 +171,7 @@ class Engine(object):
             _raise(self.L, rc, "zs_profile_read")
         return {"tick_ms": out[0], "tick_n": int(out[1]), "obs_ms": out[2], "obs_n": int(out[3])}
 
-    def debug_stamps(self, n=6):
+    def debug_stamps(self, n=5):
         """Per-phase k_tick cycle sums / maxima (diagnostic -DZS_STAMPS build only)."""
         ssum = np.zeros(n, dtype=np.uint64)
         smax = np.zeros(n, dtype=np.uint64)

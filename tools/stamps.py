@@ -9,7 +9,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 SO = os.path.join(ROOT, "libzombsole_amd", "_build", "libzombsole_mi355x_stamps.so")
-PHASES = ["stage-in", "ranks", "decide", "leader", "stage-out", "mt-refill"]
+PHASES = ["stage-in", "decide", "leader", "stage-out", "mt-refill"]
 
 
 def main():
