@@ -19,6 +19,15 @@
 
 #define NOTHING ((int)0x80000000)
 
+// Explicit LDS (address space 3) pointer types for every view into the workgroup's image, so the
+// compiler always emits ds_* instructions (a pointer that might be LDS or global degrades to
+// flat accesses and pushes the lane context to scratch).
+#define ZS_LDS __attribute__((address_space(3)))
+typedef ZS_LDS uint32_t lu32;
+typedef ZS_LDS int32_t li32;
+typedef ZS_LDS uint16_t lu16;
+typedef ZS_LDS uint8_t lu8;
+
 enum { K_NONE = 0, K_MOVE = 1, K_ATTACK = 2, K_HEAL = 3, K_DEFER = 4 };
 
 // Diagnostic build only (-DZS_STAMPS, never the product .so): lane 0 of every workgroup adds the
@@ -109,22 +118,21 @@ __host__ __device__ inline TickLayout tick_layout(int ne, int E, int DW, int rw_
 // one env as seen by one lane of its group
 struct Grp {
     int e, g, j, ne;
-    const int32_t* pspawn;  // spawn lists (LDS copy when they fit, else global)
-    const int32_t* zspawn;
-    int32_t* misc;
-    uint32_t* bm;
-    uint32_t* rw;
-    uint16_t* cand;
-    int32_t* lpos;
-    int32_t* llife;
-    int32_t* ltgt;
-    uint8_t* lweap;
-    uint8_t* lpres;
-    uint8_t* lorder;
-    uint8_t* lrank;
-    uint8_t* lkind;
-    uint8_t* lperm;
-    uint8_t* lmoved;
+    li32* lists;  // static spawn lists (player then zombie) when d.lists_cap
+    li32* misc;
+    lu32* bm;
+    lu32* rw;
+    lu16* cand;
+    li32* lpos;
+    li32* llife;
+    li32* ltgt;
+    lu8* lweap;
+    lu8* lpres;
+    lu8* lorder;
+    lu8* lrank;
+    lu8* lkind;
+    lu8* lperm;
+    lu8* lmoved;
     // leader registers
     uint32_t st0;  // ring state at the start of the LDS window
     int wpos, wlen;
@@ -207,7 +215,7 @@ __device__ __forceinline__ bool occupied(const Dev& d, const Grp& c, int x, int 
 }
 
 // things.get(position): entity slot (>= 0), obstacle -(index+1), or NOTHING
-__device__ int thing_at(const Dev& d, const Grp& c, int x, int y) {
+__device__ __forceinline__ int thing_at(const Dev& d, const Grp& c, int x, int y) {
     if (!occupied(d, c, x, y)) return NOTHING;
     int32_t pk = pack_xy(x, y);
     for (int s = 0; s < d.E; s++)
@@ -267,10 +275,16 @@ __device__ __forceinline__ void place(const Dev& d, Grp& c, int s, int cell) {
     d.serial[(size_t)s * d.N + c.e] = (uint32_t)(++c.serial);
 }
 
+// entry i of the player (which = 0) or zombie (which = 1) spawn list, packed x | y << 16
+__device__ __forceinline__ int32_t spawn_at(const Dev& d, const Grp& c, int which, int i) {
+    if (d.lists_cap) return c.lists[(which ? d.nps : 0) + i];
+    return which ? d.zspawn[i] : d.pspawn[i];
+}
+
 // World.spawn_in_random (core.py:40-66) for the k slots listed in LM(c, 0..k).  Only the first
 // k Fisher-Yates iterations can move the k cells that get popped; the rest are replayed for
 // their RNG draws alone.
-__device__ int spawn_in_random(const Dev& d, Grp& c, int k, const int32_t* list, int nlist, int fail_if_cant) {
+__device__ __forceinline__ int spawn_in_random(const Dev& d, Grp& c, int k, int which, int nlist, int fail_if_cant) {
     const int total = nlist ? nlist : d.W * d.H;
     const bool lds = total <= d.cand_cap;
     int32_t* gc = d.cand + (size_t)c.e * d.ncand;
@@ -292,7 +306,7 @@ __device__ int spawn_in_random(const Dev& d, Grp& c, int k, const int32_t* list,
             }
     } else {
         for (int i = 0; i < nlist; i++) {
-            int32_t p = list[i];
+            int32_t p = spawn_at(d, c, which, i);
             int cell = unpack_y(p) * d.W + unpack_x(p);
             if (!bm_test(c, cell)) {
                 CSET(n, cell);
@@ -326,7 +340,7 @@ __device__ int spawn_in_random(const Dev& d, Grp& c, int k, const int32_t* list,
 
 // Game.spawn_zombies(count) into free zombie slots (game.py:189-194); every Zombie() draws
 // randint(50, 100) before the spawn shuffle (things.py:61-68).
-__device__ void spawn_zombies(const Dev& d, Grp& c, int count) {
+__device__ __forceinline__ void spawn_zombies(const Dev& d, Grp& c, int count) {
     int k = 0;
     for (int s = d.A + d.P; s < d.E && k < count; s++)
         if (!LPR(c, s)) LM(c, k++) = (uint8_t)s;
@@ -335,12 +349,12 @@ __device__ void spawn_zombies(const Dev& d, Grp& c, int count) {
         LL(c, s) = rng_int(d, c, 50, 100);
         LW(c, s) = ZS_WEAPON_CLAWS;
     }
-    spawn_in_random(d, c, k, c.zspawn, d.nzs, 0);
+    spawn_in_random(d, c, k, 1, d.nzs, 0);
 }
 
 // Game.__initialize_world__ (game.py:151-169) after the group has laid the map obstacles into
 // the bitmap and cleared the entity table; plus the reward-tracker / env.agents reset.
-__device__ int env_reset_leader(const Dev& d, Grp& c) {
+__device__ __forceinline__ int env_reset_leader(const Dev& d, Grp& c) {
     c.t = -1;
     c.deaths = 0;
     c.zd = 0;
@@ -372,10 +386,10 @@ __device__ int env_reset_leader(const Dev& d, Grp& c) {
         LL(c, a) = 100;
     }
     for (int p = 0; p < d.P; p++) LM(c, p) = (uint8_t)(d.A + p);
-    int rc = spawn_in_random(d, c, d.P, c.pspawn, d.nps, 1);
+    int rc = spawn_in_random(d, c, d.P, 0, d.nps, 1);
     if (rc) return rc;
     for (int a = 0; a < d.A; a++) LM(c, a) = (uint8_t)a;
-    rc = spawn_in_random(d, c, d.A, c.pspawn, d.nps, 1);
+    rc = spawn_in_random(d, c, d.A, 0, d.nps, 1);
     if (rc) return rc;
     spawn_zombies(d, c, d.initial_zombies);
     c.prevzd = 0;
@@ -402,7 +416,7 @@ __device__ __forceinline__ int pick_bit(int mask, int j) {  // j-th set bit (asc
 }
 
 // Zombie.next_step (things.py:70-105)
-__device__ void decide_zombie(const Dev& d, Grp& c, int s, bool rng, int& kind, int& tgt) {
+__device__ __forceinline__ void decide_zombie(const Dev& d, Grp& c, int s, bool rng, int& kind, int& tgt) {
     int p = LP(c, s), x = unpack_x(p), y = unpack_y(p);
     int freemask = 0;
     for (int k = 0; k < 4; k++)  // possible_moves: not in things, not bounds-checked (utils.py:47-52)
@@ -464,7 +478,7 @@ __device__ void decide_zombie(const Dev& d, Grp& c, int s, bool rng, int& kind, 
 __device__ __forceinline__ int clamp16(int v) { return v < -16384 ? -16384 : (v > 16383 ? 16383 : v); }
 
 // Agent.next_step (players/agent.py:28-96) on the action triple
-__device__ void decide_agent(const Dev& d, const Grp& c, int s, const int32_t* act, int& kind, int& tgt) {
+__device__ __forceinline__ void decide_agent(const Dev& d, const Grp& c, int s, const int32_t* act, int& kind, int& tgt) {
     int p = LP(c, s), x = unpack_x(p), y = unpack_y(p);
     int ak = act[0], dx = clamp16(act[1]), dy = clamp16(act[2]);
     kind = K_NONE;
@@ -502,7 +516,7 @@ __device__ void decide_agent(const Dev& d, const Grp& c, int s, const int32_t* a
 }
 
 // scripted bots (players/{terminator,sniper,troll,hamster,randoman}.py)
-__device__ void decide_bot(const Dev& d, Grp& c, int s, bool rng, int& kind, int& tgt) {
+__device__ __forceinline__ void decide_bot(const Dev& d, Grp& c, int s, bool rng, int& kind, int& tgt) {
     int p = LP(c, s), x = unpack_x(p), y = unpack_y(p);
     int bt = d.bot_types[s - d.A];
     kind = K_NONE;
@@ -604,7 +618,7 @@ __device__ __forceinline__ void decide(const Dev& d, Grp& c, int s, const int32_
 // ---------------------------------------------------------------------------
 // rules (rules/{extermination,survival,safehouse,evacuation}.py)
 // ---------------------------------------------------------------------------
-__device__ void rules_check(const Dev& d, const Grp& c, int& ended, int& won) {
+__device__ __forceinline__ void rules_check(const Dev& d, const Grp& c, int& ended, int& won) {
     int pa = 0;  // Rules.players_alive (rules.py:6-11)
     for (int s = 0; s < d.A + d.P; s++) pa |= LL(c, s) > 0;
     if (d.rules == ZS_RULES_EXTERMINATION) {
@@ -671,9 +685,9 @@ __device__ void rules_check(const Dev& d, const Grp& c, int& ended, int& won) {
 // ---------------------------------------------------------------------------
 // leader: the order-dependent rest of the tick (gym_env.py:99-145 / multiagent_env.py:111-171)
 // ---------------------------------------------------------------------------
-__device__ void env_step_leader(const Dev& d, Grp& c, const int32_t* actions, double* rew, uint8_t* done_out,
+__device__ __forceinline__ void env_step_leader(const Dev& d, Grp& c, const int32_t* actions, double* rew, uint8_t* done_out,
                                 uint8_t* trunc_out, uint8_t* listed_out) {
-    const int A = d.A, E = d.E, N = d.N;
+    const int A = d.A, E = d.E;
     // World.get_actions (core.py:80-101): deferred (RNG-drawing) decisions in dict order
     int nact = 0;
     for (int k = 0; k < c.n_order; k++) {
@@ -833,7 +847,7 @@ __device__ void env_step_leader(const Dev& d, Grp& c, const int32_t* actions, do
 // wave-cooperative MT19937 refill: every env of the workgroup whose next block is not ready
 // gets it twisted by all 64 lanes (3 dependency phases over the 624-word block).
 // ---------------------------------------------------------------------------
-__device__ void coop_refill(const Dev& d, int base, int count, const uint32_t* lst, uint32_t* tw) {
+__device__ __forceinline__ void coop_refill(const Dev& d, int base, int count, const lu32* lst, lu32* tw) {
     const int tid = threadIdx.x, nt = blockDim.x;
     for (int i = 0; i < count; i++) {
         uint32_t st = lst[i];
@@ -844,7 +858,7 @@ __device__ void coop_refill(const Dev& d, int base, int count, const uint32_t* l
         uint32_t* dst = ring + (slot ^ 1u) * ZS_MT_N;
         for (int k = tid; k < ZS_MT_N; k += nt) tw[k] = src[k];
         __syncthreads();
-        uint32_t* nw = tw + ZS_MT_N;
+        lu32* nw = tw + ZS_MT_N;
         for (int k = tid; k < ZS_MT_N - ZS_MT_M; k += nt) nw[k] = mt_f(tw[k], tw[k + 1], tw[k + ZS_MT_M]);
         __syncthreads();
         for (int k = (ZS_MT_N - ZS_MT_M) + tid; k < 2 * (ZS_MT_N - ZS_MT_M); k += nt)
@@ -873,35 +887,29 @@ __global__ void __launch_bounds__(64) k_tick(Dev d, int mode, const uint8_t* mas
     const bool active = e < N;
     const bool leader = j == 0;
     const TickLayout L = tick_layout(NE, E, d.DW, d.rw_cap, d.cand_cap, d.lists_cap, A);
-    uint32_t* lst = (uint32_t*)(smem + L.off_lst);
+    lu32* lst = (lu32*)(smem + L.off_lst);
     Grp c;
     c.e = e;
     c.g = g;
     c.j = j;
     c.ne = NE;
-    c.misc = (int32_t*)(smem + L.off_misc);
-    c.bm = (uint32_t*)(smem + L.off_bm);
-    c.rw = (uint32_t*)(smem + L.off_rw);
-    c.cand = (uint16_t*)(smem + L.off_cand);
-    c.lpos = (int32_t*)(smem + L.off_pos);
-    c.llife = (int32_t*)(smem + L.off_life);
-    c.ltgt = (int32_t*)(smem + L.off_tgt);
-    c.lweap = smem + L.off_weap;
-    c.lpres = smem + L.off_pres;
-    c.lorder = smem + L.off_order;
-    c.lrank = smem + L.off_rank;
-    c.lkind = smem + L.off_kind;
-    c.lperm = smem + L.off_perm;
-    c.lmoved = smem + L.off_moved;
-    if (d.lists_cap) {  // the static spawn lists, staged once per workgroup
-        int32_t* ll = (int32_t*)(smem + L.off_lists);
-        for (int i = lane; i < d.nps + d.nzs; i += 64) ll[i] = i < d.nps ? d.pspawn[i] : d.zspawn[i - d.nps];
-        c.pspawn = ll;
-        c.zspawn = ll + d.nps;
-    } else {
-        c.pspawn = d.pspawn;
-        c.zspawn = d.zspawn;
-    }
+    c.misc = (li32*)(smem + L.off_misc);
+    c.bm = (lu32*)(smem + L.off_bm);
+    c.rw = (lu32*)(smem + L.off_rw);
+    c.cand = (lu16*)(smem + L.off_cand);
+    c.lpos = (li32*)(smem + L.off_pos);
+    c.llife = (li32*)(smem + L.off_life);
+    c.ltgt = (li32*)(smem + L.off_tgt);
+    c.lweap = (lu8*)(smem + L.off_weap);
+    c.lpres = (lu8*)(smem + L.off_pres);
+    c.lorder = (lu8*)(smem + L.off_order);
+    c.lrank = (lu8*)(smem + L.off_rank);
+    c.lkind = (lu8*)(smem + L.off_kind);
+    c.lperm = (lu8*)(smem + L.off_perm);
+    c.lmoved = (lu8*)(smem + L.off_moved);
+    c.lists = (li32*)(smem + L.off_lists);
+    if (d.lists_cap)  // the static spawn lists, staged once per workgroup
+        for (int i = lane; i < d.nps + d.nzs; i += 64) c.lists[i] = i < d.nps ? d.pspawn[i] : d.zspawn[i - d.nps];
 
     STAMP_DECL
     STAMP(0);
@@ -1057,6 +1065,6 @@ __global__ void __launch_bounds__(64) k_tick(Dev d, int mode, const uint8_t* mas
     }
     __syncthreads();
     STAMP(4);
-    coop_refill(d, base, min(NE, N - base), lst, (uint32_t*)(smem + L.off_bm));
+    coop_refill(d, base, min(NE, N - base), lst, (lu32*)(smem + L.off_bm));
     STAMP(5);
 }
