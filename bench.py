@@ -143,6 +143,7 @@ def main():
     tick_b, obs_b = algorithmic_bytes(E, args.agents, (m.size[0] * m.size[1] + 7) // 8, obs_per_env, mt_words)
     tick_ms = prof["tick_ms"] / max(prof["tick_n"], 1)
     obs_ms = prof["obs_ms"] / max(prof["obs_n"], 1)
+    reset_ms = prof["reset_ms"] / max(prof["reset_n"], 1)
     if tick_ms >= obs_ms:
         dom, dom_ms, dom_b = "k_tick", tick_ms, tick_b
     else:
@@ -171,7 +172,8 @@ def main():
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
                      "algorithmic_bytes_per_launch": dom_b * n_local,
-                     "avg_launch_ms": dom_ms, "k_tick_ms": tick_ms, "k_obs_ms": obs_ms},
+                     "avg_launch_ms": dom_ms, "k_tick_ms": tick_ms, "k_obs_ms": obs_ms,
+                     "k_reset_ms": reset_ms},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -154,7 +154,9 @@ int zs_obs_shape(const zs_handle* h, int32_t out[4]);
 int zs_seed(zs_handle* h, int32_t env0, int32_t n, const uint64_t* seeds_host, void* stream);
 
 /* Reset the envs whose byte in env_mask_dev is nonzero (NULL = all) and write
- * their reset observations into obs_dev (other envs' slices untouched). */
+ * their reset observations into obs_dev (other envs' slices untouched).  A new
+ * handle's envs are all pending reset: the first zs_step resets them if zs_reset
+ * was not called. */
 int zs_reset(zs_handle* h, const uint8_t* env_mask_dev, void* obs_dev, void* stream);
 
 /* One lock-step tick for every env.
@@ -182,12 +184,13 @@ int zs_get_state(zs_handle* h, int32_t env, int32_t* buf_host, void* stream);
 int zs_set_state(zs_handle* h, int32_t env, const int32_t* buf_host, void* stream);
 
 /* Diagnostics (not part of the reference surface): when enabled, every k_tick
- * (the step kernel) and k_obs (the observation kernel) launch is bracketed by
- * HIP events on its stream.  zs_profile_read synchronizes and returns
- * out[0] = total k_tick ms, out[1] = k_tick launches, out[2] = total k_obs ms,
- * out[3] = k_obs launches, then clears the record. */
+ * (the step kernel), k_obs (the observation kernel) and k_reset (world rebuild)
+ * launch is bracketed by HIP events on its stream.  zs_profile_read synchronizes
+ * and returns out[0] = total k_tick ms, out[1] = k_tick launches, out[2] = total
+ * k_obs ms, out[3] = k_obs launches, out[4] = total k_reset ms, out[5] = k_reset
+ * launches, then clears the record. */
 int zs_profile(zs_handle* h, int32_t enable);
-int zs_profile_read(zs_handle* h, double out[4]);
+int zs_profile_read(zs_handle* h, double out[6]);
 /* Diagnostic builds compiled with -DZS_STAMPS only (the product .so returns ZS_ESTATE):
  * per-phase k_tick cycle sums / maxima over all workgroup launches since the last call. */
 int zs_debug_stamps(zs_handle* h, uint64_t* sum_out, uint64_t* max_out, int32_t n);

@@ -16,7 +16,7 @@
 
 #include "zs_device.hpp"
 
-#include "zs_tick.hpp"
+#include "zs_reset.hpp"
 
 // ---------------------------------------------------------------------------
 // observations (gym/observation.py:36-173): one workgroup per env.  The env's entity slots
@@ -269,6 +269,17 @@ __global__ void k_set_state(Dev d, int e, const int32_t* buf) {
         }
 }
 
+__global__ void k_init_pending(Dev d, int* list, int* count) {
+    int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e == 0) {
+        count[0] = d.N;
+        count[1] = 0;
+    }
+    if (e >= d.N) return;
+    list[e] = e;
+    d.scal[S_NEEDRESET * d.N + e] = 1;
+}
+
 __global__ void k_init_obstacles(Dev d) {
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (size_t)d.N * d.O) return;
@@ -304,10 +315,15 @@ struct zs_handle {
     int32_t* d_state;
     uint64_t* d_seedbuf;
     int* d_err;
+    // next-step autoreset work lists: k_tick appends to list[1-par], k_reset drains list[par]
+    int* d_rlist[2];
+    int* d_rcount;  // [2]
+    int rpar = 0;
+    size_t reset_lds = 0;
     // diagnostics: HIP events bracketing every k_tick / k_obs launch on its stream
     int prof = 0;
     std::vector<hipEvent_t> ev_pool;
-    std::vector<std::pair<int, int>> ev_tick, ev_obs;  // (start, end) indices into ev_pool
+    std::vector<std::pair<int, int>> ev_tick, ev_obs, ev_reset;  // (start, end) indices into ev_pool
     size_t ev_next = 0;
 };
 
@@ -553,8 +569,24 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
     TRY(dalloc(h, &h->d_state, (size_t)h->state_words));
     TRY(dalloc(h, &h->d_seedbuf, N));
     TRY(dalloc(h, &h->d_err, 1));
+    TRY(dalloc(h, &h->d_rlist[0], N));
+    TRY(dalloc(h, &h->d_rlist[1], N));
+    TRY(dalloc(h, &h->d_rcount, 2));
     // workgroup: 64 envs (one wave) unless the LDS image of the entity table is too large
     TRY(choose_layout(h, cfg->lanes_per_env));
+    h->reset_lds = (size_t)reset_lds_bytes(d.E, d.DW, d.ncand, d.lists_cap);
+    if (h->reset_lds > 160 * 1024) {
+        free_all(h);
+        delete h;
+        return fail(ZS_EINVAL, "map too large for the reset kernel's LDS image");
+    }
+    if (h->reset_lds > 64 * 1024 &&
+        hipFuncSetAttribute((const void*)k_reset, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->reset_lds) !=
+            hipSuccess) {
+        free_all(h);
+        delete h;
+        return fail(ZS_EHIP, "cannot raise k_reset's dynamic LDS limit");
+    }
     {
         int gb = ((d.W * d.H + 15) / 16) * 16;
         h->obs_grid = gb <= 64 * 1024 ? gb : 0;
@@ -569,6 +601,9 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
             return fail(ZS_EHIP, std::string("k_init_obstacles: ") + hipGetErrorString(le));
         }
     }
+    // every env starts "pending reset": the first zs_step (or zs_reset) builds its world
+    hipLaunchKernelGGL(k_init_pending, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, 0, d, h->d_rlist[0],
+                       h->d_rcount);
     // default seeds: env index (every env has a valid stream even if never seeded)
     std::vector<uint64_t> seeds(N);
     for (size_t i = 0; i < N; i++) seeds[i] = i;
@@ -632,16 +667,16 @@ static int launch_obs(zs_handle* h, void* obs, const uint8_t* mask, hipStream_t 
     return ZS_OK;
 }
 
-static int launch_tick(zs_handle* h, int mode, const uint8_t* mask, const int32_t* actions, double* rew,
-                       uint8_t* done, uint8_t* trunc, uint8_t* listed, uint8_t* reset_out, hipStream_t s) {
+static int launch_tick(zs_handle* h, const int32_t* actions, double* rew, uint8_t* done, uint8_t* trunc,
+                       uint8_t* listed, uint8_t* reset_out, int* rlist, int* rcount, hipStream_t s) {
     const Dev& d = h->d;
     const int ne = 64 / h->G;
     unsigned grid = (unsigned)((d.N + ne - 1) / ne);
     int i0 = -1, i1 = -1;
     if (h->prof) HIPCHK(hipEventRecord(prof_event(h, &i0), s));
-#define ZS_TICK(GG)                                                                                                  \
-    hipLaunchKernelGGL(k_tick<GG>, dim3(grid), dim3(64), h->lds, s, d, mode, mask, actions, rew, done, trunc, listed, \
-                       reset_out, h->d_err)
+#define ZS_TICK(GG)                                                                                                \
+    hipLaunchKernelGGL(k_tick<GG>, dim3(grid), dim3(64), h->lds, s, d, actions, rew, done, trunc, listed, reset_out, \
+                       rlist, rcount)
     switch (h->G) {
     case 1: ZS_TICK(1); break;
     case 2: ZS_TICK(2); break;
@@ -660,12 +695,28 @@ static int launch_tick(zs_handle* h, int mode, const uint8_t* mask, const int32_
     return ZS_OK;
 }
 
+static int launch_reset(zs_handle* h, int list_mode, const uint8_t* mask, hipStream_t s) {
+    const Dev& d = h->d;
+    unsigned grid = (unsigned)std::min(d.N, list_mode ? 512 : 4096);
+    int p = h->rpar;
+    int i0 = -1, i1 = -1;
+    if (h->prof) HIPCHK(hipEventRecord(prof_event(h, &i0), s));
+    hipLaunchKernelGGL(k_reset, dim3(grid), dim3(64), h->reset_lds, s, d, list_mode, h->d_rlist[p], h->d_rcount + p,
+                       list_mode ? h->d_rcount + (1 - p) : nullptr, mask, h->d_err);
+    HIPCHK(hipGetLastError());
+    if (h->prof) {
+        HIPCHK(hipEventRecord(prof_event(h, &i1), s));
+        h->ev_reset.push_back({i0, i1});
+    }
+    return ZS_OK;
+}
+
 extern "C" int zs_reset(zs_handle* h, const uint8_t* env_mask_dev, void* obs_dev, void* stream) {
     if (!h) return fail(ZS_EINVAL, "null handle");
     hipStream_t s = (hipStream_t)stream;
     HIPCHK(hipSetDevice(h->device));
     HIPCHK(hipMemsetAsync(h->d_err, 0, sizeof(int), s));
-    int rc = launch_tick(h, MODE_RESET, env_mask_dev, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, s);
+    int rc = launch_reset(h, 0, env_mask_dev, s);
     if (rc) return rc;
     rc = launch_obs(h, obs_dev, env_mask_dev, s);
     if (rc) return rc;
@@ -682,8 +733,16 @@ extern "C" int zs_step(zs_handle* h, const int32_t* actions_dev, void* obs_dev, 
     if (!h || !actions_dev || !rewards_dev || !done_dev || !trunc_dev) return fail(ZS_EINVAL, "null argument");
     hipStream_t s = (hipStream_t)stream;
     HIPCHK(hipSetDevice(h->device));
-    int rc = launch_tick(h, MODE_STEP, nullptr, actions_dev, rewards_dev, done_dev, trunc_dev, listed_dev, reset_dev, s);
+    // 1) rebuild the envs that ended at the previous call (and clear the list k_tick fills now)
+    int rc = launch_reset(h, 1, nullptr, s);
     if (rc) return rc;
+    // 2) tick every other env; envs that end now are queued for the next call
+    int q = 1 - h->rpar;
+    rc = launch_tick(h, actions_dev, rewards_dev, done_dev, trunc_dev, listed_dev, reset_dev, h->d_rlist[q],
+                     h->d_rcount + q, s);
+    if (rc) return rc;
+    h->rpar = q;
+    // 3) observations of every env
     return launch_obs(h, obs_dev, nullptr, s);
 }
 
@@ -736,6 +795,7 @@ extern "C" int zs_profile(zs_handle* h, int32_t enable) {
     h->prof = enable ? 1 : 0;
     h->ev_tick.clear();
     h->ev_obs.clear();
+    h->ev_reset.clear();
     h->ev_next = 0;
     return ZS_OK;
 }
@@ -743,9 +803,9 @@ extern "C" int zs_profile(zs_handle* h, int32_t enable) {
 extern "C" int zs_profile_read(zs_handle* h, double* out) {
     if (!h || !out) return fail(ZS_EINVAL, "null argument");
     HIPCHK(hipSetDevice(h->device));
-    double tot[2] = {0.0, 0.0};
-    std::vector<std::pair<int, int>>* lists[2] = {&h->ev_tick, &h->ev_obs};
-    for (int k = 0; k < 2; k++)
+    double tot[3] = {0.0, 0.0, 0.0};
+    std::vector<std::pair<int, int>>* lists[3] = {&h->ev_tick, &h->ev_obs, &h->ev_reset};
+    for (int k = 0; k < 3; k++)
         for (auto& pr : *lists[k]) {
             HIPCHK(hipEventSynchronize(h->ev_pool[pr.second]));
             float ms = 0.f;
@@ -756,8 +816,11 @@ extern "C" int zs_profile_read(zs_handle* h, double* out) {
     out[1] = (double)h->ev_tick.size();
     out[2] = tot[1];
     out[3] = (double)h->ev_obs.size();
+    out[4] = tot[2];
+    out[5] = (double)h->ev_reset.size();
     h->ev_tick.clear();
     h->ev_obs.clear();
+    h->ev_reset.clear();
     h->ev_next = 0;
     return ZS_OK;
 }

@@ -1,0 +1,309 @@
+// zs_reset.hpp — k_reset: Game.__initialize_world__ (game.py:151-169) for one env per wave.
+//
+// A reset is the longest serial RNG consumer of the hot path: each spawn_in_random
+// (core.py:40-66) filters the candidate cells and Fisher-Yates-shuffles ALL of them
+// (bridge64: 40 player + 232 zombie cells, ~400 MT words; maps without zombie spawns:
+// every free cell).  Here the whole wave works on one env:
+//   * the candidate filter is a ballot compaction over 64 cells at a time;
+//   * the MT stream is held one word per lane; each randbelow (random.py:239-249) is
+//     one ballot over "lane >= pos && (word >> (32-k)) < n" — the first set bit is the
+//     accepted word, so rejection sampling costs no serial memory round trips;
+//   * when the block of 624 words runs out the wave twists the next one cooperatively.
+// Envs to reset come from a device work list written by k_tick (next-step autoreset) or
+// from an env mask (zs_reset).
+#pragma once
+#include "zs_tick.hpp"
+
+struct WaveRng {
+    uint32_t st;    // ring state of this lane block's word 0 (uniform)
+    int pos;        // next unconsumed word within the block (uniform)
+    uint32_t word;  // this lane's tempered word
+    uint32_t* ring;
+    lu32* tw;       // 2 x 624 words of LDS for the cooperative twist
+};
+
+__device__ __forceinline__ void wave_twist(WaveRng& r, uint32_t slot) {
+    const int lane = threadIdx.x;
+    const uint32_t* src = r.ring + slot * ZS_MT_N;
+    uint32_t* dst = r.ring + (slot ^ 1u) * ZS_MT_N;
+    for (int k = lane; k < ZS_MT_N; k += 64) r.tw[k] = src[k];
+    __syncthreads();
+    lu32* nw = r.tw + ZS_MT_N;
+    for (int k = lane; k < ZS_MT_N - ZS_MT_M; k += 64) nw[k] = mt_f(r.tw[k], r.tw[k + 1], r.tw[k + ZS_MT_M]);
+    __syncthreads();
+    for (int k = (ZS_MT_N - ZS_MT_M) + lane; k < 2 * (ZS_MT_N - ZS_MT_M); k += 64)
+        nw[k] = mt_f(r.tw[k], r.tw[k + 1], nw[k + ZS_MT_M - ZS_MT_N]);
+    __syncthreads();
+    for (int k = 2 * (ZS_MT_N - ZS_MT_M) + lane; k < ZS_MT_N; k += 64)
+        nw[k] = mt_f(r.tw[k], k + 1 < ZS_MT_N ? r.tw[k + 1] : nw[0], nw[k + ZS_MT_M - ZS_MT_N]);
+    __syncthreads();
+    for (int k = lane; k < ZS_MT_N; k += 64) dst[k] = nw[k];
+    __syncthreads();
+}
+
+// load the 64 words that start at ring state st (twisting the next block first if needed)
+__device__ __forceinline__ void wave_rng_load(WaveRng& r, uint32_t st) {
+    uint32_t off = st & 1023u, slot = (st >> 10) & 1u, ready = (st >> 11) & 1u;
+    if (off >= ZS_MT_N) {
+        if (!ready) wave_twist(r, slot);
+        slot ^= 1u;
+        off = 0;
+        ready = 0;
+    }
+    if (off + 64 > ZS_MT_N && !ready) {
+        wave_twist(r, slot);
+        ready = 1;
+    }
+    uint32_t q = off + threadIdx.x;
+    uint32_t w = q < ZS_MT_N ? r.ring[slot * ZS_MT_N + q] : r.ring[(slot ^ 1u) * ZS_MT_N + q - ZS_MT_N];
+    r.word = mt_temper(w);
+    r.st = st_pack(off, slot, ready);
+    r.pos = 0;
+}
+
+// Random._randbelow(n) (random.py:239-249), wave-uniform result
+__device__ __forceinline__ int wave_below(WaveRng& r, int n) {
+    if (n <= 0) return 0;
+    const int k = 32 - __clz(n);
+    const int lane = threadIdx.x;
+    for (;;) {
+        bool acc = lane >= r.pos && (r.word >> (32 - k)) < (uint32_t)n;
+        unsigned long long m = __ballot(acc);
+        if (m) {
+            int p = __ffsll((long long)m) - 1;
+            uint32_t v = __builtin_amdgcn_readlane(r.word, p) >> (32 - k);
+            r.pos = p + 1;
+            return (int)v;
+        }
+        wave_rng_load(r, st_advance(r.st, 64));
+    }
+}
+
+__device__ __forceinline__ int wave_int(WaveRng& r, int a, int b) { return a + wave_below(r, b - a + 1); }
+
+struct ResetLds {
+    lu32* bm;       // occupancy bitmap [DW]
+    lu32* cand;     // candidate cells [ncand]
+    li32* lpos;     // [E]
+    li32* llife;
+    lu8* lweap;
+    lu8* lpres;
+    lu8* lorder;
+    lu8* lslots;    // slots being spawned
+    li32* lists;    // static spawn lists (player then zombie), or unused
+    lu32* tw;
+};
+
+__host__ __device__ inline int reset_lds_bytes(int E, int DW, int ncand, int lists_cap) {
+    int o = DW * 4 + ncand * 4 + 2 * E * 4 + 4 * E + lists_cap * 4;
+    o = ((o + 15) / 16) * 16;
+    return o + 2 * ZS_MT_N * 4;
+}
+
+__device__ __forceinline__ bool rbm_test(const ResetLds& L, int cell) { return (L.bm[cell >> 5] >> (cell & 31)) & 1u; }
+
+// World.spawn_in_random (core.py:40-66) for k slots in L.lslots[0..k): ballot-compacted
+// candidate filter, Fisher-Yates whose first k iterations swap (the popped tail) and whose
+// remaining iterations only consume their draws.  Returns the number of things placed.
+__device__ __forceinline__ int wave_spawn(const Dev& d, const ResetLds& L, WaveRng& r, int e, int k, int which,
+                                          int nlist, int& n_order, int& serial) {
+    const int lane = threadIdx.x;
+    const int total = nlist ? nlist : d.W * d.H;
+    int n = 0;
+    for (int b = 0; b < total; b += 64) {
+        int i = b + lane;
+        int cell = -1;
+        if (i < total) {
+            if (nlist) {
+                int32_t p = d.lists_cap ? L.lists[(which ? d.nps : 0) + i] : (which ? d.zspawn[i] : d.pspawn[i]);
+                cell = unpack_y(p) * d.W + unpack_x(p);
+            } else {
+                cell = (i % d.H) * d.W + i / d.H;  // x-major (core.py:45-47)
+            }
+        }
+        bool fr = cell >= 0 && !rbm_test(L, cell);
+        unsigned long long m = __ballot(fr);
+        if (fr) L.cand[n + __popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)cell;
+        n += __popcll(m);
+    }
+    __syncthreads();
+    const int lim = n - k;
+    for (int i = n - 1; i >= 1; i--) {
+        int j = wave_below(r, i + 1);
+        if (i >= lim && lane == 0) {
+            uint32_t a = L.cand[i], bb = L.cand[j];
+            L.cand[i] = bb;
+            L.cand[j] = a;
+        }
+    }
+    __syncthreads();
+    int placed = min(k, n);
+    if (lane < placed) {
+        int s = L.lslots[lane];
+        int cell = (int)L.cand[n - 1 - lane];
+        L.lpos[s] = pack_xy(cell % d.W, cell / d.W);
+        L.lpres[s] = 1;
+        __hip_atomic_fetch_or(&L.bm[cell >> 5], 1u << (cell & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        L.lorder[n_order + lane] = (uint8_t)s;
+        d.serial[(size_t)s * d.N + e] = (uint32_t)(serial + lane + 1);
+    }
+    n_order += placed;
+    serial += placed;
+    __syncthreads();
+    return placed;
+}
+
+__device__ __forceinline__ void reset_env_wave(const Dev& d, const ResetLds& L, int e, int list_mode, int* err_out) {
+    const int lane = threadIdx.x, N = d.N, E = d.E, A = d.A, P = d.P;
+    // new World: the map's obstacles (all present, HP carried over), no things, no decoration
+    for (int w = lane; w < d.DW; w += 64) {
+        L.bm[w] = d.obstbits[w];
+        d.dead[(size_t)e * d.DW + w] = 0;
+    }
+    int nonpos = 0;
+    for (int w = lane; w < d.OW; w += 64) {
+        int nb = min(32, d.O - 32 * w);
+        d.obst_present[(size_t)e * d.OW + w] = nb == 32 ? 0xffffffffu : ((1u << nb) - 1u);
+        nonpos |= d.obst_nonpos[(size_t)e * d.OW + w] != 0;
+    }
+    int odirty = __ballot(nonpos) != 0ull;
+    for (int s = lane; s < E; s += 64) {
+        L.lpres[s] = 0;
+        L.lpos[s] = d.pos[(size_t)s * N + e];
+        L.llife[s] = d.life[(size_t)s * N + e];
+        L.lweap[s] = d.weapon[(size_t)s * N + e];
+    }
+    WaveRng r;
+    r.ring = d.ring + (size_t)e * ZS_RING_WORDS;
+    r.tw = L.tw;
+    __syncthreads();
+    wave_rng_load(r, d.rngst[e]);
+    // players: Player() picks a random weapon unless its module gives one (things.py:113-116)
+    for (int p = 0; p < P; p++) {
+        int bt = d.bot_types[p], w;
+        if (bt == ZS_BOT_TERMINATOR) w = ZS_WEAPON_SHOTGUN;  // terminator.py:40-42
+        else if (bt == ZS_BOT_SNIPER) w = ZS_WEAPON_RIFLE;   // sniper.py:22-24
+        else {                                               // choice([Gun, Shotgun, Rifle, Knife, Axe])
+            int k = wave_below(r, 5);
+            w = k == 0 ? ZS_WEAPON_GUN : k == 1 ? ZS_WEAPON_SHOTGUN : k == 2 ? ZS_WEAPON_RIFLE : k == 3 ? ZS_WEAPON_KNIFE : ZS_WEAPON_AXE;
+        }
+        if (lane == 0) {
+            L.lweap[A + p] = (uint8_t)w;
+            L.llife[A + p] = 100;
+        }
+    }
+    // agents: WeaponFactory.create_player_weapon (weapons.py:28-45)
+    for (int a = 0; a < A; a++) {
+        int w = d.agent_weapons[a];
+        if (w == ZS_WEAPON_RANDOM) {  // choice([Knife(), Axe(), Gun(), Rifle(), Shotgun()])
+            int k = wave_below(r, 5);
+            w = k == 0 ? ZS_WEAPON_KNIFE : k == 1 ? ZS_WEAPON_AXE : k == 2 ? ZS_WEAPON_GUN : k == 3 ? ZS_WEAPON_RIFLE : ZS_WEAPON_SHOTGUN;
+        }
+        if (lane == 0) {
+            L.lweap[a] = (uint8_t)w;
+            L.llife[a] = 100;
+        }
+    }
+    int n_order = 0, serial = d.scal[S_SERIAL * N + e];
+    int rc = ZS_OK;
+    // spawn_players, spawn_agents (game.py:181-187): fail_if_cant=True
+    for (int i = lane; i < P; i += 64) L.lslots[i] = (uint8_t)(A + i);
+    __syncthreads();
+    if (wave_spawn(d, L, r, e, P, 0, d.nps, n_order, serial) < P) rc = ZS_ENOSPACE;
+    if (rc == ZS_OK) {
+        for (int i = lane; i < A; i += 64) L.lslots[i] = (uint8_t)i;
+        __syncthreads();
+        if (wave_spawn(d, L, r, e, A, 0, d.nps, n_order, serial) < A) rc = ZS_ENOSPACE;
+    }
+    if (rc == ZS_OK) {
+        // spawn_zombies(initial) (game.py:189-194): Zombie() draws randint(50, 100) first
+        int nz = d.initial_zombies;
+        for (int i = 0; i < nz; i++) {
+            int life = wave_int(r, 50, 100);
+            if (lane == 0) {
+                L.llife[A + P + i] = life;
+                L.lweap[A + P + i] = ZS_WEAPON_CLAWS;
+                L.lslots[i] = (uint8_t)(A + P + i);
+            }
+        }
+        __syncthreads();
+        wave_spawn(d, L, r, e, nz, 1, d.nzs, n_order, serial);
+    } else if (lane == 0 && err_out) {
+        atomicMax(err_out, rc);
+    }
+    // the stream must hold its next block for k_tick's window
+    uint32_t stf = st_advance(r.st, r.pos);
+    if (!((stf >> 11) & 1u)) {
+        wave_twist(r, (stf >> 10) & 1u);
+        stf |= 1u << 11;
+    }
+    // write the new world back
+    for (int s = lane; s < E; s += 64) {
+        d.pos[(size_t)s * N + e] = L.lpos[s];
+        d.life[(size_t)s * N + e] = L.llife[s];
+        d.weapon[(size_t)s * N + e] = L.lweap[s];
+        d.present[(size_t)s * N + e] = L.lpres[s];
+        d.order[(size_t)s * N + e] = L.lorder[s];
+    }
+    for (int w = lane; w < d.DW; w += 64) d.occ_bits[(size_t)e * d.DW + w] = L.bm[w];
+    for (int a = lane; a < A; a += 64) {  // reward_tracker.reset / env.agents = possible_agents
+        d.prev_life[(size_t)a * N + e] = L.llife[a];
+        d.listed[(size_t)a * N + e] = 1;
+    }
+    if (lane == 0) {
+        d.scal[S_T * N + e] = -1;
+        d.scal[S_DEATHS * N + e] = 0;
+        d.scal[S_ZD * N + e] = 0;
+        d.scal[S_EPSTEPS * N + e] = 0;
+        d.scal[S_NORDER * N + e] = n_order;
+        d.scal[S_PREVZD * N + e] = 0;
+        d.scal[S_SERIAL * N + e] = serial;
+        d.scal[S_ODIRTY * N + e] = odirty;
+        d.scal[S_NEEDRESET * N + e] = list_mode ? 2 : 0;  // 2: k_tick reports this call as a reset
+        d.rngst[e] = stf;
+    }
+    __syncthreads();
+}
+
+// list_mode: envs list[0..*count) whose needs_reset == 1 (next-step autoreset); clears *count_clear
+// (the list k_tick fills this call).  Otherwise: every env with mask[e] (all if mask == NULL).
+__global__ void __launch_bounds__(64) k_reset(Dev d, int list_mode, const int* list, const int* count,
+                                              int* count_clear, const uint8_t* mask, int* err_out) {
+    extern __shared__ __align__(16) uint8_t smem[];
+    ResetLds L;
+    int o = 0;
+    L.bm = (lu32*)(smem + o);
+    o += d.DW * 4;
+    L.cand = (lu32*)(smem + o);
+    o += d.ncand * 4;
+    L.lpos = (li32*)(smem + o);
+    o += d.E * 4;
+    L.llife = (li32*)(smem + o);
+    o += d.E * 4;
+    L.lweap = (lu8*)(smem + o);
+    o += d.E;
+    L.lpres = (lu8*)(smem + o);
+    o += d.E;
+    L.lorder = (lu8*)(smem + o);
+    o += d.E;
+    L.lslots = (lu8*)(smem + o);
+    o += d.E;
+    L.lists = (li32*)(smem + o);
+    o += d.lists_cap * 4;
+    o = ((o + 15) / 16) * 16;
+    L.tw = (lu32*)(smem + o);
+    if (d.lists_cap)
+        for (int i = threadIdx.x; i < d.nps + d.nzs; i += 64) L.lists[i] = i < d.nps ? d.pspawn[i] : d.zspawn[i - d.nps];
+    if (list_mode && count_clear && blockIdx.x == 0 && threadIdx.x == 0) *count_clear = 0;
+    __syncthreads();
+    const int n = list_mode ? *count : d.N;
+    for (int idx = blockIdx.x; idx < n; idx += gridDim.x) {
+        int e = list_mode ? list[idx] : idx;
+        if (list_mode) {
+            if (d.scal[S_NEEDRESET * d.N + e] != 1) continue;
+        } else if (mask && !mask[e]) {
+            continue;
+        }
+        reset_env_wave(d, L, e, list_mode, err_out);
+    }
+}

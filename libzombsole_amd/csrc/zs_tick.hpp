@@ -50,7 +50,6 @@ __device__ unsigned long long g_stamp_wg[ZS_STAMP_WGS * ZS_NPHASE];
 #define STAMP_DECL
 #define STAMP(k)
 #endif
-enum { MODE_STEP = 0, MODE_RESET = 1 };
 
 // adjacent_positions order (utils.py:34-44)
 __constant__ int c_adj_dx[4] = {0, 0, 1, -1};
@@ -350,55 +349,6 @@ __device__ __forceinline__ void spawn_zombies(const Dev& d, Grp& c, int count) {
         LW(c, s) = ZS_WEAPON_CLAWS;
     }
     spawn_in_random(d, c, k, 1, d.nzs, 0);
-}
-
-// Game.__initialize_world__ (game.py:151-169) after the group has laid the map obstacles into
-// the bitmap and cleared the entity table; plus the reward-tracker / env.agents reset.
-__device__ __forceinline__ int env_reset_leader(const Dev& d, Grp& c) {
-    c.t = -1;
-    c.deaths = 0;
-    c.zd = 0;
-    c.n_order = 0;
-    // the map's obstacles re-entered the world with their carried-over HP (game.py:154-155):
-    // the group set every present bit in the prologue and flagged carried-over dead ones
-    c.odirty = MISC(c, MISC_NONPOS);
-    // players: Player() picks a random weapon unless its module gives one (things.py:113-116)
-    for (int p = 0; p < d.P; p++) {
-        int s = d.A + p, w;
-        int bt = d.bot_types[p];
-        if (bt == ZS_BOT_TERMINATOR) w = ZS_WEAPON_SHOTGUN;  // terminator.py:40-42
-        else if (bt == ZS_BOT_SNIPER) w = ZS_WEAPON_RIFLE;   // sniper.py:22-24
-        else {                                               // choice([Gun, Shotgun, Rifle, Knife, Axe])
-            int k = rng_below(d, c, 5);
-            w = k == 0 ? ZS_WEAPON_GUN : k == 1 ? ZS_WEAPON_SHOTGUN : k == 2 ? ZS_WEAPON_RIFLE : k == 3 ? ZS_WEAPON_KNIFE : ZS_WEAPON_AXE;
-        }
-        LW(c, s) = (uint8_t)w;
-        LL(c, s) = 100;
-    }
-    // agents: WeaponFactory.create_player_weapon (weapons.py:28-45)
-    for (int a = 0; a < d.A; a++) {
-        int w = d.agent_weapons[a];
-        if (w == ZS_WEAPON_RANDOM) {  // choice([Knife(), Axe(), Gun(), Rifle(), Shotgun()])
-            int k = rng_below(d, c, 5);
-            w = k == 0 ? ZS_WEAPON_KNIFE : k == 1 ? ZS_WEAPON_AXE : k == 2 ? ZS_WEAPON_GUN : k == 3 ? ZS_WEAPON_RIFLE : ZS_WEAPON_SHOTGUN;
-        }
-        LW(c, a) = (uint8_t)w;
-        LL(c, a) = 100;
-    }
-    for (int p = 0; p < d.P; p++) LM(c, p) = (uint8_t)(d.A + p);
-    int rc = spawn_in_random(d, c, d.P, 0, d.nps, 1);
-    if (rc) return rc;
-    for (int a = 0; a < d.A; a++) LM(c, a) = (uint8_t)a;
-    rc = spawn_in_random(d, c, d.A, 0, d.nps, 1);
-    if (rc) return rc;
-    spawn_zombies(d, c, d.initial_zombies);
-    c.prevzd = 0;
-    for (int a = 0; a < d.A; a++) {
-        MISC(c, MISC_N + a) = LL(c, a);
-        MISC(c, MISC_N + d.A + a) = 1;
-    }
-    c.epsteps = 0;
-    return ZS_OK;
 }
 
 // ---------------------------------------------------------------------------
@@ -877,9 +827,9 @@ __device__ __forceinline__ void coop_refill(const Dev& d, int base, int count, c
 // k_tick: one workgroup = one wave = 64/G envs
 // ---------------------------------------------------------------------------
 template <int G>
-__global__ void __launch_bounds__(64) k_tick(Dev d, int mode, const uint8_t* mask, const int32_t* actions,
-                                             double* rew, uint8_t* done_out, uint8_t* trunc_out,
-                                             uint8_t* listed_out, uint8_t* reset_out, int* err_out) {
+__global__ void __launch_bounds__(64) k_tick(Dev d, const int32_t* actions, double* rew, uint8_t* done_out,
+                                             uint8_t* trunc_out, uint8_t* listed_out, uint8_t* reset_out,
+                                             int* reset_list, int* reset_count) {
     extern __shared__ __align__(16) uint8_t smem[];
     constexpr int NE = 64 / G;
     const int lane = threadIdx.x, g = lane / G, j = lane - g * G;
@@ -913,19 +863,20 @@ __global__ void __launch_bounds__(64) k_tick(Dev d, int mode, const uint8_t* mas
 
     STAMP_DECL
     STAMP(0);
-    int do_reset = 0, n_order = 0;
+    // needs_reset: 0 step, 1 pending (never stepped), 2 k_reset rebuilt this env for this call
+    int needs_reset = 0, stepping = 0, n_order = 0;
     uint32_t st0 = 0;
     int wlen = 0;
     if (active) {
-        int needs_reset = d.scal[S_NEEDRESET * N + e];
-        do_reset = mode == MODE_RESET ? (mask == nullptr || mask[e]) : needs_reset;
+        needs_reset = d.scal[S_NEEDRESET * N + e];
+        stepping = needs_reset == 0;
         n_order = d.scal[S_NORDER * N + e];
         // stage the entity table
         for (int s = j; s < E; s += G) {
             LP(c, s) = d.pos[(size_t)s * N + e];
             LL(c, s) = d.life[(size_t)s * N + e];
             LW(c, s) = d.weapon[(size_t)s * N + e];
-            LPR(c, s) = do_reset ? 0 : d.present[(size_t)s * N + e];
+            LPR(c, s) = d.present[(size_t)s * N + e];
             LO(c, s) = d.order[(size_t)s * N + e];
         }
         // per-env scalars and the reward tracker / env.agents rows
@@ -943,17 +894,9 @@ __global__ void __launch_bounds__(64) k_tick(Dev d, int mode, const uint8_t* mas
             else v = d.listed[(size_t)(f - MISC_N - A) * N + e];
             MISC(c, f) = v;
         }
-        // occupancy bitmap: persisted one, or the map's obstacles for a new World
-        const uint32_t* src = do_reset ? d.obstbits : d.occ_bits + (size_t)e * d.DW;
+        // occupancy bitmap
+        const uint32_t* src = d.occ_bits + (size_t)e * d.DW;
         for (int w = j; w < d.DW; w += G) c.bm[IX(c, w)] = src[w];
-        if (do_reset) {
-            for (int w = j; w < d.DW; w += G) d.dead[(size_t)e * d.DW + w] = 0;
-            // every map obstacle re-enters the dict (game.py:154-155); flag carried-over dead ones
-            for (int w = j; w < d.OW; w += G) {
-                int nb = min(32, d.O - 32 * w);
-                d.obst_present[(size_t)e * d.OW + w] = nb == 32 ? 0xffffffffu : ((1u << nb) - 1u);
-            }
-        }
         // RNG window: the next words of this env's stream, tempered
         uint32_t st = d.rngst[e];
         uint32_t off = st & 1023u, slot = (st >> 10) & 1u, ready = (st >> 11) & 1u;
@@ -963,7 +906,7 @@ __global__ void __launch_bounds__(64) k_tick(Dev d, int mode, const uint8_t* mas
             ready = 0;
         }
         int maxw = off >= ZS_MT_N ? 0 : (ready ? d.rw_cap : min(d.rw_cap, ZS_MT_N - (int)off));
-        wlen = min(do_reset ? d.rw_cap : d.rw_step, maxw);
+        wlen = min(d.rw_step, maxw);
         const uint32_t* ring = d.ring + (size_t)e * ZS_RING_WORDS;
         for (int i = j; i < wlen; i += G) {
             uint32_t q = off + i;
@@ -973,16 +916,13 @@ __global__ void __launch_bounds__(64) k_tick(Dev d, int mode, const uint8_t* mas
         st0 = st_pack(off, slot, ready);
     }
     __syncthreads();
-    if (active && do_reset)
-        for (int w = j; w < d.OW; w += G)
-            if (d.obst_nonpos[(size_t)e * d.OW + w]) MISC(c, MISC_NONPOS) = 1;
-    if (active && !do_reset && mode == MODE_STEP) {
+    if (active && stepping) {
         // dict-order ranks for closest() tie-breaks
         for (int k = j; k < n_order; k += G) LR(c, LO(c, k)) = (uint8_t)k;
     }
     __syncthreads();
     STAMP(1);
-    if (active && !do_reset && mode == MODE_STEP) {
+    if (active && stepping) {
         // decisions (start-of-tick state), the group's lanes over the actors
         for (int k = j; k < n_order; k += G) {
             int s = LO(c, k), kind, tgt;
@@ -1005,26 +945,24 @@ __global__ void __launch_bounds__(64) k_tick(Dev d, int mode, const uint8_t* mas
         c.prevzd = MISC(c, MISC_PREVZD);
         c.serial = MISC(c, MISC_SERIAL);
         c.odirty = MISC(c, MISC_ODIRTY);
-        int needs_reset = 0;
-        if (do_reset) {
-            int rc = env_reset_leader(d, c);
-            if (rc && err_out) atomicMax(err_out, rc);
-            if (mode == MODE_STEP) {
-                int nr = d.reward_mode == ZS_REWARD_SINGLE ? 1 : A;
-                for (int a = 0; a < nr; a++) rew[(size_t)e * nr + a] = 0.0;
-                done_out[e] = 0;
-                trunc_out[e] = 0;
-                if (listed_out)
-                    for (int a = 0; a < A; a++) listed_out[(size_t)e * A + a] = 1;
-            }
-        } else if (mode == MODE_STEP) {
+        if (needs_reset) {  // this call is the env's reset (obs written by k_obs); outputs as after env.reset()
+            int nr = d.reward_mode == ZS_REWARD_SINGLE ? 1 : A;
+            for (int a = 0; a < nr; a++) rew[(size_t)e * nr + a] = 0.0;
+            done_out[e] = 0;
+            trunc_out[e] = 0;
+            if (listed_out)
+                for (int a = 0; a < A; a++) listed_out[(size_t)e * A + a] = 1;
+            if (needs_reset == 1) reset_list[atomicAdd(reset_count, 1)] = e;  // not yet rebuilt: retry
+            else needs_reset = 0;
+        } else {
             c.t += 1;
             env_step_leader(d, c, actions, rew, done_out, trunc_out, listed_out);
-            if ((done_out[e] || trunc_out[e]) && (d.flags & ZS_FLAG_AUTORESET)) needs_reset = 1;
-        } else {
-            needs_reset = d.scal[S_NEEDRESET * N + e];
+            if ((done_out[e] || trunc_out[e]) && (d.flags & ZS_FLAG_AUTORESET)) {
+                needs_reset = 1;
+                reset_list[atomicAdd(reset_count, 1)] = e;  // rebuilt by k_reset at the next call
+            }
         }
-        if (mode == MODE_STEP && reset_out) reset_out[e] = (uint8_t)do_reset;
+        if (reset_out) reset_out[e] = (uint8_t)(d.scal[S_NEEDRESET * N + e] != 0);
         MISC(c, MISC_T) = c.t;
         MISC(c, MISC_DEATHS) = c.deaths;
         MISC(c, MISC_ZD) = c.zd;

@@ -42,8 +42,9 @@ def main():
         prof = eng.profile_read()
         ssum, smax = eng.debug_stamps()
         wgs = (n_envs + 64 // G - 1) // (64 // G)
-        print("G=%2d  k_tick %.1f us  k_obs %.1f us" % (G, 1e3 * prof["tick_ms"] / prof["tick_n"],
-                                                       1e3 * prof["obs_ms"] / prof["obs_n"]))
+        print("G=%2d  k_tick %.1f us  k_obs %.1f us  k_reset %.1f us" % (
+            G, 1e3 * prof["tick_ms"] / prof["tick_n"], 1e3 * prof["obs_ms"] / prof["obs_n"],
+            1e3 * prof["reset_ms"] / max(prof["reset_n"], 1)))
         for k, name in enumerate(PHASES):
             print("   %-10s mean %9.0f cyc   max %9d cyc" % (name, ssum[k] / (wgs * steps), smax[k]))
         eng.close()
