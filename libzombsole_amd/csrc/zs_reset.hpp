@@ -71,7 +71,8 @@ __device__ __forceinline__ int wave_below(WaveRng& r, int n) {
         unsigned long long m = __ballot(acc);
         if (m) {
             int p = __ffsll((long long)m) - 1;
-            uint32_t v = __builtin_amdgcn_readlane(r.word, p) >> (32 - k);
+            // readlane returns a signed int: shift the word as unsigned
+            uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)r.word, p) >> (32 - k);
             r.pos = p + 1;
             return (int)v;
         }
@@ -127,9 +128,17 @@ __device__ __forceinline__ int wave_spawn(const Dev& d, const ResetLds& L, WaveR
         n += __popcll(m);
     }
     __syncthreads();
+#ifdef ZS_DEBUG_RESET
+    if (lane == 0) printf("e=%d which=%d total=%d k=%d n=%d cand[0]=%u cand[n-1]=%u\n", e, which, total, k, n,
+                          (unsigned)L.cand[0], n > 0 ? (unsigned)L.cand[n - 1] : 0u);
+#endif
     const int lim = n - k;
     for (int i = n - 1; i >= 1; i--) {
         int j = wave_below(r, i + 1);
+#ifdef ZS_DEBUG_RESET
+        if (lane == 0 && e == 2 && which == 0 && k == 2)
+            printf("  swap i=%d j=%d ci=%u cj=%u pos=%d\n", i, j, (unsigned)L.cand[i], (unsigned)L.cand[j], r.pos);
+#endif
         if (i >= lim && lane == 0) {
             uint32_t a = L.cand[i], bb = L.cand[j];
             L.cand[i] = bb;
@@ -138,6 +147,9 @@ __device__ __forceinline__ int wave_spawn(const Dev& d, const ResetLds& L, WaveR
     }
     __syncthreads();
     int placed = min(k, n);
+#ifdef ZS_DEBUG_RESET
+    if (lane < placed) printf("e=%d place lane=%d slot=%d cell=%u\n", e, lane, (int)L.lslots[lane], (unsigned)L.cand[n - 1 - lane]);
+#endif
     if (lane < placed) {
         int s = L.lslots[lane];
         int cell = (int)L.cand[n - 1 - lane];
