@@ -14,12 +14,15 @@
 #pragma once
 #include "zs_tick.hpp"
 
+#define WR_Q 4               // words per lane held in registers
+#define WR_BLOCK (64 * WR_Q)  // words per register block
+
 struct WaveRng {
-    uint32_t st;    // ring state of this lane block's word 0 (uniform)
-    int pos;        // next unconsumed word within the block (uniform)
-    uint32_t word;  // this lane's tempered word
+    uint32_t st;          // ring state of the register block's word 0 (uniform)
+    int pos;              // next unconsumed word within the block (uniform, 0..WR_BLOCK)
+    uint32_t word[WR_Q];  // word[q] = tempered stream word q*64 + lane of the block
     uint32_t* ring;
-    lu32* tw;       // 2 x 624 words of LDS for the cooperative twist
+    lu32* tw;             // 2 x 624 words of LDS for the cooperative twist
 };
 
 __device__ __forceinline__ void wave_twist(WaveRng& r, uint32_t slot) {
@@ -41,7 +44,7 @@ __device__ __forceinline__ void wave_twist(WaveRng& r, uint32_t slot) {
     __syncthreads();
 }
 
-// load the 64 words that start at ring state st (twisting the next block first if needed)
+// load the WR_BLOCK words that start at ring state st (twisting the next block first if needed)
 __device__ __forceinline__ void wave_rng_load(WaveRng& r, uint32_t st) {
     uint32_t off = st & 1023u, slot = (st >> 10) & 1u, ready = (st >> 11) & 1u;
     if (off >= ZS_MT_N) {
@@ -50,15 +53,23 @@ __device__ __forceinline__ void wave_rng_load(WaveRng& r, uint32_t st) {
         off = 0;
         ready = 0;
     }
-    if (off + 64 > ZS_MT_N && !ready) {
+    if (off + WR_BLOCK > ZS_MT_N && !ready) {
         wave_twist(r, slot);
         ready = 1;
     }
-    uint32_t q = off + threadIdx.x;
-    uint32_t w = q < ZS_MT_N ? r.ring[slot * ZS_MT_N + q] : r.ring[(slot ^ 1u) * ZS_MT_N + q - ZS_MT_N];
-    r.word = mt_temper(w);
+#pragma unroll
+    for (int q = 0; q < WR_Q; q++) {
+        uint32_t p = off + q * 64 + threadIdx.x;
+        r.word[q] = p < ZS_MT_N ? r.ring[slot * ZS_MT_N + p] : r.ring[(slot ^ 1u) * ZS_MT_N + p - ZS_MT_N];
+    }
+#pragma unroll
+    for (int q = 0; q < WR_Q; q++) r.word[q] = mt_temper(r.word[q]);
     r.st = st_pack(off, slot, ready);
     r.pos = 0;
+}
+
+__device__ __forceinline__ uint32_t wr_sub(const WaveRng& r, int q) {
+    return q == 0 ? r.word[0] : q == 1 ? r.word[1] : q == 2 ? r.word[2] : r.word[3];
 }
 
 // Random._randbelow(n) (random.py:239-249), wave-uniform result
@@ -67,16 +78,48 @@ __device__ __forceinline__ int wave_below(WaveRng& r, int n) {
     const int k = 32 - __clz(n);
     const int lane = threadIdx.x;
     for (;;) {
-        bool acc = lane >= r.pos && (r.word >> (32 - k)) < (uint32_t)n;
+        if (r.pos >= WR_BLOCK) wave_rng_load(r, st_advance(r.st, WR_BLOCK));
+        const int q = r.pos >> 6, base = q << 6;
+        const uint32_t w = wr_sub(r, q);
+        bool acc = base + lane >= r.pos && (w >> (32 - k)) < (uint32_t)n;
         unsigned long long m = __ballot(acc);
         if (m) {
             int p = __ffsll((long long)m) - 1;
             // readlane returns a signed int: shift the word as unsigned
-            uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)r.word, p) >> (32 - k);
-            r.pos = p + 1;
+            uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)w, p) >> (32 - k);
+            r.pos = base + p + 1;
             return (int)v;
         }
-        wave_rng_load(r, st_advance(r.st, 64));
+        r.pos = base + 64;
+    }
+}
+
+// Consume the draws _randbelow(n), _randbelow(n-1), ..., _randbelow(lo) whose results are not
+// needed (the tail of a Fisher-Yates pass).  Speculate that every word from pos on is accepted
+// (lane l then serves draw n - (l - pos)); one ballot confirms the run up to the first rejected
+// word, which restarts the speculation one word later with n unchanged.
+__device__ __forceinline__ void wave_skip(WaveRng& r, int n, int lo) {
+    const int lane = threadIdx.x;
+    while (n >= lo) {
+        if (r.pos >= WR_BLOCK) wave_rng_load(r, st_advance(r.st, WR_BLOCK));
+        const int q = r.pos >> 6, base = q << 6;
+        const uint32_t w = wr_sub(r, q);
+        const int idx = base + lane - r.pos;  // speculative draw index from pos (>= 0 for live lanes)
+        int nl = n - idx;                     // the bound this word serves if all before were accepted
+        bool live = idx >= 0 && nl >= lo;
+        int kl = 32 - __clz(max(nl, 1));
+        bool rej = live && (w >> (32 - kl)) >= (uint32_t)nl;
+        unsigned long long mr = __ballot(rej);
+        unsigned long long ml = __ballot(live);
+        if (mr) {
+            int p = __ffsll((long long)mr) - 1;       // first rejection: words pos..p-1 accepted
+            n -= (base + p) - r.pos;
+            r.pos = base + p + 1;
+        } else {
+            int last = 63 - __clzll((long long)ml);  // all live words accepted
+            n -= (base + last + 1) - r.pos;
+            r.pos = base + last + 1;
+        }
     }
 }
 
@@ -128,36 +171,29 @@ __device__ __forceinline__ int wave_spawn(const Dev& d, const ResetLds& L, WaveR
         n += __popcll(m);
     }
     __syncthreads();
-#ifdef ZS_DEBUG_RESET
-    if (lane == 0) printf("e=%d which=%d total=%d k=%d n=%d cand[0]=%u cand[n-1]=%u\n", e, which, total, k, n,
-                          (unsigned)L.cand[0], n > 0 ? (unsigned)L.cand[n - 1] : 0u);
-#endif
-    const int lim = n - k;
-    for (int i = n - 1; i >= 1; i--) {
+    // random.shuffle: for i = n-1 .. 1, j = _randbelow(i+1), swap.  Iterations i >= n-k decide the
+    // k popped cells; the rest only consume their draws.
+    const int lim = max(n - k, 1);
+    int i = n - 1;
+    for (; i >= lim; i--) {
         int j = wave_below(r, i + 1);
-#ifdef ZS_DEBUG_RESET
-        if (lane == 0 && e == 2 && which == 0 && k == 2)
-            printf("  swap i=%d j=%d ci=%u cj=%u pos=%d\n", i, j, (unsigned)L.cand[i], (unsigned)L.cand[j], r.pos);
-#endif
-        if (i >= lim && lane == 0) {
+        if (lane == 0) {
             uint32_t a = L.cand[i], bb = L.cand[j];
             L.cand[i] = bb;
             L.cand[j] = a;
         }
     }
+    if (i >= 1) wave_skip(r, i + 1, 2);
     __syncthreads();
     int placed = min(k, n);
-#ifdef ZS_DEBUG_RESET
-    if (lane < placed) printf("e=%d place lane=%d slot=%d cell=%u\n", e, lane, (int)L.lslots[lane], (unsigned)L.cand[n - 1 - lane]);
-#endif
-    if (lane < placed) {
-        int s = L.lslots[lane];
-        int cell = (int)L.cand[n - 1 - lane];
+    for (int m = lane; m < placed; m += 64) {
+        int s = L.lslots[m];
+        int cell = (int)L.cand[n - 1 - m];
         L.lpos[s] = pack_xy(cell % d.W, cell / d.W);
         L.lpres[s] = 1;
         __hip_atomic_fetch_or(&L.bm[cell >> 5], 1u << (cell & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        L.lorder[n_order + lane] = (uint8_t)s;
-        d.serial[(size_t)s * d.N + e] = (uint32_t)(serial + lane + 1);
+        L.lorder[n_order + m] = (uint8_t)s;
+        d.serial[(size_t)s * d.N + e] = (uint32_t)(serial + m + 1);
     }
     n_order += placed;
     serial += placed;
