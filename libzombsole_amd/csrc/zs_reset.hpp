@@ -29,7 +29,7 @@ __device__ __forceinline__ void wave_twist(WaveRng& r, uint32_t slot) {
     const int lane = threadIdx.x;
     const uint32_t* src = r.ring + slot * ZS_MT_N;
     uint32_t* dst = r.ring + (slot ^ 1u) * ZS_MT_N;
-    for (int k = lane; k < ZS_MT_N; k += 64) r.tw[k] = src[k];
+    stage_in(src, ZS_MT_N, lane, 64, r.tw, [](int k) { return k; });
     __syncthreads();
     lu32* nw = r.tw + ZS_MT_N;
     for (int k = lane; k < ZS_MT_N - ZS_MT_M; k += 64) nw[k] = mt_f(r.tw[k], r.tw[k + 1], r.tw[k + ZS_MT_M]);

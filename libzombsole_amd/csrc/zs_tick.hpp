@@ -28,13 +28,33 @@ typedef ZS_LDS int32_t li32;
 typedef ZS_LDS uint16_t lu16;
 typedef ZS_LDS uint8_t lu8;
 
+// Stage n global words into LDS: lane `lane0` of a team of `step` lanes copies elements
+// lane0, lane0 + step, ...  All loads of a chunk of 8 are issued before any LDS store, so one
+// memory latency is paid per chunk instead of one per element.
+template <typename T, typename LT, typename Idx>
+__device__ __forceinline__ void stage_in(const T* src, int n, int lane0, int step, LT* dst, Idx dst_index) {
+    for (int b = lane0; b < n; b += 8 * step) {
+        T v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            int i = b + u * step;
+            v[u] = src[i < n ? i : n - 1];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            int i = b + u * step;
+            if (i < n) dst[dst_index(i)] = v[u];
+        }
+    }
+}
+
 enum { K_NONE = 0, K_MOVE = 1, K_ATTACK = 2, K_HEAL = 3, K_DEFER = 4 };
 
 // Diagnostic build only (-DZS_STAMPS, never the product .so): lane 0 of every workgroup adds the
 // s_memtime ticks each k_tick phase took into its own slot g_stamp_wg[block][phase] (plain
 // stores, no contended atomics); zs_debug_stamps sums / maxes the slots on the host.
 #ifdef ZS_STAMPS
-#define ZS_NPHASE 8
+#define ZS_NPHASE 12
 #define ZS_STAMP_WGS 65536
 __device__ unsigned long long g_stamp_wg[ZS_STAMP_WGS * ZS_NPHASE];
 #define STAMP_DECL unsigned long long _st_prev = 0;
@@ -46,9 +66,20 @@ __device__ unsigned long long g_stamp_wg[ZS_STAMP_WGS * ZS_NPHASE];
             g_stamp_wg[blockIdx.x * ZS_NPHASE + (k)-1] += _t - _st_prev;                  \
         _st_prev = _t;                                                                    \
     } while (0)
+#define SUB_DECL unsigned long long _sub_prev;
+#define SUB(k)                                                                            \
+    do {                                                                                  \
+        unsigned long long _t;                                                            \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");      \
+        if ((k) > 0 && blockIdx.x < ZS_STAMP_WGS && c.g == 0)                             \
+            g_stamp_wg[blockIdx.x * ZS_NPHASE + 6 + (k)-1] += _t - _sub_prev;             \
+        _sub_prev = _t;                                                                   \
+    } while (0)
 #else
 #define STAMP_DECL
 #define STAMP(k)
+#define SUB_DECL
+#define SUB(k)
 #endif
 
 // adjacent_positions order (utils.py:34-44)
@@ -638,6 +669,8 @@ __device__ __forceinline__ void rules_check(const Dev& d, const Grp& c, int& end
 __device__ __forceinline__ void env_step_leader(const Dev& d, Grp& c, const int32_t* actions, double* rew, uint8_t* done_out,
                                 uint8_t* trunc_out, uint8_t* listed_out) {
     const int A = d.A, E = d.E;
+    SUB_DECL
+    SUB(0);
     // World.get_actions (core.py:80-101): deferred (RNG-drawing) decisions in dict order
     int nact = 0;
     for (int k = 0; k < c.n_order; k++) {
@@ -657,6 +690,7 @@ __device__ __forceinline__ void env_step_leader(const Dev& d, Grp& c, const int3
         LPE(c, i) = LPE(c, j);
         LPE(c, j) = tmp;
     }
+    SUB(1);
     // execute_actions (core.py:103-119)
     int nmoved = 0;
     for (int i = 0; i < nact; i++) {
@@ -687,6 +721,7 @@ __device__ __forceinline__ void env_step_leader(const Dev& d, Grp& c, const int3
             }
         }
     }
+    SUB(2);
     {  // dict order after the tick's moves: unmoved in old order, then movers in execution order
         int m = 0;
         for (int k = 0; k < c.n_order; k++) {
@@ -731,6 +766,7 @@ __device__ __forceinline__ void env_step_leader(const Dev& d, Grp& c, const int3
         }
         c.n_order = m;
     }
+    SUB(3);
     // reward_tracker.update (gym/reward.py:30-35, 77-86)
     double rs = 0.0;
     if (d.reward_mode == ZS_REWARD_SINGLE) {
@@ -791,6 +827,7 @@ __device__ __forceinline__ void env_step_leader(const Dev& d, Grp& c, const int3
     if (d.max_steps > 0 && c.epsteps >= d.max_steps) tr = 1;
     done_out[c.e] = (uint8_t)ended;
     trunc_out[c.e] = (uint8_t)tr;
+    SUB(4);
 }
 
 // ---------------------------------------------------------------------------
@@ -806,7 +843,7 @@ __device__ __forceinline__ void coop_refill(const Dev& d, int base, int count, c
         uint32_t* ring = d.ring + (size_t)(base + i) * ZS_RING_WORDS;
         const uint32_t* src = ring + slot * ZS_MT_N;
         uint32_t* dst = ring + (slot ^ 1u) * ZS_MT_N;
-        for (int k = tid; k < ZS_MT_N; k += nt) tw[k] = src[k];
+        stage_in(src, ZS_MT_N, tid, nt, tw, [](int k) { return k; });
         __syncthreads();
         lu32* nw = tw + ZS_MT_N;
         for (int k = tid; k < ZS_MT_N - ZS_MT_M; k += nt) nw[k] = mt_f(tw[k], tw[k + 1], tw[k + ZS_MT_M]);
@@ -871,13 +908,35 @@ __global__ void __launch_bounds__(64) k_tick(Dev d, const int32_t* actions, doub
         needs_reset = d.scal[S_NEEDRESET * N + e];
         stepping = needs_reset == 0;
         n_order = d.scal[S_NORDER * N + e];
-        // stage the entity table
-        for (int s = j; s < E; s += G) {
-            LP(c, s) = d.pos[(size_t)s * N + e];
-            LL(c, s) = d.life[(size_t)s * N + e];
-            LW(c, s) = d.weapon[(size_t)s * N + e];
-            LPR(c, s) = d.present[(size_t)s * N + e];
-            LO(c, s) = d.order[(size_t)s * N + e];
+        // stage the entity table (SoA [slot][N]: this env's column)
+        {
+            auto ix = [&](int s) { return IX(c, s); };
+            const int32_t* pcol = d.pos + e;
+            const int32_t* lcol = d.life + e;
+            for (int b = j; b < E; b += 4 * G) {
+                int32_t vp[4], vl[4];
+                uint8_t vw[4], vr[4], vo[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    int s = min(b + u * G, E - 1);
+                    vp[u] = pcol[(size_t)s * N];
+                    vl[u] = lcol[(size_t)s * N];
+                    vw[u] = d.weapon[(size_t)s * N + e];
+                    vr[u] = d.present[(size_t)s * N + e];
+                    vo[u] = d.order[(size_t)s * N + e];
+                }
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    int s = b + u * G;
+                    if (s < E) {
+                        c.lpos[ix(s)] = vp[u];
+                        c.llife[ix(s)] = vl[u];
+                        c.lweap[ix(s)] = vw[u];
+                        c.lpres[ix(s)] = vr[u];
+                        c.lorder[ix(s)] = vo[u];
+                    }
+                }
+            }
         }
         // per-env scalars and the reward tracker / env.agents rows
         for (int f = j; f < MISC_N + 2 * A; f += G) {
@@ -895,8 +954,7 @@ __global__ void __launch_bounds__(64) k_tick(Dev d, const int32_t* actions, doub
             MISC(c, f) = v;
         }
         // occupancy bitmap
-        const uint32_t* src = d.occ_bits + (size_t)e * d.DW;
-        for (int w = j; w < d.DW; w += G) c.bm[IX(c, w)] = src[w];
+        stage_in(d.occ_bits + (size_t)e * d.DW, d.DW, j, G, c.bm, [&](int w) { return IX(c, w); });
         // RNG window: the next words of this env's stream, tempered
         uint32_t st = d.rngst[e];
         uint32_t off = st & 1023u, slot = (st >> 10) & 1u, ready = (st >> 11) & 1u;
@@ -908,10 +966,16 @@ __global__ void __launch_bounds__(64) k_tick(Dev d, const int32_t* actions, doub
         int maxw = off >= ZS_MT_N ? 0 : (ready ? d.rw_cap : min(d.rw_cap, ZS_MT_N - (int)off));
         wlen = min(d.rw_step, maxw);
         const uint32_t* ring = d.ring + (size_t)e * ZS_RING_WORDS;
-        for (int i = j; i < wlen; i += G) {
-            uint32_t q = off + i;
-            uint32_t w = q < ZS_MT_N ? ring[slot * ZS_MT_N + q] : ring[(slot ^ 1u) * ZS_MT_N + q - ZS_MT_N];
-            c.rw[IX(c, i)] = mt_temper(w);
+        for (int b = j; b < wlen; b += 8 * G) {
+            uint32_t v[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                uint32_t q = off + min(b + u * G, wlen - 1);
+                v[u] = q < ZS_MT_N ? ring[slot * ZS_MT_N + q] : ring[(slot ^ 1u) * ZS_MT_N + q - ZS_MT_N];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++)
+                if (b + u * G < wlen) c.rw[IX(c, b + u * G)] = mt_temper(v[u]);
         }
         st0 = st_pack(off, slot, ready);
     }
@@ -962,7 +1026,7 @@ __global__ void __launch_bounds__(64) k_tick(Dev d, const int32_t* actions, doub
                 reset_list[atomicAdd(reset_count, 1)] = e;  // rebuilt by k_reset at the next call
             }
         }
-        if (reset_out) reset_out[e] = (uint8_t)(d.scal[S_NEEDRESET * N + e] != 0);
+        if (reset_out) reset_out[e] = (uint8_t)(stepping == 0);
         MISC(c, MISC_T) = c.t;
         MISC(c, MISC_DEATHS) = c.deaths;
         MISC(c, MISC_ZD) = c.zd;
