@@ -203,6 +203,8 @@ __device__ __forceinline__ int wave_spawn(const Dev& d, const ResetLds& L, WaveR
 
 __device__ __forceinline__ void reset_env_wave(const Dev& d, const ResetLds& L, int e, int list_mode, int* err_out) {
     const int lane = threadIdx.x, N = d.N, E = d.E, A = d.A, P = d.P;
+    RST_DECL
+    RST(0);
     // new World: the map's obstacles (all present, HP carried over), no things, no decoration
     for (int w = lane; w < d.DW; w += 64) {
         L.bm[w] = d.obstbits[w];
@@ -226,6 +228,7 @@ __device__ __forceinline__ void reset_env_wave(const Dev& d, const ResetLds& L, 
     r.tw = L.tw;
     __syncthreads();
     wave_rng_load(r, d.rngst[e]);
+    RST(1);
     // players: Player() picks a random weapon unless its module gives one (things.py:113-116)
     for (int p = 0; p < P; p++) {
         int bt = d.bot_types[p], w;
@@ -254,6 +257,7 @@ __device__ __forceinline__ void reset_env_wave(const Dev& d, const ResetLds& L, 
     }
     int n_order = 0, serial = d.scal[S_SERIAL * N + e];
     int rc = ZS_OK;
+    RST(2);
     // spawn_players, spawn_agents (game.py:181-187): fail_if_cant=True
     for (int i = lane; i < P; i += 64) L.lslots[i] = (uint8_t)(A + i);
     __syncthreads();
@@ -263,6 +267,7 @@ __device__ __forceinline__ void reset_env_wave(const Dev& d, const ResetLds& L, 
         __syncthreads();
         if (wave_spawn(d, L, r, e, A, 0, d.nps, n_order, serial) < A) rc = ZS_ENOSPACE;
     }
+    RST(3);
     if (rc == ZS_OK) {
         // spawn_zombies(initial) (game.py:189-194): Zombie() draws randint(50, 100) first
         int nz = d.initial_zombies;
@@ -275,10 +280,13 @@ __device__ __forceinline__ void reset_env_wave(const Dev& d, const ResetLds& L, 
             }
         }
         __syncthreads();
+        RST(4);
         wave_spawn(d, L, r, e, nz, 1, d.nzs, n_order, serial);
+        RST(5);
     } else if (lane == 0 && err_out) {
         atomicMax(err_out, rc);
     }
+    RST(6);
     // the stream must hold its next block for k_tick's window
     uint32_t stf = st_advance(r.st, r.pos);
     if (!((stf >> 11) & 1u)) {
@@ -311,6 +319,7 @@ __device__ __forceinline__ void reset_env_wave(const Dev& d, const ResetLds& L, 
         d.rngst[e] = stf;
     }
     __syncthreads();
+    RST(7);
 }
 
 // list_mode: envs list[0..*count) whose needs_reset == 1 (next-step autoreset); clears *count_clear

@@ -54,7 +54,7 @@ enum { K_NONE = 0, K_MOVE = 1, K_ATTACK = 2, K_HEAL = 3, K_DEFER = 4 };
 // s_memtime ticks each k_tick phase took into its own slot g_stamp_wg[block][phase] (plain
 // stores, no contended atomics); zs_debug_stamps sums / maxes the slots on the host.
 #ifdef ZS_STAMPS
-#define ZS_NPHASE 12
+#define ZS_NPHASE 20
 #define ZS_STAMP_WGS 65536
 __device__ unsigned long long g_stamp_wg[ZS_STAMP_WGS * ZS_NPHASE];
 #define STAMP_DECL unsigned long long _st_prev = 0;
@@ -75,11 +75,22 @@ __device__ unsigned long long g_stamp_wg[ZS_STAMP_WGS * ZS_NPHASE];
             g_stamp_wg[blockIdx.x * ZS_NPHASE + 6 + (k)-1] += _t - _sub_prev;             \
         _sub_prev = _t;                                                                   \
     } while (0)
+#define RST_DECL unsigned long long _r_prev;
+#define RST(k)                                                                            \
+    do {                                                                                  \
+        unsigned long long _t;                                                            \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");      \
+        if ((k) > 0 && blockIdx.x < ZS_STAMP_WGS && threadIdx.x == 0)                     \
+            g_stamp_wg[blockIdx.x * ZS_NPHASE + 12 + (k)-1] += _t - _r_prev;              \
+        _r_prev = _t;                                                                     \
+    } while (0)
 #else
 #define STAMP_DECL
 #define STAMP(k)
 #define SUB_DECL
 #define SUB(k)
+#define RST_DECL
+#define RST(k)
 #endif
 
 // adjacent_positions order (utils.py:34-44)

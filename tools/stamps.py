@@ -10,7 +10,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 SO = os.path.join(ROOT, "libzombsole_amd", "_build", "libzombsole_mi355x_stamps.so")
 PHASES = ["stage-in", "decide", "leader", "stage-out", "mt-refill", "-",
-          "  L:defer+shuffle", "  L:execute", "  L:order+cleanup", "  L:reward+rules"]
+          "  L:defer+shuffle", "  L:execute", "  L:order+cleanup", "  L:reward+rules", "-", "-",
+          "R:setup+rng", "R:weapons", "R:spawn p+a", "R:zombie lives", "R:spawn z", "R:twist+out"]
 
 
 def main():
@@ -36,11 +37,15 @@ def main():
         eng.debug_stamps()
         eng.profile(True)
         steps = 50
+        nres_t = torch.zeros((), dtype=torch.int64, device=eng.device)
         for t in range(31, 31 + steps):
             eng.gen_actions(t, 7)
             eng.step()
+            nres_t += eng.was_reset.sum()
         torch.cuda.synchronize()
         prof = eng.profile_read()
+        nres = int(nres_t.item())
+        print("resets per step: %.1f" % (nres / steps))
         ssum, smax = eng.debug_stamps(len(PHASES))
         wgs = (n_envs + 64 // G - 1) // (64 // G)
         print("G=%2d  k_tick %.1f us  k_obs %.1f us  k_reset %.1f us" % (
@@ -49,7 +54,10 @@ def main():
         for k, name in enumerate(PHASES):
             if name == "-":
                 continue
-            print("   %-10s mean %9.0f cyc   max %9d cyc" % (name, ssum[k] / (wgs * steps), smax[k]))
+            if name.startswith("R:"):  # per reset performed
+                print("   %-10s per-reset %9.0f cyc" % (name, ssum[k] / max(1, nres)))
+            else:
+                print("   %-10s mean %9.0f cyc   max %9d cyc" % (name, ssum[k] / (wgs * steps), smax[k]))
         eng.close()
 
 
