@@ -72,58 +72,66 @@ __device__ __forceinline__ uint32_t wr_sub(const WaveRng& r, int q) {
     return q == 0 ? r.word[0] : q == 1 ? r.word[1] : q == 2 ? r.word[2] : r.word[3];
 }
 
-// Random._randbelow(n) (random.py:239-249), wave-uniform result
-__device__ __forceinline__ int wave_below(WaveRng& r, int n) {
-    if (n <= 0) return 0;
-    const int k = 32 - __clz(n);
+#define WR_H 4  // rejection hypotheses resolved per round
+
+// `count` consecutive draws _randbelow(b_t), b_t = n - t * dstep (dstep 0: a fixed bound; 1: the
+// decreasing bounds of a Fisher-Yates pass), all in wave-uniform control flow.  Draw t consumes
+// words until one word w gives (w >> (32 - bitlen(b_t))) < b_t (random.py:239-249).
+//
+// One round per 64-word sub-block: lane l evaluates its word under each hypothesis "h words of
+// this round before me were rejected" (then it serves draw t = idx - h, idx = l - start), one
+// ballot per hypothesis; the scalar unit walks the chain of first rejections h = 0, 1, 2, ...
+// (up to WR_H per round).  A second pass lets every accepted lane store its draw's value into
+// out[t] for t < krec.  Returns nothing; advances r past the consumed words.
+__device__ __forceinline__ void wave_draws(WaveRng& r, int n, int dstep, int count, int krec, lu32* out) {
     const int lane = threadIdx.x;
-    for (;;) {
+    int done = 0;
+    while (done < count) {
         if (r.pos >= WR_BLOCK) wave_rng_load(r, st_advance(r.st, WR_BLOCK));
-        const int q = r.pos >> 6, base = q << 6;
+        const int q = r.pos >> 6, base = q << 6, start = r.pos - base;
         const uint32_t w = wr_sub(r, q);
-        bool acc = base + lane >= r.pos && (w >> (32 - k)) < (uint32_t)n;
-        unsigned long long m = __ballot(acc);
-        if (m) {
+        const int idx = lane - start;
+        unsigned long long rej[WR_H], live[WR_H];
+#pragma unroll
+        for (int h = 0; h < WR_H; h++) {
+            int t = done + idx - h;            // draw this word serves under hypothesis h
+            bool lv = idx >= h && t < count;
+            int b = n - t * dstep;
+            int kk = 32 - __clz(max(b, 1));
+            bool rj = lv && (w >> (32 - kk)) >= (uint32_t)b;
+            rej[h] = __ballot(rj);
+            live[h] = __ballot(lv);
+        }
+        // resolve the chain of rejections
+        unsigned long long rmask = 0;
+        int c = start, end = start;
+#pragma unroll
+        for (int h = 0; h < WR_H; h++) {
+            const unsigned long long from = c >= 64 ? 0ull : (~0ull << c);
+            unsigned long long m = rej[h] & from, lm = live[h] & from;
+            if (!m) {  // every live word from c on is accepted
+                end = lm ? 64 - __clzll((long long)lm) : c;
+                c = 65;  // resolved
+                break;
+            }
             int p = __ffsll((long long)m) - 1;
-            // readlane returns a signed int: shift the word as unsigned
-            uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)w, p) >> (32 - k);
-            r.pos = base + p + 1;
-            return (int)v;
+            rmask |= 1ull << p;
+            c = p + 1;
+            end = c;
         }
-        r.pos = base + 64;
-    }
-}
-
-// Consume the draws _randbelow(n), _randbelow(n-1), ..., _randbelow(lo) whose results are not
-// needed (the tail of a Fisher-Yates pass).  Speculate that every word from pos on is accepted
-// (lane l then serves draw n - (l - pos)); one ballot confirms the run up to the first rejected
-// word, which restarts the speculation one word later with n unchanged.
-__device__ __forceinline__ void wave_skip(WaveRng& r, int n, int lo) {
-    const int lane = threadIdx.x;
-    while (n >= lo) {
-        if (r.pos >= WR_BLOCK) wave_rng_load(r, st_advance(r.st, WR_BLOCK));
-        const int q = r.pos >> 6, base = q << 6;
-        const uint32_t w = wr_sub(r, q);
-        const int idx = base + lane - r.pos;  // speculative draw index from pos (>= 0 for live lanes)
-        int nl = n - idx;                     // the bound this word serves if all before were accepted
-        bool live = idx >= 0 && nl >= lo;
-        int kl = 32 - __clz(max(nl, 1));
-        bool rej = live && (w >> (32 - kl)) >= (uint32_t)nl;
-        unsigned long long mr = __ballot(rej);
-        unsigned long long ml = __ballot(live);
-        if (mr) {
-            int p = __ffsll((long long)mr) - 1;       // first rejection: words pos..p-1 accepted
-            n -= (base + p) - r.pos;
-            r.pos = base + p + 1;
-        } else {
-            int last = 63 - __clzll((long long)ml);  // all live words accepted
-            n -= (base + last + 1) - r.pos;
-            r.pos = base + last + 1;
+        // accepted lanes in [start, end) store the value of the draw they served
+        const bool mine = lane >= start && lane < end && !((rmask >> lane) & 1ull);
+        const int hl = __popcll(rmask & ((1ull << lane) - 1ull));
+        const int t = done + idx - hl;
+        if (mine && t < krec) {
+            int b = n - t * dstep;
+            out[t] = w >> (32 - (32 - __clz(b)));
         }
+        done += (end - start) - __popcll(rmask);
+        r.pos = base + end;
     }
+    __syncthreads();
 }
-
-__device__ __forceinline__ int wave_int(WaveRng& r, int a, int b) { return a + wave_below(r, b - a + 1); }
 
 struct ResetLds {
     lu32* bm;       // occupancy bitmap [DW]
@@ -135,11 +143,12 @@ struct ResetLds {
     lu8* lorder;
     lu8* lslots;    // slots being spawned
     li32* lists;    // static spawn lists (player then zombie), or unused
+    lu32* jbuf;     // draw results [max(E, 8)]
     lu32* tw;
 };
 
 __host__ __device__ inline int reset_lds_bytes(int E, int DW, int ncand, int lists_cap) {
-    int o = DW * 4 + ncand * 4 + 2 * E * 4 + 4 * E + lists_cap * 4;
+    int o = DW * 4 + ncand * 4 + 2 * E * 4 + 4 * E + lists_cap * 4 + (E + 8) * 4;
     o = ((o + 15) / 16) * 16;
     return o + 2 * ZS_MT_N * 4;
 }
@@ -173,17 +182,15 @@ __device__ __forceinline__ int wave_spawn(const Dev& d, const ResetLds& L, WaveR
     __syncthreads();
     // random.shuffle: for i = n-1 .. 1, j = _randbelow(i+1), swap.  Iterations i >= n-k decide the
     // k popped cells; the rest only consume their draws.
-    const int lim = max(n - k, 1);
-    int i = n - 1;
-    for (; i >= lim; i--) {
-        int j = wave_below(r, i + 1);
-        if (lane == 0) {
+    const int ndraw = max(n - 1, 0), nswap = min(k, ndraw);
+    wave_draws(r, n, 1, ndraw, nswap, L.jbuf);
+    if (lane == 0)
+        for (int t = 0; t < nswap; t++) {
+            int i = n - 1 - t, j = (int)L.jbuf[t];
             uint32_t a = L.cand[i], bb = L.cand[j];
             L.cand[i] = bb;
             L.cand[j] = a;
         }
-    }
-    if (i >= 1) wave_skip(r, i + 1, 2);
     __syncthreads();
     int placed = min(k, n);
     for (int m = lane; m < placed; m += 64) {
@@ -229,32 +236,37 @@ __device__ __forceinline__ void reset_env_wave(const Dev& d, const ResetLds& L, 
     __syncthreads();
     wave_rng_load(r, d.rngst[e]);
     RST(1);
-    // players: Player() picks a random weapon unless its module gives one (things.py:113-116)
-    for (int p = 0; p < P; p++) {
-        int bt = d.bot_types[p], w;
-        if (bt == ZS_BOT_TERMINATOR) w = ZS_WEAPON_SHOTGUN;  // terminator.py:40-42
-        else if (bt == ZS_BOT_SNIPER) w = ZS_WEAPON_RIFLE;   // sniper.py:22-24
-        else {                                               // choice([Gun, Shotgun, Rifle, Knife, Axe])
-            int k = wave_below(r, 5);
-            w = k == 0 ? ZS_WEAPON_GUN : k == 1 ? ZS_WEAPON_SHOTGUN : k == 2 ? ZS_WEAPON_RIFLE : k == 3 ? ZS_WEAPON_KNIFE : ZS_WEAPON_AXE;
-        }
-        if (lane == 0) {
+    // players: Player() picks a random weapon unless its module gives one (things.py:113-116);
+    // agents: WeaponFactory.create_player_weapon (weapons.py:28-45).  Each random pick is one
+    // _randbelow(5), in bots-then-agents order.
+    int nrw = 0;
+    for (int p = 0; p < P; p++) nrw += d.bot_types[p] != ZS_BOT_TERMINATOR && d.bot_types[p] != ZS_BOT_SNIPER;
+    for (int a = 0; a < A; a++) nrw += d.agent_weapons[a] == ZS_WEAPON_RANDOM;
+    if (nrw) wave_draws(r, 5, 0, nrw, nrw, L.jbuf);
+    if (lane == 0) {
+        int t = 0;
+        for (int p = 0; p < P; p++) {
+            int bt = d.bot_types[p], w;
+            if (bt == ZS_BOT_TERMINATOR) w = ZS_WEAPON_SHOTGUN;  // terminator.py:40-42
+            else if (bt == ZS_BOT_SNIPER) w = ZS_WEAPON_RIFLE;   // sniper.py:22-24
+            else {                                               // choice([Gun, Shotgun, Rifle, Knife, Axe])
+                int k = (int)L.jbuf[t++];
+                w = k == 0 ? ZS_WEAPON_GUN : k == 1 ? ZS_WEAPON_SHOTGUN : k == 2 ? ZS_WEAPON_RIFLE : k == 3 ? ZS_WEAPON_KNIFE : ZS_WEAPON_AXE;
+            }
             L.lweap[A + p] = (uint8_t)w;
             L.llife[A + p] = 100;
         }
-    }
-    // agents: WeaponFactory.create_player_weapon (weapons.py:28-45)
-    for (int a = 0; a < A; a++) {
-        int w = d.agent_weapons[a];
-        if (w == ZS_WEAPON_RANDOM) {  // choice([Knife(), Axe(), Gun(), Rifle(), Shotgun()])
-            int k = wave_below(r, 5);
-            w = k == 0 ? ZS_WEAPON_KNIFE : k == 1 ? ZS_WEAPON_AXE : k == 2 ? ZS_WEAPON_GUN : k == 3 ? ZS_WEAPON_RIFLE : ZS_WEAPON_SHOTGUN;
-        }
-        if (lane == 0) {
+        for (int a = 0; a < A; a++) {
+            int w = d.agent_weapons[a];
+            if (w == ZS_WEAPON_RANDOM) {  // choice([Knife(), Axe(), Gun(), Rifle(), Shotgun()])
+                int k = (int)L.jbuf[t++];
+                w = k == 0 ? ZS_WEAPON_KNIFE : k == 1 ? ZS_WEAPON_AXE : k == 2 ? ZS_WEAPON_GUN : k == 3 ? ZS_WEAPON_RIFLE : ZS_WEAPON_SHOTGUN;
+            }
             L.lweap[a] = (uint8_t)w;
             L.llife[a] = 100;
         }
     }
+    __syncthreads();
     int n_order = 0, serial = d.scal[S_SERIAL * N + e];
     int rc = ZS_OK;
     RST(2);
@@ -271,15 +283,16 @@ __device__ __forceinline__ void reset_env_wave(const Dev& d, const ResetLds& L, 
     if (rc == ZS_OK) {
         // spawn_zombies(initial) (game.py:189-194): Zombie() draws randint(50, 100) first
         int nz = d.initial_zombies;
-        for (int i = 0; i < nz; i++) {
-            int life = wave_int(r, 50, 100);
-            if (lane == 0) {
-                L.llife[A + P + i] = life;
-                L.lweap[A + P + i] = ZS_WEAPON_CLAWS;
-                L.lslots[i] = (uint8_t)(A + P + i);
+        for (int b0 = 0; b0 < nz; b0 += d.E + 8) {  // randint(50, 100) = 50 + _randbelow(51) each
+            int cnt = min(nz - b0, d.E + 8);
+            wave_draws(r, 51, 0, cnt, cnt, L.jbuf);
+            for (int i = lane; i < cnt; i += 64) {
+                L.llife[A + P + b0 + i] = 50 + (int)L.jbuf[i];
+                L.lweap[A + P + b0 + i] = ZS_WEAPON_CLAWS;
+                L.lslots[b0 + i] = (uint8_t)(A + P + b0 + i);
             }
+            __syncthreads();
         }
-        __syncthreads();
         RST(4);
         wave_spawn(d, L, r, e, nz, 1, d.nzs, n_order, serial);
         RST(5);
@@ -347,6 +360,8 @@ __global__ void __launch_bounds__(64) k_reset(Dev d, int list_mode, const int* l
     o += d.E;
     L.lists = (li32*)(smem + o);
     o += d.lists_cap * 4;
+    L.jbuf = (lu32*)(smem + o);
+    o += (d.E + 8) * 4;
     o = ((o + 15) / 16) * 16;
     L.tw = (lu32*)(smem + o);
     if (d.lists_cap)
