@@ -90,6 +90,15 @@ __device__ __forceinline__ int unpack_y(int32_t p) { return (int)(p >> 16); }
 // the rare slow path, cooperatively by a whole wave in zs_rng_refill).
 // rngst packs: offset (bits 0..9), current slot (bit 10), next-ready (bit 11).
 // ---------------------------------------------------------------------------
+// Lane hand-off through LDS inside a one-wave workgroup.  LDS instructions of a wave execute in
+// program order, so lanes only need the compiler kept from reordering across this point; unlike
+// __syncthreads() (a workgroup release fence) it does not wait for outstanding global stores.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
     y ^= (y >> 11);
     y ^= (y << 7) & 0x9d2c5680u;

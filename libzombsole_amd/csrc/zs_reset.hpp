@@ -30,18 +30,18 @@ __device__ __forceinline__ void wave_twist(WaveRng& r, uint32_t slot) {
     const uint32_t* src = r.ring + slot * ZS_MT_N;
     uint32_t* dst = r.ring + (slot ^ 1u) * ZS_MT_N;
     stage_in(src, ZS_MT_N, lane, 64, r.tw, [](int k) { return k; });
-    __syncthreads();
+    wave_sync();
     lu32* nw = r.tw + ZS_MT_N;
     for (int k = lane; k < ZS_MT_N - ZS_MT_M; k += 64) nw[k] = mt_f(r.tw[k], r.tw[k + 1], r.tw[k + ZS_MT_M]);
-    __syncthreads();
+    wave_sync();
     for (int k = (ZS_MT_N - ZS_MT_M) + lane; k < 2 * (ZS_MT_N - ZS_MT_M); k += 64)
         nw[k] = mt_f(r.tw[k], r.tw[k + 1], nw[k + ZS_MT_M - ZS_MT_N]);
-    __syncthreads();
+    wave_sync();
     for (int k = 2 * (ZS_MT_N - ZS_MT_M) + lane; k < ZS_MT_N; k += 64)
         nw[k] = mt_f(r.tw[k], k + 1 < ZS_MT_N ? r.tw[k + 1] : nw[0], nw[k + ZS_MT_M - ZS_MT_N]);
-    __syncthreads();
+    wave_sync();
     for (int k = lane; k < ZS_MT_N; k += 64) dst[k] = nw[k];
-    __syncthreads();
+    __syncthreads();  // the new block's global stores complete before the wave re-reads it
 }
 
 // load the WR_BLOCK words that start at ring state st (twisting the next block first if needed)
@@ -130,7 +130,7 @@ __device__ __forceinline__ void wave_draws(WaveRng& r, int n, int dstep, int cou
         done += (end - start) - __popcll(rmask);
         r.pos = base + end;
     }
-    __syncthreads();
+    wave_sync();
 }
 
 struct ResetLds {
@@ -179,7 +179,7 @@ __device__ __forceinline__ int wave_spawn(const Dev& d, const ResetLds& L, WaveR
         if (fr) L.cand[n + __popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)cell;
         n += __popcll(m);
     }
-    __syncthreads();
+    wave_sync();
     // random.shuffle: for i = n-1 .. 1, j = _randbelow(i+1), swap.  Iterations i >= n-k decide the
     // k popped cells; the rest only consume their draws.
     const int ndraw = max(n - 1, 0), nswap = min(k, ndraw);
@@ -191,7 +191,7 @@ __device__ __forceinline__ int wave_spawn(const Dev& d, const ResetLds& L, WaveR
             L.cand[i] = bb;
             L.cand[j] = a;
         }
-    __syncthreads();
+    wave_sync();
     int placed = min(k, n);
     for (int m = lane; m < placed; m += 64) {
         int s = L.lslots[m];
@@ -204,7 +204,7 @@ __device__ __forceinline__ int wave_spawn(const Dev& d, const ResetLds& L, WaveR
     }
     n_order += placed;
     serial += placed;
-    __syncthreads();
+    wave_sync();
     return placed;
 }
 
@@ -233,7 +233,7 @@ __device__ __forceinline__ void reset_env_wave(const Dev& d, const ResetLds& L, 
     WaveRng r;
     r.ring = d.ring + (size_t)e * ZS_RING_WORDS;
     r.tw = L.tw;
-    __syncthreads();
+    wave_sync();
     wave_rng_load(r, d.rngst[e]);
     RST(1);
     // players: Player() picks a random weapon unless its module gives one (things.py:113-116);
@@ -266,17 +266,17 @@ __device__ __forceinline__ void reset_env_wave(const Dev& d, const ResetLds& L, 
             L.llife[a] = 100;
         }
     }
-    __syncthreads();
+    wave_sync();
     int n_order = 0, serial = d.scal[S_SERIAL * N + e];
     int rc = ZS_OK;
     RST(2);
     // spawn_players, spawn_agents (game.py:181-187): fail_if_cant=True
     for (int i = lane; i < P; i += 64) L.lslots[i] = (uint8_t)(A + i);
-    __syncthreads();
+    wave_sync();
     if (wave_spawn(d, L, r, e, P, 0, d.nps, n_order, serial) < P) rc = ZS_ENOSPACE;
     if (rc == ZS_OK) {
         for (int i = lane; i < A; i += 64) L.lslots[i] = (uint8_t)i;
-        __syncthreads();
+        wave_sync();
         if (wave_spawn(d, L, r, e, A, 0, d.nps, n_order, serial) < A) rc = ZS_ENOSPACE;
     }
     RST(3);
@@ -291,7 +291,7 @@ __device__ __forceinline__ void reset_env_wave(const Dev& d, const ResetLds& L, 
                 L.lweap[A + P + b0 + i] = ZS_WEAPON_CLAWS;
                 L.lslots[b0 + i] = (uint8_t)(A + P + b0 + i);
             }
-            __syncthreads();
+            wave_sync();
         }
         RST(4);
         wave_spawn(d, L, r, e, nz, 1, d.nzs, n_order, serial);
@@ -331,7 +331,7 @@ __device__ __forceinline__ void reset_env_wave(const Dev& d, const ResetLds& L, 
         d.scal[S_NEEDRESET * N + e] = list_mode ? 2 : 0;  // 2: k_tick reports this call as a reset
         d.rngst[e] = stf;
     }
-    __syncthreads();
+    wave_sync();
     RST(7);
 }
 
@@ -367,7 +367,7 @@ __global__ void __launch_bounds__(64) k_reset(Dev d, int list_mode, const int* l
     if (d.lists_cap)
         for (int i = threadIdx.x; i < d.nps + d.nzs; i += 64) L.lists[i] = i < d.nps ? d.pspawn[i] : d.zspawn[i - d.nps];
     if (list_mode && count_clear && blockIdx.x == 0 && threadIdx.x == 0) *count_clear = 0;
-    __syncthreads();
+    wave_sync();
     const int n = list_mode ? *count : d.N;
     for (int idx = blockIdx.x; idx < n; idx += gridDim.x) {
         int e = list_mode ? list[idx] : idx;

@@ -850,24 +850,25 @@ __device__ __forceinline__ void coop_refill(const Dev& d, int base, int count, c
     for (int i = 0; i < count; i++) {
         uint32_t st = lst[i];
         if ((st >> 11) & 1u) continue;
+        __syncthreads();  // the leader's stores (incl. a serial twist of this block) are complete
         uint32_t slot = (st >> 10) & 1u;
         uint32_t* ring = d.ring + (size_t)(base + i) * ZS_RING_WORDS;
         const uint32_t* src = ring + slot * ZS_MT_N;
         uint32_t* dst = ring + (slot ^ 1u) * ZS_MT_N;
         stage_in(src, ZS_MT_N, tid, nt, tw, [](int k) { return k; });
-        __syncthreads();
+        wave_sync();
         lu32* nw = tw + ZS_MT_N;
         for (int k = tid; k < ZS_MT_N - ZS_MT_M; k += nt) nw[k] = mt_f(tw[k], tw[k + 1], tw[k + ZS_MT_M]);
-        __syncthreads();
+        wave_sync();
         for (int k = (ZS_MT_N - ZS_MT_M) + tid; k < 2 * (ZS_MT_N - ZS_MT_M); k += nt)
             nw[k] = mt_f(tw[k], tw[k + 1], nw[k + ZS_MT_M - ZS_MT_N]);
-        __syncthreads();
+        wave_sync();
         for (int k = 2 * (ZS_MT_N - ZS_MT_M) + tid; k < ZS_MT_N; k += nt)
             nw[k] = mt_f(tw[k], k + 1 < ZS_MT_N ? tw[k + 1] : nw[0], nw[k + ZS_MT_M - ZS_MT_N]);
-        __syncthreads();
+        wave_sync();
         for (int k = tid; k < ZS_MT_N; k += nt) dst[k] = nw[k];
         if (tid == 0) d.rngst[base + i] = st | (1u << 11);
-        __syncthreads();
+        wave_sync();
     }
 }
 
@@ -990,12 +991,12 @@ __global__ void __launch_bounds__(64) k_tick(Dev d, const int32_t* actions, doub
         }
         st0 = st_pack(off, slot, ready);
     }
-    __syncthreads();
+    wave_sync();
     if (active && stepping) {
         // dict-order ranks for closest() tie-breaks
         for (int k = j; k < n_order; k += G) LR(c, LO(c, k)) = (uint8_t)k;
     }
-    __syncthreads();
+    wave_sync();
     STAMP(1);
     if (active && stepping) {
         // decisions (start-of-tick state), the group's lanes over the actors
@@ -1006,7 +1007,7 @@ __global__ void __launch_bounds__(64) k_tick(Dev d, const int32_t* actions, doub
             LT(c, s) = tgt;
         }
     }
-    __syncthreads();
+    wave_sync();
     STAMP(2);
     if (active && leader) {
         c.st0 = st0;
@@ -1051,7 +1052,7 @@ __global__ void __launch_bounds__(64) k_tick(Dev d, const int32_t* actions, doub
         d.rngst[e] = stf;
         lst[g] = stf;
     }
-    __syncthreads();
+    wave_sync();
     STAMP(3);
     if (active) {
         for (int s = j; s < E; s += G) {
@@ -1076,7 +1077,7 @@ __global__ void __launch_bounds__(64) k_tick(Dev d, const int32_t* actions, doub
         }
         for (int w = j; w < d.DW; w += G) d.occ_bits[(size_t)e * d.DW + w] = c.bm[IX(c, w)];
     }
-    __syncthreads();
+    wave_sync();
     STAMP(4);
     coop_refill(d, base, min(NE, N - base), lst, (lu32*)(smem + L.off_bm));
     STAMP(5);
