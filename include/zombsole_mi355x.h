@@ -22,6 +22,10 @@
  *   zs_get_state / zs_set_state
  *                  <- the test pokes env.game.world.things, env.game.agents[i].life = x
  *                     (tests/test_game.py:55,105, tests/test_multiagent_env.py:108)
+ *   zs_observe     <- env.get_observation() (gym_env.py:93-94)
+ *   zs_get_rng / zs_set_rng
+ *                  <- random.getstate()/setstate(): the process-global stream the
+ *                     reference's World/Game draw from (core.py:2, things.py:2, game.py)
  *   zs_gen_actions <- (bench/parity only) the uniform discrete policy of SURVEY.md §8(d)
  *
  * Conventions: plain C types only; device buffers are raw HIP device pointers,
@@ -159,6 +163,11 @@ int zs_seed(zs_handle* h, int32_t env0, int32_t n, const uint64_t* seeds_host, v
  * was not called. */
 int zs_reset(zs_handle* h, const uint8_t* env_mask_dev, void* obs_dev, void* stream);
 
+/* Re-encode the observation of the envs whose mask byte is nonzero (NULL = all)
+ * from their current state — env.get_observation() (gym_env.py:93-94,
+ * gym/multiagent_env.py:87-96), e.g. after a zs_set_state poke. */
+int zs_observe(zs_handle* h, const uint8_t* env_mask_dev, void* obs_dev, void* stream);
+
 /* One lock-step tick for every env.
  *   actions_dev      int32 [N][num_agents][3]  (kind, dx, dy)
  *   obs_dev          [N][obs_per_env][C][H][W] of cfg->obs_dtype
@@ -182,6 +191,14 @@ int zs_gen_actions(zs_handle* h, uint64_t step, int32_t n_discrete, int32_t* act
 int zs_state_size(const zs_handle* h, int32_t* n_words);
 int zs_get_state(zs_handle* h, int32_t env, int32_t* buf_host, void* stream);
 int zs_set_state(zs_handle* h, int32_t env, const int32_t* buf_host, void* stream);
+
+/* One env's MT19937 stream in CPython random.getstate() form (625 words: the raw
+ * 624-word block being consumed, then the index 0..624 of its next word).  The
+ * single-env wrappers move the process-global `random` state through these around
+ * every call, so the engine consumes the same global stream the reference draws
+ * from (zombsole/core.py:1-2 `import random`; random.py:128-168 getstate/setstate). */
+int zs_get_rng(zs_handle* h, int32_t env, uint32_t* state_host, void* stream);
+int zs_set_rng(zs_handle* h, int32_t env, const uint32_t* state_host, void* stream);
 
 /* Diagnostics (not part of the reference surface): when enabled, every k_tick
  * (the step kernel), k_obs (the observation kernel) and k_reset (world rebuild)

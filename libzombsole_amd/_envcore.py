@@ -1,0 +1,79 @@
+"""Shared plumbing of the drop-in envs: one engine env on the GPU driven with the
+process-global `random` stream.
+
+The reference's game draws every random number from CPython's module-global `random`
+(`zombsole/core.py:2`, `things.py:2`, `weapons.py:2`, `players/*.py`), so two envs in one
+process interleave on one stream and `random.seed(s)` before construction / `reset()`
+fixes an episode.  `EnvCore` keeps exactly that contract: around every engine call it
+moves `random.getstate()` into the env's MT19937 slot (`zs_set_rng`) and the advanced
+state back out (`zs_get_rng` -> `random.setstate`).  The tick itself always runs in the
+HIP engine; there is no host fallback.
+"""
+import random
+
+import numpy as np
+
+from . import _abi
+from .actions import ActionError, encode_action
+from .engine import Engine
+from .game import GameView
+
+
+class EnvCore(object):
+    def __init__(self, builder, map_, rules_name, player_names, agent_ids, agent_weapons, initial_zombies,
+                 minimum_zombies, debug, device=None):
+        self.engine = Engine(builder, device=device)
+        self.torch = self.engine.torch
+        self.debug = debug
+        self.game = GameView(self.engine, 0, map_, rules_name, player_names, agent_ids, agent_weapons,
+                             initial_zombies, minimum_zombies, debug)
+        self._host_actions = np.zeros((1, self.engine.A, 3), dtype=np.int32)
+        self.new_world()
+
+    # Game.__initialize_world__ (game.py:151-169) on the engine, drawing from `random`
+    def new_world(self):
+        eng = self.engine
+        eng.load_python_random(0)
+        try:
+            eng.reset()
+        finally:
+            eng.store_python_random(0)
+        self.game.new_episode()
+
+    def encode(self, action):
+        """Agent.next_step's parse of one action dict; errors as World.get_actions treats them
+        (core.py:96-99): re-raised with debug, otherwise the agent idles."""
+        try:
+            return encode_action(action)
+        except ActionError as err:
+            if self.debug:
+                raise err.args[0]
+            return (0, 0, 0)
+
+    def tick(self, triples):
+        """One World.step + env glue for the single engine env; returns host copies of
+        (obs[n_obs, C, H, W], rewards[A], done, truncated)."""
+        eng = self.engine
+        self._host_actions[0, :len(triples)] = np.asarray(triples, dtype=np.int32).reshape(-1, 3)
+        eng.actions.copy_(self.torch.from_numpy(self._host_actions))
+        eng.load_python_random(0)
+        try:
+            eng.step()
+        finally:
+            eng.store_python_random(0)
+            self.game.invalidate()
+        obs = eng.obs[0].cpu().numpy()
+        rew = eng.rewards[0].cpu().numpy()
+        return obs, rew, bool(eng.done[0].item()), bool(eng.trunc[0].item())
+
+    def observe(self):
+        eng = self.engine
+        eng.observe()
+        return eng.obs[0].cpu().numpy()
+
+    def close(self):
+        self.engine.close()
+
+
+def obs_np_dtype(builder):
+    return _abi.DTYPE_NP[builder.cfg.obs_dtype]

@@ -728,6 +728,15 @@ extern "C" int zs_reset(zs_handle* h, const uint8_t* env_mask_dev, void* obs_dev
     return ZS_OK;
 }
 
+// Observation only (the reference's env.get_observation(), gym_env.py:93-94): re-encode the
+// current state of the masked envs, e.g. after a zs_set_state poke.
+extern "C" int zs_observe(zs_handle* h, const uint8_t* env_mask_dev, void* obs_dev, void* stream) {
+    if (!h || !obs_dev) return fail(ZS_EINVAL, "null argument");
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(hipSetDevice(h->device));
+    return launch_obs(h, obs_dev, env_mask_dev, s);
+}
+
 extern "C" int zs_step(zs_handle* h, const int32_t* actions_dev, void* obs_dev, double* rewards_dev, uint8_t* done_dev,
                        uint8_t* trunc_dev, uint8_t* listed_dev, uint8_t* reset_dev, void* stream) {
     if (!h || !actions_dev || !rewards_dev || !done_dev || !trunc_dev) return fail(ZS_EINVAL, "null argument");
@@ -783,6 +792,52 @@ extern "C" int zs_set_state(zs_handle* h, int32_t env, const int32_t* buf_host, 
     HIPCHK(hipMemcpyAsync(h->d_state, buf_host, sizeof(int32_t) * h->state_words, hipMemcpyHostToDevice, s));
     hipLaunchKernelGGL(k_set_state, dim3(1), dim3(64), 0, s, h->d, env, h->d_state);
     HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(s));
+    return ZS_OK;
+}
+
+// ---------------------------------------------------------------------------
+// An env's MT19937 stream in CPython's random.getstate() form: state[0..623] = the raw
+// block being consumed, state[624] = index of the next word (0..624; 624 = exhausted, the
+// next draw twists).  The single-env wrappers move the process-global `random` state in
+// and out of the engine around every call, so the engine draws from exactly the stream the
+// reference's `random` module would (one process-global RNG).
+// ---------------------------------------------------------------------------
+extern "C" int zs_get_rng(zs_handle* h, int32_t env, uint32_t* state_host, void* stream) {
+    if (!h || !state_host) return fail(ZS_EINVAL, "null argument");
+    if (env < 0 || env >= h->d.N) return fail(ZS_EINVAL, "env index out of range");
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(hipSetDevice(h->device));
+    uint32_t st = 0;
+    std::vector<uint32_t> ring(ZS_RING_WORDS);
+    HIPCHK(hipMemcpyAsync(&st, h->d.rngst + env, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(ring.data(), h->d.ring + (size_t)env * ZS_RING_WORDS, sizeof(uint32_t) * ZS_RING_WORDS,
+                          hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    uint32_t off = st & 1023u, slot = (st >> 10) & 1u;
+    std::memcpy(state_host, ring.data() + slot * ZS_MT_N, sizeof(uint32_t) * ZS_MT_N);
+    state_host[ZS_MT_N] = off;
+    return ZS_OK;
+}
+
+extern "C" int zs_set_rng(zs_handle* h, int32_t env, const uint32_t* state_host, void* stream) {
+    if (!h || !state_host) return fail(ZS_EINVAL, "null argument");
+    if (env < 0 || env >= h->d.N) return fail(ZS_EINVAL, "env index out of range");
+    if (state_host[ZS_MT_N] > ZS_MT_N) return fail(ZS_EINVAL, "MT index out of range (0..624)");
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(hipSetDevice(h->device));
+    // slot 0 = the given block, slot 1 = its successor (x[k+624] = x[k+397] ^ f(x[k], x[k+1]))
+    std::vector<uint32_t> ring(ZS_RING_WORDS);
+    std::memcpy(ring.data(), state_host, sizeof(uint32_t) * ZS_MT_N);
+    for (int k = 0; k < ZS_MT_N; k++) {
+        uint32_t a = ring[k], b = ring[k + 1], c = ring[k + ZS_MT_M];
+        uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
+        ring[ZS_MT_N + k] = c ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+    }
+    uint32_t st = state_host[ZS_MT_N] | (0u << 10) | (1u << 11);
+    HIPCHK(hipMemcpyAsync(h->d.ring + (size_t)env * ZS_RING_WORDS, ring.data(), sizeof(uint32_t) * ZS_RING_WORDS,
+                          hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(h->d.rngst + env, &st, sizeof(uint32_t), hipMemcpyHostToDevice, s));
     HIPCHK(hipStreamSynchronize(s));
     return ZS_OK;
 }

@@ -12,8 +12,8 @@ import numpy as np
 from . import _abi
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_build", "libzombsole_mi355x.so")
-SYMBOLS = ["zs_last_error", "zs_create", "zs_destroy", "zs_obs_shape", "zs_seed", "zs_reset", "zs_step",
-           "zs_gen_actions", "zs_state_size", "zs_get_state", "zs_set_state", "zs_profile", "zs_profile_read",
+SYMBOLS = ["zs_last_error", "zs_create", "zs_destroy", "zs_obs_shape", "zs_seed", "zs_reset", "zs_step", "zs_observe",
+           "zs_gen_actions", "zs_state_size", "zs_get_state", "zs_set_state", "zs_get_rng", "zs_set_rng", "zs_profile", "zs_profile_read",
            "zs_debug_stamps"]
 
 _lib = None
@@ -45,10 +45,13 @@ def load_library(path=None):
     L.zs_seed.argtypes = [vp, i32, i32, C.POINTER(u64), vp]
     L.zs_reset.argtypes = [vp, vp, vp, vp]
     L.zs_step.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.zs_observe.argtypes = [vp, vp, vp, vp]
     L.zs_gen_actions.argtypes = [vp, u64, i32, vp, vp]
     L.zs_state_size.argtypes = [vp, C.POINTER(i32)]
     L.zs_get_state.argtypes = [vp, i32, vp, vp]
     L.zs_set_state.argtypes = [vp, i32, vp, vp]
+    L.zs_get_rng.argtypes = [vp, i32, vp, vp]
+    L.zs_set_rng.argtypes = [vp, i32, vp, vp]
     L.zs_profile.argtypes = [vp, i32]
     L.zs_profile_read.argtypes = [vp, C.POINTER(C.c_double)]
     L.zs_debug_stamps.argtypes = [vp, vp, vp, i32]
@@ -152,6 +155,13 @@ class Engine(object):
             _raise(self.L, rc, "zs_step")
         return self.obs, self.rewards, self.done, self.trunc
 
+    def observe(self, mask=None):
+        """Re-encode observations from the current state (after pokes)."""
+        rc = self.L.zs_observe(self.h, _ptr(mask), _ptr(self.obs), self._stream())
+        if rc:
+            _raise(self.L, rc, "zs_observe")
+        return self.obs
+
     def gen_actions(self, step, n_discrete, out=None):
         o = self.actions if out is None else out
         rc = self.L.zs_gen_actions(self.h, int(step), int(n_discrete), _ptr(o), self._stream())
@@ -192,6 +202,34 @@ class Engine(object):
         rc = self.L.zs_set_state(self.h, int(env), C.c_void_p(view.buf.ctypes.data), self._stream())
         if rc:
             _raise(self.L, rc, "zs_set_state")
+
+
+    def get_rng(self, env):
+        """(mt[624] uint32, index) of env's MT19937 stream, CPython getstate() form."""
+        buf = np.zeros(625, dtype=np.uint32)
+        rc = self.L.zs_get_rng(self.h, int(env), C.c_void_p(buf.ctypes.data), self._stream())
+        if rc:
+            _raise(self.L, rc, "zs_get_rng")
+        return buf
+
+    def set_rng(self, env, state):
+        buf = np.ascontiguousarray(np.asarray(state, dtype=np.uint32).reshape(625))
+        rc = self.L.zs_set_rng(self.h, int(env), C.c_void_p(buf.ctypes.data), self._stream())
+        if rc:
+            _raise(self.L, rc, "zs_set_rng")
+
+    def load_python_random(self, env, rnd=None):
+        """Move a `random.Random` (default: the module-global one) state into env."""
+        import random as _random
+        st = (rnd or _random).getstate()
+        self.set_rng(env, np.asarray(st[1], dtype=np.uint64).astype(np.uint32))
+
+    def store_python_random(self, env, rnd=None):
+        """Write env's stream back into a `random.Random` (default: the module-global one)."""
+        import random as _random
+        buf = self.get_rng(env)
+        r = rnd or _random
+        r.setstate((3, tuple(int(v) for v in buf), None))
 
 
 class StateView(object):

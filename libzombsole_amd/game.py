@@ -1,0 +1,255 @@
+"""`env.game` of the drop-in envs: a host view of one engine env shaped like the
+reference's `Game` / `World` (`zombsole/game.py:109-201`, `zombsole/core.py:10-22`).
+
+Nothing here runs game logic — the tick, respawn, rules and rewards all run in the HIP
+engine.  `GameView` reads the env's state record (`zs_get_state`) lazily, caches it until
+the env next changes, and writes pokes back through `zs_set_state`.  The rules objects
+re-evaluate the reference's predicates (`rules/*.py`) on that state so that
+`env.game.rules.game_won()` answers like the reference after a step.
+"""
+from . import _abi
+from .maps import Map, load_map  # noqa: F401  (reference: zombsole.game.Map)
+from .things import OBSTACLE_CLASSES, Agent, DeadBody, ObjectiveLocation, Player, Zombie
+
+BOT_NAMES = {v: k for k, v in _abi._BOTS.items()}
+
+
+class MapView(object):
+    """`game.map`: the parsed map, whose `things` are this env's (shared, HP-carrying)
+    obstacle objects — the same objects `world.things` holds (game.py:154-155)."""
+
+    def __init__(self, map_, obstacles):
+        self._map = map_
+        self._obstacles = obstacles
+
+    def __getattr__(self, name):
+        if name.startswith("_"):
+            raise AttributeError(name)
+        return getattr(self._map, name)
+
+    @property
+    def things(self):
+        return list(self._obstacles) + [ObjectiveLocation(p) for p in self._map.objectives]
+
+
+class WorldView(object):
+    """`core.World` attributes read by user code: size, t, deaths, zombie_deaths, things,
+    decoration (core.py:12-22).  `things` is a fresh dict in the reference's insertion
+    order: present obstacles in map-file order, then dynamic things in dict order."""
+
+    def __init__(self, game):
+        self._game = game
+        self.size = tuple(game.map.size)
+        self.debug = game.debug
+        self.events = []  # the reference's event log is not kept by the engine
+
+    t = property(lambda s: s._game._state().t)
+    deaths = property(lambda s: s._game._state().deaths)
+    zombie_deaths = property(lambda s: s._game._state().zombie_deaths)
+
+    @property
+    def things(self):
+        g = self._game
+        st = g._state()
+        out = {}
+        for i, ob in enumerate(g._obstacles):
+            if st.obst_present[i]:
+                out[ob.position] = ob
+        for slot in st.order[:st.n_order]:
+            v = g._entity(int(slot))
+            out[v.position] = v
+        return out
+
+    @property
+    def decoration(self):
+        g = self._game
+        st = g._state()
+        dead = set(st.dead_cells())
+        W = self.size[0]
+        out = {}
+        for (x, y) in g.map.objectives:
+            c = y * W + x
+            out[(x, y)] = DeadBody("dead body", (x, y)) if c in dead else ObjectiveLocation((x, y))
+            dead.discard(c)
+        for c in sorted(dead):
+            p = (c % W, c // W)
+            out[p] = DeadBody("dead body", p)
+        return out
+
+
+class _Rules(object):
+    """`rules/rules.py:6-18` predicates over the view."""
+
+    def __init__(self, game):
+        self.game = game
+
+    def players_alive(self):
+        return any(p.life > 0 for p in self.game.get_all_players())
+
+    def agents_alive(self):
+        return any(p.life > 0 for p in self.game.agents)
+
+
+class ExterminationRules(_Rules):
+    """rules/extermination.py:11-26"""
+
+    def zombies_alive(self):
+        return any(isinstance(t, Zombie) and t.life > 0 for t in self.game.world.things.values())
+
+    def game_ended(self):
+        return not self.players_alive() or not self.zombies_alive()
+
+    def game_won(self):
+        if self.players_alive():
+            return True, 'zombies exterminated! :)'
+        return False, 'players exterminated! :('
+
+
+class SurvivalRules(_Rules):
+    """rules/survival.py:5-15"""
+
+    def game_ended(self):
+        return not self.players_alive()
+
+    def game_won(self):
+        if self.players_alive():
+            return True, u'you won a game that never ends (?!)'
+        return False, u'everybody is dead :('
+
+
+class SafeHouseRules(_Rules):
+    """rules/safehouse.py:10-32"""
+
+    def alive_players_in_house(self):
+        obj = set(map(tuple, self.game.map.objectives))
+        return all(p.position in obj for p in self.game.get_all_players() if p.life > 0)
+
+    def game_ended(self):
+        if self.players_alive():
+            return self.alive_players_in_house()
+        return True
+
+    def game_won(self):
+        if self.players_alive():
+            return True, u'everybody made it into the safehouse :)'
+        return False, u'nobody made it into the safehouse :('
+
+
+class EvacuationRules(_Rules):
+    """rules/evacuation.py:13-57"""
+
+    def get_alive_players(self):
+        return [p for p in self.game.get_all_players() if p.life > 0]
+
+    def alive_players_together(self):
+        alive = self.get_alive_players()
+        by_pos = dict((p.position, p) for p in alive)
+        together = set()
+        pending = [alive[0]]
+        while pending:
+            p = pending.pop()
+            together.add(id(p))
+            x, y = p.position
+            for q in ((x, y + 1), (x, y - 1), (x + 1, y), (x - 1, y)):
+                if q in by_pos and id(by_pos[q]) not in together:
+                    pending.append(by_pos[q])
+        return len(together) == len(alive)
+
+    def half_team_alive(self):
+        return len(self.get_alive_players()) >= len(self.game.get_all_players()) / 2.0
+
+    def game_ended(self):
+        if self.half_team_alive():
+            return self.alive_players_together()
+        return True
+
+    def game_won(self):
+        if self.half_team_alive():
+            return True, u'players got together and were evacuated :)'
+        return False, u'too few survivors to send a rescue helicopter :('
+
+
+_RULES = {"extermination": ExterminationRules, "survival": SurvivalRules,
+          "evacuation": EvacuationRules, "safehouse": SafeHouseRules}
+
+
+class GameView(object):
+    """`game.Game` attributes (game.py:115-140): rules_name, rules, map, initial_zombies,
+    minimum_zombies, debug, player_names, agent_ids, agent_weapons, world, players, agents.
+
+    `engine` is a `libzombsole_amd.engine.Engine`; `env` the env index inside it."""
+
+    def __init__(self, engine, env, map_, rules_name, player_names, agent_ids, agent_weapons,
+                 initial_zombies, minimum_zombies, debug):
+        self.engine = engine
+        self.env = env
+        self._obstacles = [OBSTACLE_CLASSES[k]((x, y), self, i) for i, (x, y, k) in enumerate(map_.obstacles)]
+        self.map = MapView(map_, self._obstacles)
+        self.rules_name = rules_name
+        self.rules = _RULES[rules_name](self)
+        self.player_names = list(player_names)
+        self.agent_ids = list(agent_ids)
+        self.agent_weapons = list(agent_weapons)
+        self.initial_zombies = initial_zombies
+        self.minimum_zombies = minimum_zombies
+        self.debug = debug
+        self._cache = None
+        self.new_episode()
+
+    # -- state cache ---------------------------------------------------------
+    def invalidate(self):
+        self._cache = None
+
+    def _state(self):
+        if self._cache is None:
+            self._cache = self.engine.get_state(self.env)
+        return self._cache
+
+    def _poke_entity(self, slot, life):
+        st = self.engine.get_state(self.env)
+        st.ent[slot][4] = life
+        self.engine.set_state(self.env, st)
+        self._cache = None
+
+    def _poke_obstacle(self, index, life):
+        st = self.engine.get_state(self.env)
+        st.obst_life[index] = life
+        self.engine.set_state(self.env, st)
+        self._cache = None
+
+    # -- objects ---------------------------------------------------------------
+    def new_episode(self):
+        """Fresh objects after a reset (the reference builds a new World and new players,
+        game.py:151-169)."""
+        self._cache = None
+        A = len(self.agent_ids)
+        self.agents = [Agent(self, i, self.agent_ids[i]) for i in range(A)]
+        self.players = [Player(self, A + j, self.player_names[j]) for j in range(len(self.player_names))]
+        self._views = {}
+        for i, a in enumerate(self.agents):
+            self._views[i] = a
+        for j, p in enumerate(self.players):
+            self._views[A + j] = p
+        self.world = WorldView(self)
+
+    def _entity(self, slot):
+        v = self._views.get(slot)
+        st = self._state()
+        if v is not None and isinstance(v, Zombie) and v._serial != int(st.ent[slot][7]):
+            v = None
+        if v is None:
+            v = Zombie(self, slot)
+            self._views[slot] = v
+        return v
+
+    def get_all_players(self):
+        return self.players + self.agents
+
+    def get_agents_health(self):
+        return sum(t.life for t in self.agents)
+
+    def get_players_health(self):
+        return sum(t.life for t in self.players)
+
+    def draw(self):
+        raise NotImplementedError("rendering is out of scope for the MI355X engine (SURVEY.md §8)")

@@ -89,6 +89,15 @@ class Map(object):
     def from_map_name(cls, map_name):
         return load_map(map_name)
 
+    @property
+    def things(self):
+        """Box/Wall then ObjectiveLocation objects (the reference's `Map.things`, game.py:38-97,
+        which interleaves them in file order; only the obstacles' relative order matters)."""
+        from .things import OBSTACLE_CLASSES, ObjectiveLocation
+        out = [OBSTACLE_CLASSES[k]((x, y)) for (x, y, k) in self.obstacles]
+        out += [ObjectiveLocation((x, y)) for (x, y) in self.objectives]
+        return out
+
     # counts used by the reference's tests/test_map.py
     @property
     def n_walls(self):

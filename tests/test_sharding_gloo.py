@@ -1,0 +1,71 @@
+"""Multi-rank env sharding on CPU (gloo, world_size 2), SURVEY.md §8(e).
+
+Envs are independent and env i is seeded base+i, so a node's results must not depend on
+how envs are split over ranks: each rank runs its `shard_range` of the bench workload
+through the C oracle (test infrastructure) and the all-reduced checksum must equal the
+single-rank run.  The optional observation gather (`gather_observations`) is checked with
+rank-tagged tensors.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from libzombsole_amd import _abi
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _builder():
+    return _abi.multi_env_config(1, "extermination", [], "bridge64", ["0", "1"], initial_zombies=10,
+                                 max_episode_steps=1000, obs_dtype=_abi.DTYPE_I64)
+
+
+TOTAL, STEPS = 24, 60
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from libzombsole_amd.vector import gather_observations, shard_range
+        from oracle.oracle import run_batch
+        e0, n = shard_range(TOTAL, rank, world)
+        cnt, csum = run_batch(_builder(), e0, n, STEPS, 7, threads=1)
+        parts = [None] * world
+        dist.all_gather_object(parts, (cnt, csum))
+        obs = torch.full((n, 2, 3, 5, 5), rank, dtype=torch.int32)
+        g = gather_observations(obs)
+        if rank == 0:
+            q.put((sum(c for c, _ in parts), sum(s for _, s in parts) % (1 << 64), g[:, 0, 0, 0, 0].tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_shards_match_single_rank():
+    from oracle.oracle import run_batch
+    cnt1, csum1 = run_batch(_builder(), 0, TOTAL, STEPS, 7, threads=1)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    cnt2, csum2, tags = res
+    assert cnt2 == cnt1 == TOTAL * STEPS
+    assert csum2 == csum1  # checksums add over envs (oracle/zs_oracle.c zo_run_batch)
+    assert tags == [0] * 12 + [1] * 12
