@@ -40,7 +40,7 @@ def parse():
     p.add_argument("--max-episode-steps", type=int, default=1000)
     p.add_argument("--obs-dtype", default="int64", choices=["int64", "int32", "int16"])
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-steps", type=int, default=300)
+    p.add_argument("--cpu-steps", type=int, default=2000)
     return p.parse_args()
 
 
@@ -70,7 +70,8 @@ def cpu_baseline(args, builder_fn):
     dt = time.perf_counter() - t0
     return {"value": n / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
             "sample": "C oracle (oracle/zs_oracle.c, OpenMP over envs), %d envs x %d steps of the same "
-                      "workload (same map/agents/zombies/policy/obs), %.1f s wall" % (n_envs, args.cpu_steps, dt)}
+                      "workload (same map/agents/zombies/policy/obs, autoreset, TimeLimit), %.1f s wall x %d "
+                      "threads = %.0f thread-s" % (n_envs, args.cpu_steps, dt, threads, dt * threads)}
 
 
 def main():
