@@ -16,4 +16,5 @@ for c in FETCH_SIZE WRITE_SIZE; do
         > "$OUT/$c.log" 2>&1 || { echo "pmc $c pass failed"; tail -5 "$OUT/$c.log"; exit 1; }
     echo "pmc $c ok"
 done
+# profiles/ written on the box is not merged back: run tools/pmc_summary.py locally on gpurun_out/prof
 python3 tools/pmc_summary.py "$OUT" ${TAG:-r01}
