@@ -39,6 +39,7 @@ def parse():
     p.add_argument("--zombies", type=int, default=10)
     p.add_argument("--max-episode-steps", type=int, default=1000)
     p.add_argument("--obs-dtype", default="int64", choices=["int64", "int32", "int16"])
+    p.add_argument("--lanes-per-env", type=int, default=0, help="k_tick lanes per env (0 = engine default)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-steps", type=int, default=2000)
     return p.parse_args()
@@ -98,7 +99,7 @@ def main():
     def builder(n):
         return _abi.multi_env_config(n, "extermination", [], args.map, agent_ids, initial_zombies=args.zombies,
                                      minimum_zombies=0, max_episode_steps=args.max_episode_steps,
-                                     obs_dtype=dtype)
+                                     obs_dtype=dtype, lanes_per_env=args.lanes_per_env)
 
     n_local = args.envs_per_gpu
     env0 = rank * n_local

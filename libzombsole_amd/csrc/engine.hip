@@ -18,6 +18,22 @@
 
 #include "zs_reset.hpp"
 
+// One launch per step: workgroups [0, n_reset) rebuild the envs of the pending list (next-step
+// autoreset, World rebuilt as in game.py:151-169), the others tick every other env (zs_tick.hpp).
+// An env is either pending (reset work only; the tick reports it as reset without touching its
+// state) or stepping (tick only), so the two roles never share an env.
+template <int G>
+__global__ void __launch_bounds__(64) k_step(Dev d, int n_reset, const int32_t* actions, double* rew,
+                                             uint8_t* done_out, uint8_t* trunc_out, uint8_t* listed_out,
+                                             uint8_t* reset_out, int* reset_list, int* reset_count,
+                                             const int* cur_list, const int* cur_count, int* err_out) {
+    if ((int)blockIdx.x < n_reset)
+        reset_role(d, 1, cur_list, cur_count, nullptr, err_out, blockIdx.x, n_reset);
+    else
+        tick_wg<G>(d, blockIdx.x - n_reset, actions, rew, done_out, trunc_out, listed_out, reset_out, reset_list,
+                   reset_count);
+}
+
 // ---------------------------------------------------------------------------
 // observations (gym/observation.py:36-173): one workgroup per env.  The env's entity slots
 // are scattered into an LDS cell grid first, then every thread encodes cells of the
@@ -320,6 +336,7 @@ struct zs_handle {
     int* d_rcount;  // [2]
     int rpar = 0;
     size_t reset_lds = 0;
+    int fused = 0;  // zs_step runs reset work and the tick in one launch (k_step)
     // diagnostics: HIP events bracketing every k_tick / k_obs launch on its stream
     int prof = 0;
     std::vector<hipEvent_t> ev_pool;
@@ -416,7 +433,7 @@ static int validate(const zs_config* c) {
 static int choose_layout(zs_handle* h, int want_g) {
     Dev& d = h->d;
     const int kMax = 64 * 1024;
-    int g0 = want_g > 0 ? want_g : 8;
+    int g0 = want_g > 0 ? want_g : 16;  // measured: G=16 and 32 beat 8 and 64 at C3 (tools/sweep_lanes.sh)
     for (int G = g0; G <= 64; G *= 2) {
         int ne = 64 / G;
         int cand_full = (d.W * d.H <= 65535) ? d.ncand : 0;
@@ -587,6 +604,10 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
         delete h;
         return fail(ZS_EHIP, "cannot raise k_reset's dynamic LDS limit");
     }
+    // one launch for reset work + tick when the reset image fits the tick's LDS allocation
+    // (otherwise the tick's occupancy would pay for the larger reset image)
+    h->fused = h->reset_lds <= h->lds ? 1 : 0;
+    if (const char* f = getenv("ZS_FUSED")) h->fused = h->fused && atoi(f) != 0;
     {
         int gb = ((d.W * d.H + 15) / 16) * 16;
         h->obs_grid = gb <= 64 * 1024 ? gb : 0;
@@ -673,10 +694,19 @@ static int launch_tick(zs_handle* h, const int32_t* actions, double* rew, uint8_
     const int ne = 64 / h->G;
     unsigned grid = (unsigned)((d.N + ne - 1) / ne);
     int i0 = -1, i1 = -1;
+    const int p = h->rpar;
+    // fused: the first n_reset workgroups rebuild the envs of the pending list (ended at the previous
+    // call) while the others tick every other env; the two sets of envs are disjoint
+    const int n_reset = std::min(d.N, 512);
     if (h->prof) HIPCHK(hipEventRecord(prof_event(h, &i0), s));
-#define ZS_TICK(GG)                                                                                                \
-    hipLaunchKernelGGL(k_tick<GG>, dim3(grid), dim3(64), h->lds, s, d, actions, rew, done, trunc, listed, reset_out, \
-                       rlist, rcount)
+#define ZS_TICK(GG)                                                                                                   \
+    if (h->fused)                                                                                                     \
+        hipLaunchKernelGGL(k_step<GG>, dim3(grid + n_reset), dim3(64), h->lds, s, d, n_reset, actions, rew, done,    \
+                           trunc, listed, reset_out, rlist, rcount, (const int*)h->d_rlist[p],                        \
+                           (const int*)(h->d_rcount + p), h->d_err);                                                  \
+    else                                                                                                              \
+        hipLaunchKernelGGL(k_tick<GG>, dim3(grid), dim3(64), h->lds, s, d, actions, rew, done, trunc, listed,        \
+                           reset_out, rlist, rcount)
     switch (h->G) {
     case 1: ZS_TICK(1); break;
     case 2: ZS_TICK(2); break;
@@ -702,7 +732,7 @@ static int launch_reset(zs_handle* h, int list_mode, const uint8_t* mask, hipStr
     int i0 = -1, i1 = -1;
     if (h->prof) HIPCHK(hipEventRecord(prof_event(h, &i0), s));
     hipLaunchKernelGGL(k_reset, dim3(grid), dim3(64), h->reset_lds, s, d, list_mode, h->d_rlist[p], h->d_rcount + p,
-                       list_mode ? h->d_rcount + (1 - p) : nullptr, mask, h->d_err);
+                       mask, h->d_err);
     HIPCHK(hipGetLastError());
     if (h->prof) {
         HIPCHK(hipEventRecord(prof_event(h, &i1), s));
@@ -718,6 +748,20 @@ extern "C" int zs_reset(zs_handle* h, const uint8_t* env_mask_dev, void* obs_dev
     HIPCHK(hipMemsetAsync(h->d_err, 0, sizeof(int), s));
     int rc = launch_reset(h, 0, env_mask_dev, s);
     if (rc) return rc;
+    // the pending-reset list must hold exactly the envs still pending: drop the ones just rebuilt
+    {
+        int p = h->rpar, q = 1 - p;
+        if (!env_mask_dev) {
+            HIPCHK(hipMemsetAsync(h->d_rcount + p, 0, sizeof(int), s));
+        } else {
+            HIPCHK(hipMemsetAsync(h->d_rcount + q, 0, sizeof(int), s));
+            hipLaunchKernelGGL(k_list_filter, dim3(std::min(64, (h->d.N + 255) / 256)), dim3(256), 0, s,
+                               (const int*)h->d_rlist[p], (const int*)(h->d_rcount + p), h->d_rlist[q],
+                               h->d_rcount + q, env_mask_dev);
+            HIPCHK(hipGetLastError());
+            h->rpar = q;
+        }
+    }
     rc = launch_obs(h, obs_dev, env_mask_dev, s);
     if (rc) return rc;
     int err = 0;
@@ -742,11 +786,15 @@ extern "C" int zs_step(zs_handle* h, const int32_t* actions_dev, void* obs_dev, 
     if (!h || !actions_dev || !rewards_dev || !done_dev || !trunc_dev) return fail(ZS_EINVAL, "null argument");
     hipStream_t s = (hipStream_t)stream;
     HIPCHK(hipSetDevice(h->device));
-    // 1) rebuild the envs that ended at the previous call (and clear the list k_tick fills now)
-    int rc = launch_reset(h, 1, nullptr, s);
-    if (rc) return rc;
-    // 2) tick every other env; envs that end now are queued for the next call
-    int q = 1 - h->rpar;
+    // 1) rebuild the envs that ended at the previous call (list[p]); fused into the tick launch
+    //    when the LDS images allow, else a k_reset launch first
+    int q = 1 - h->rpar, rc = ZS_OK;
+    if (!h->fused) {
+        rc = launch_reset(h, 1, nullptr, s);
+        if (rc) return rc;
+    }
+    // 2) tick every other env; envs that end now are queued on list[q] for the next call
+    HIPCHK(hipMemsetAsync(h->d_rcount + q, 0, sizeof(int), s));
     rc = launch_tick(h, actions_dev, rewards_dev, done_dev, trunc_dev, listed_dev, reset_dev, h->d_rlist[q],
                      h->d_rcount + q, s);
     if (rc) return rc;

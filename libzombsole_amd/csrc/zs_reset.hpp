@@ -328,18 +328,23 @@ __device__ __forceinline__ void reset_env_wave(const Dev& d, const ResetLds& L, 
         d.scal[S_PREVZD * N + e] = 0;
         d.scal[S_SERIAL * N + e] = serial;
         d.scal[S_ODIRTY * N + e] = odirty;
-        d.scal[S_NEEDRESET * N + e] = list_mode ? 2 : 0;  // 2: k_tick reports this call as a reset
+        // list mode (autoreset): the env stays pending; the tick of this same call reports it as
+        // reset and clears the flag (it never reads this env's state).  Mask mode: done now.
+        if (!list_mode) d.scal[S_NEEDRESET * N + e] = 0;
         d.rngst[e] = stf;
     }
     wave_sync();
     RST(7);
 }
 
-// list_mode: envs list[0..*count) whose needs_reset == 1 (next-step autoreset); clears *count_clear
-// (the list k_tick fills this call).  Otherwise: every env with mask[e] (all if mask == NULL).
-__global__ void __launch_bounds__(64) k_reset(Dev d, int list_mode, const int* list, const int* count,
-                                              int* count_clear, const uint8_t* mask, int* err_out) {
+// The reset work of workgroup `wg` of `nwg`.  list_mode: envs list[0..*count) (next-step
+// autoreset; the list holds exactly the pending envs, see zs_reset's list filter).  Otherwise
+// every env with mask[e] (all if mask == NULL).
+__device__ __forceinline__ void reset_role(const Dev& d, int list_mode, const int* list, const int* count,
+                                           const uint8_t* mask, int* err_out, int wg, int nwg) {
     extern __shared__ __align__(16) uint8_t smem[];
+    const int n = list_mode ? *count : d.N;
+    if (wg >= n) return;
     ResetLds L;
     int o = 0;
     L.bm = (lu32*)(smem + o);
@@ -366,16 +371,27 @@ __global__ void __launch_bounds__(64) k_reset(Dev d, int list_mode, const int* l
     L.tw = (lu32*)(smem + o);
     if (d.lists_cap)
         for (int i = threadIdx.x; i < d.nps + d.nzs; i += 64) L.lists[i] = i < d.nps ? d.pspawn[i] : d.zspawn[i - d.nps];
-    if (list_mode && count_clear && blockIdx.x == 0 && threadIdx.x == 0) *count_clear = 0;
     wave_sync();
-    const int n = list_mode ? *count : d.N;
-    for (int idx = blockIdx.x; idx < n; idx += gridDim.x) {
+    for (int idx = wg; idx < n; idx += nwg) {
         int e = list_mode ? list[idx] : idx;
-        if (list_mode) {
-            if (d.scal[S_NEEDRESET * d.N + e] != 1) continue;
-        } else if (mask && !mask[e]) {
-            continue;
-        }
+        if (!list_mode && mask && !mask[e]) continue;
         reset_env_wave(d, L, e, list_mode, err_out);
+    }
+}
+
+__global__ void __launch_bounds__(64) k_reset(Dev d, int list_mode, const int* list, const int* count,
+                                              const uint8_t* mask, int* err_out) {
+    reset_role(d, list_mode, list, count, mask, err_out, blockIdx.x, gridDim.x);
+}
+
+// Drop the envs a mask-mode reset just rebuilt from the pending list (src -> dst, dst count
+// zeroed by the host); mask == NULL drops all.  Keeps "list == pending envs" exact.
+__global__ void __launch_bounds__(256) k_list_filter(const int* src, const int* src_count, int* dst, int* dst_count,
+                                                     const uint8_t* mask) {
+    if (!mask) return;
+    const int n = *src_count;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        int e = src[i];
+        if (!mask[e]) dst[atomicAdd(dst_count, 1)] = e;
     }
 }

@@ -876,13 +876,13 @@ __device__ __forceinline__ void coop_refill(const Dev& d, int base, int count, c
 // k_tick: one workgroup = one wave = 64/G envs
 // ---------------------------------------------------------------------------
 template <int G>
-__global__ void __launch_bounds__(64) k_tick(Dev d, const int32_t* actions, double* rew, uint8_t* done_out,
-                                             uint8_t* trunc_out, uint8_t* listed_out, uint8_t* reset_out,
-                                             int* reset_list, int* reset_count) {
+__device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* actions, double* rew, uint8_t* done_out,
+                                        uint8_t* trunc_out, uint8_t* listed_out, uint8_t* reset_out, int* reset_list,
+                                        int* reset_count) {
     extern __shared__ __align__(16) uint8_t smem[];
     constexpr int NE = 64 / G;
     const int lane = threadIdx.x, g = lane / G, j = lane - g * G;
-    const int base = blockIdx.x * NE, e = base + g, N = d.N, E = d.E, A = d.A;
+    const int base = wg * NE, e = base + g, N = d.N, E = d.E, A = d.A;
     const bool active = e < N;
     const bool leader = j == 0;
     const TickLayout L = tick_layout(NE, E, d.DW, d.rw_cap, d.cand_cap, d.lists_cap, A);
@@ -912,13 +912,15 @@ __global__ void __launch_bounds__(64) k_tick(Dev d, const int32_t* actions, doub
 
     STAMP_DECL
     STAMP(0);
-    // needs_reset: 0 step, 1 pending (never stepped), 2 k_reset rebuilt this env for this call
+    // needs_reset != 0: the env ended at the previous call (or was never reset) and is rebuilt by
+    // this call's reset work, possibly concurrently: its state is neither read nor written here,
+    // only this call's outputs (as after env.reset()) and the flag.
     int needs_reset = 0, stepping = 0, n_order = 0;
     uint32_t st0 = 0;
     int wlen = 0;
-    if (active) {
-        needs_reset = d.scal[S_NEEDRESET * N + e];
-        stepping = needs_reset == 0;
+    if (active) needs_reset = d.scal[S_NEEDRESET * N + e];
+    stepping = active && needs_reset == 0;
+    if (stepping) {
         n_order = d.scal[S_NORDER * N + e];
         // stage the entity table (SoA [slot][N]: this env's column)
         {
@@ -992,13 +994,13 @@ __global__ void __launch_bounds__(64) k_tick(Dev d, const int32_t* actions, doub
         st0 = st_pack(off, slot, ready);
     }
     wave_sync();
-    if (active && stepping) {
+    if (stepping) {
         // dict-order ranks for closest() tie-breaks
         for (int k = j; k < n_order; k += G) LR(c, LO(c, k)) = (uint8_t)k;
     }
     wave_sync();
     STAMP(1);
-    if (active && stepping) {
+    if (stepping) {
         // decisions (start-of-tick state), the group's lanes over the actors
         for (int k = j; k < n_order; k += G) {
             int s = LO(c, k), kind, tgt;
@@ -1009,36 +1011,35 @@ __global__ void __launch_bounds__(64) k_tick(Dev d, const int32_t* actions, doub
     }
     wave_sync();
     STAMP(2);
-    if (active && leader) {
+    if (active && leader && !stepping) {  // this call is the env's reset; outputs as after env.reset()
+        int nr = d.reward_mode == ZS_REWARD_SINGLE ? 1 : A;
+        for (int a = 0; a < nr; a++) rew[(size_t)e * nr + a] = 0.0;
+        done_out[e] = 0;
+        trunc_out[e] = 0;
+        if (listed_out)
+            for (int a = 0; a < A; a++) listed_out[(size_t)e * A + a] = 1;
+        if (reset_out) reset_out[e] = 1;
+        d.scal[S_NEEDRESET * N + e] = 0;
+        lst[g] = 1u << 11;  // no MT refill for this env here
+    }
+    if (leader && stepping) {
         c.st0 = st0;
         c.wpos = 0;
         c.wlen = wlen;
         c.n_order = n_order;
-        c.t = MISC(c, MISC_T);
+        c.t = MISC(c, MISC_T) + 1;
         c.deaths = MISC(c, MISC_DEATHS);
         c.zd = MISC(c, MISC_ZD);
         c.epsteps = MISC(c, MISC_EPSTEPS);
         c.prevzd = MISC(c, MISC_PREVZD);
         c.serial = MISC(c, MISC_SERIAL);
         c.odirty = MISC(c, MISC_ODIRTY);
-        if (needs_reset) {  // this call is the env's reset (obs written by k_obs); outputs as after env.reset()
-            int nr = d.reward_mode == ZS_REWARD_SINGLE ? 1 : A;
-            for (int a = 0; a < nr; a++) rew[(size_t)e * nr + a] = 0.0;
-            done_out[e] = 0;
-            trunc_out[e] = 0;
-            if (listed_out)
-                for (int a = 0; a < A; a++) listed_out[(size_t)e * A + a] = 1;
-            if (needs_reset == 1) reset_list[atomicAdd(reset_count, 1)] = e;  // not yet rebuilt: retry
-            else needs_reset = 0;
-        } else {
-            c.t += 1;
-            env_step_leader(d, c, actions, rew, done_out, trunc_out, listed_out);
-            if ((done_out[e] || trunc_out[e]) && (d.flags & ZS_FLAG_AUTORESET)) {
-                needs_reset = 1;
-                reset_list[atomicAdd(reset_count, 1)] = e;  // rebuilt by k_reset at the next call
-            }
+        env_step_leader(d, c, actions, rew, done_out, trunc_out, listed_out);
+        if ((done_out[e] || trunc_out[e]) && (d.flags & ZS_FLAG_AUTORESET)) {
+            needs_reset = 1;
+            reset_list[atomicAdd(reset_count, 1)] = e;  // rebuilt by the next call's reset work
         }
-        if (reset_out) reset_out[e] = (uint8_t)(stepping == 0);
+        if (reset_out) reset_out[e] = 0;
         MISC(c, MISC_T) = c.t;
         MISC(c, MISC_DEATHS) = c.deaths;
         MISC(c, MISC_ZD) = c.zd;
@@ -1054,7 +1055,7 @@ __global__ void __launch_bounds__(64) k_tick(Dev d, const int32_t* actions, doub
     }
     wave_sync();
     STAMP(3);
-    if (active) {
+    if (stepping) {
         for (int s = j; s < E; s += G) {
             d.pos[(size_t)s * N + e] = LP(c, s);
             d.life[(size_t)s * N + e] = LL(c, s);
@@ -1081,4 +1082,11 @@ __global__ void __launch_bounds__(64) k_tick(Dev d, const int32_t* actions, doub
     STAMP(4);
     coop_refill(d, base, min(NE, N - base), lst, (lu32*)(smem + L.off_bm));
     STAMP(5);
+}
+
+template <int G>
+__global__ void __launch_bounds__(64) k_tick(Dev d, const int32_t* actions, double* rew, uint8_t* done_out,
+                                             uint8_t* trunc_out, uint8_t* listed_out, uint8_t* reset_out,
+                                             int* reset_list, int* reset_count) {
+    tick_wg<G>(d, blockIdx.x, actions, rew, done_out, trunc_out, listed_out, reset_out, reset_list, reset_count);
 }
