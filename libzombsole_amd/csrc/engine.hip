@@ -26,12 +26,12 @@ template <int G>
 __global__ void __launch_bounds__(64) k_step(Dev d, int n_reset, const int32_t* actions, double* rew,
                                              uint8_t* done_out, uint8_t* trunc_out, uint8_t* listed_out,
                                              uint8_t* reset_out, int* reset_list, int* reset_count,
-                                             const int* cur_list, const int* cur_count, int* err_out) {
+                                             const int* cur_list, const int* cur_count, int* err_out, void* obs_out) {
     if ((int)blockIdx.x < n_reset)
-        reset_role(d, 1, cur_list, cur_count, nullptr, err_out, blockIdx.x, n_reset);
+        reset_role(d, 1, cur_list, cur_count, nullptr, err_out, blockIdx.x, n_reset, d.fobs ? obs_out : nullptr);
     else
         tick_wg<G>(d, blockIdx.x - n_reset, actions, rew, done_out, trunc_out, listed_out, reset_out, reset_list,
-                   reset_count);
+                   reset_count, obs_out);
 }
 
 // ---------------------------------------------------------------------------
@@ -430,14 +430,46 @@ static int validate(const zs_config* c) {
 
 // Pick lanes-per-env G, the LDS RNG window and the LDS candidate list so one workgroup's
 // image fits the 64 KiB dynamic-LDS budget.
-static int choose_layout(zs_handle* h, int want_g) {
+// workgroups of the step launch resident at once on 256 CUs decide how much LDS one may take
+static const int kResetWGs = 256;  // reset-work workgroups of a fused step launch
+
+static bool getenv_off(const char* name) {
+    const char* f = getenv(name);
+    return f && atoi(f) == 0;
+}
+
+static int choose_layout(zs_handle* h, int want_g, bool fobs_ok) {
     Dev& d = h->d;
     const int kMax = 64 * 1024;
     int g0 = want_g > 0 ? want_g : 16;  // measured: G=16 and 32 beat 8 and 64 at C3 (tools/sweep_lanes.sh)
+    int cand_full = (d.W * d.H <= 65535) ? d.ncand : 0;
+    int lists = (d.nps + d.nzs <= 4096) ? d.nps + d.nzs : 0;
+    d.fobs = 0;
+    if (fobs_ok) {
+        // tick + observation image in one workgroup: keep every workgroup of the launch resident
+        // (160 KB LDS per CU), dropping the optional LDS copies (spawn lists, candidates) first
+        int ne = 64 / g0;
+        int wgs = (d.N + ne - 1) / ne + std::min(d.N, kResetWGs);
+        int per_cu = std::max(1, (wgs + 255) / 256);
+        int budget = std::min(kMax, std::max(16 * 1024, 160 * 1024 / per_cu));
+        for (int cand : {cand_full, 0})
+            for (int lst : {lists, 0})
+                for (int rw : {256, 128, 64}) {
+                    TickLayout L = tick_layout(ne, d.E, d.DW, rw, cand, lst, d.A, 1, d.O);
+                    if (L.bytes <= budget) {
+                        h->G = g0;
+                        d.rw_cap = rw;
+                        d.rw_step = std::min(rw, 64);
+                        d.cand_cap = cand;
+                        d.lists_cap = lst;
+                        d.fobs = 1;
+                        h->lds = L.bytes;
+                        return ZS_OK;
+                    }
+                }
+    }
     for (int G = g0; G <= 64; G *= 2) {
         int ne = 64 / G;
-        int cand_full = (d.W * d.H <= 65535) ? d.ncand : 0;
-        int lists = (d.nps + d.nzs <= 4096) ? d.nps + d.nzs : 0;
         for (int cand : {cand_full, 0}) {
             for (int rw : {512, 256, 128, 64}) {
                 TickLayout L = tick_layout(ne, d.E, d.DW, rw, cand, lists, d.A);
@@ -515,6 +547,21 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
         int cell = m.obstacle_xy[2 * i + 1] * d.W + m.obstacle_xy[2 * i];
         obstbits[cell >> 5] |= 1u << (cell & 31);
     }
+    // fused observations need obstacle index == rank of its cell among obstacle cells (row-major
+    // file order, as every map-file parse produces); boxbits / oprefix make the lookup LDS-only
+    bool rank_order = true;
+    for (int i = 1; i < d.O; i++)
+        if (m.obstacle_xy[2 * i + 1] * d.W + m.obstacle_xy[2 * i] <=
+            m.obstacle_xy[2 * i - 1] * d.W + m.obstacle_xy[2 * i - 2])
+            rank_order = false;
+    std::vector<uint32_t> boxbits(d.DW, 0);
+    for (int i = 0; i < d.O; i++)
+        if (m.obstacle_kind[i] == ZS_THING_BOX) {
+            int cell = m.obstacle_xy[2 * i + 1] * d.W + m.obstacle_xy[2 * i];
+            boxbits[cell >> 5] |= 1u << (cell & 31);
+        }
+    std::vector<int32_t> oprefix(d.DW, 0);
+    for (int w = 1; w < d.DW; w++) oprefix[w] = oprefix[w - 1] + __builtin_popcount(obstbits[w - 1]);
     std::vector<uint32_t> objbits(d.DW, 0);
     for (int i = 0; i < m.n_objectives; i++) {
         int cell = m.objective_xy[2 * i + 1] * d.W + m.objective_xy[2 * i];
@@ -540,12 +587,15 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
         }                  \
     } while (0)
     int16_t* p_cellmap;
-    uint32_t *p_objbits, *p_obstbits;
+    uint32_t *p_objbits, *p_obstbits, *p_boxbits;
+    int32_t* p_oprefix;
     int32_t *p_oxy, *p_ps, *p_zs, *p_aw, *p_ac, *p_bt;
     uint8_t* p_okind;
     TRY(dupload(h, &p_cellmap, cellmap));
     TRY(dupload(h, &p_objbits, objbits));
     TRY(dupload(h, &p_obstbits, obstbits));
+    TRY(dupload(h, &p_boxbits, boxbits));
+    TRY(dupload(h, &p_oprefix, oprefix));
     TRY(dupload(h, &p_oxy, oxy));
     TRY(dupload(h, &p_okind, okind));
     TRY(dupload(h, &p_ps, ps));
@@ -556,6 +606,8 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
     d.cellmap = p_cellmap;
     d.objbits = p_objbits;
     d.obstbits = p_obstbits;
+    d.boxbits = p_boxbits;
+    d.oprefix = p_oprefix;
     d.obst_xy = p_oxy;
     d.obst_kind = p_okind;
     d.pspawn = p_ps;
@@ -590,7 +642,11 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
     TRY(dalloc(h, &h->d_rlist[1], N));
     TRY(dalloc(h, &h->d_rcount, 2));
     // workgroup: 64 envs (one wave) unless the LDS image of the entity table is too large
-    TRY(choose_layout(h, cfg->lanes_per_env));
+    // the reset work's observation staging reuses its 2 x 624-word twist buffer
+    const bool fobs_ok = rank_order && (4 * d.DW + d.O) <= 2 * ZS_MT_N && !getenv_off("ZS_FOBS");
+    TRY(choose_layout(h, cfg->lanes_per_env, fobs_ok));
+    h->reset_lds = (size_t)reset_lds_bytes(d.E, d.DW, d.ncand, d.lists_cap);
+    if (d.fobs && h->reset_lds > h->lds) TRY(choose_layout(h, cfg->lanes_per_env, false));  // fobs needs k_step
     h->reset_lds = (size_t)reset_lds_bytes(d.E, d.DW, d.ncand, d.lists_cap);
     if (h->reset_lds > 160 * 1024) {
         free_all(h);
@@ -607,7 +663,12 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
     // one launch for reset work + tick when the reset image fits the tick's LDS allocation
     // (otherwise the tick's occupancy would pay for the larger reset image)
     h->fused = h->reset_lds <= h->lds ? 1 : 0;
-    if (const char* f = getenv("ZS_FUSED")) h->fused = h->fused && atoi(f) != 0;
+    if (getenv_off("ZS_FUSED")) h->fused = 0;
+    if (!h->fused) d.fobs = 0;
+    if (getenv("ZS_VERBOSE"))
+        fprintf(stderr, "zs_create: N=%d E=%d G=%d tick_lds=%zu reset_lds=%zu rw_cap=%d cand_cap=%d lists_cap=%d "
+                        "fused=%d fobs=%d\n", d.N, d.E, h->G, h->lds, h->reset_lds, d.rw_cap, d.cand_cap, d.lists_cap,
+                h->fused, d.fobs);
     {
         int gb = ((d.W * d.H + 15) / 16) * 16;
         h->obs_grid = gb <= 64 * 1024 ? gb : 0;
@@ -689,7 +750,7 @@ static int launch_obs(zs_handle* h, void* obs, const uint8_t* mask, hipStream_t 
 }
 
 static int launch_tick(zs_handle* h, const int32_t* actions, double* rew, uint8_t* done, uint8_t* trunc,
-                       uint8_t* listed, uint8_t* reset_out, int* rlist, int* rcount, hipStream_t s) {
+                       uint8_t* listed, uint8_t* reset_out, int* rlist, int* rcount, void* obs, hipStream_t s) {
     const Dev& d = h->d;
     const int ne = 64 / h->G;
     unsigned grid = (unsigned)((d.N + ne - 1) / ne);
@@ -697,13 +758,13 @@ static int launch_tick(zs_handle* h, const int32_t* actions, double* rew, uint8_
     const int p = h->rpar;
     // fused: the first n_reset workgroups rebuild the envs of the pending list (ended at the previous
     // call) while the others tick every other env; the two sets of envs are disjoint
-    const int n_reset = std::min(d.N, 512);
+    const int n_reset = std::min(d.N, kResetWGs);
     if (h->prof) HIPCHK(hipEventRecord(prof_event(h, &i0), s));
 #define ZS_TICK(GG)                                                                                                   \
     if (h->fused)                                                                                                     \
         hipLaunchKernelGGL(k_step<GG>, dim3(grid + n_reset), dim3(64), h->lds, s, d, n_reset, actions, rew, done,    \
                            trunc, listed, reset_out, rlist, rcount, (const int*)h->d_rlist[p],                        \
-                           (const int*)(h->d_rcount + p), h->d_err);                                                  \
+                           (const int*)(h->d_rcount + p), h->d_err, obs);                                             \
     else                                                                                                              \
         hipLaunchKernelGGL(k_tick<GG>, dim3(grid), dim3(64), h->lds, s, d, actions, rew, done, trunc, listed,        \
                            reset_out, rlist, rcount)
@@ -796,10 +857,11 @@ extern "C" int zs_step(zs_handle* h, const int32_t* actions_dev, void* obs_dev, 
     // 2) tick every other env; envs that end now are queued on list[q] for the next call
     HIPCHK(hipMemsetAsync(h->d_rcount + q, 0, sizeof(int), s));
     rc = launch_tick(h, actions_dev, rewards_dev, done_dev, trunc_dev, listed_dev, reset_dev, h->d_rlist[q],
-                     h->d_rcount + q, s);
+                     h->d_rcount + q, obs_dev, s);
     if (rc) return rc;
     h->rpar = q;
-    // 3) observations of every env
+    // 3) observations of every env (already written by the step launch when fobs)
+    if (h->d.fobs) return ZS_OK;
     return launch_obs(h, obs_dev, nullptr, s);
 }
 

@@ -42,6 +42,7 @@ struct Dev {
     int rw_step;     // words prefetched for a plain step (resets prefetch rw_cap)
     int cand_cap;    // spawn-candidate entries staged in LDS per env (0 = global scratch)
     int lists_cap;   // static spawn-list entries staged in LDS per workgroup (0 = read from global)
+    int fobs;        // observations are written by the step launch itself (tick and reset work)
     int rules, reward_mode, obs_scope, obs_enc, obs_w, obs_dtype, max_steps;
     int initial_zombies, minimum_zombies;
     uint32_t flags;
@@ -49,6 +50,8 @@ struct Dev {
     const int16_t* cellmap;
     const uint32_t* obstbits;  // static obstacle occupancy bitmap [DW]
     const uint32_t* objbits;
+    const uint32_t* boxbits;   // static: cell holds a Box (map file) [DW]
+    const int32_t* oprefix;    // static: obstacles in cells < 32*w (obstacle index = cell rank) [DW]
     const int32_t* obst_xy;  // packed x | y << 16
     const uint8_t* obst_kind;
     const int32_t* pspawn;   // packed

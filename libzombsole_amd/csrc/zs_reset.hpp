@@ -341,7 +341,7 @@ __device__ __forceinline__ void reset_env_wave(const Dev& d, const ResetLds& L, 
 // autoreset; the list holds exactly the pending envs, see zs_reset's list filter).  Otherwise
 // every env with mask[e] (all if mask == NULL).
 __device__ __forceinline__ void reset_role(const Dev& d, int list_mode, const int* list, const int* count,
-                                           const uint8_t* mask, int* err_out, int wg, int nwg) {
+                                           const uint8_t* mask, int* err_out, int wg, int nwg, void* obs_out) {
     extern __shared__ __align__(16) uint8_t smem[];
     const int n = list_mode ? *count : d.N;
     if (wg >= n) return;
@@ -376,12 +376,42 @@ __device__ __forceinline__ void reset_role(const Dev& d, int list_mode, const in
         int e = list_mode ? list[idx] : idx;
         if (!list_mode && mask && !mask[e]) continue;
         reset_env_wave(d, L, e, list_mode, err_out);
+        if (obs_out) {  // fobs: the new world's observations, from the LDS image (twist buffer reused)
+            lu32* sobst = L.tw;
+            lu32* sbox = sobst + d.DW;
+            lu32* sobj = sbox + d.DW;
+            li32* spre = (li32*)(sobj + d.DW);
+            li32* hp = spre + d.DW;
+            wave_sync();
+            stage_in(d.obstbits, d.DW, threadIdx.x, 64, sobst, [](int w) { return w; });
+            stage_in(d.boxbits, d.DW, threadIdx.x, 64, sbox, [](int w) { return w; });
+            stage_in(d.objbits, d.DW, threadIdx.x, 64, sobj, [](int w) { return w; });
+            stage_in(d.oprefix, d.DW, threadIdx.x, 64, spre, [](int w) { return w; });
+            stage_in(d.obst_hp + (size_t)e * d.O, d.O, threadIdx.x, 64, hp, [](int w) { return w; });
+            wave_sync();
+            ObsImg v;
+            v.occ = L.bm;
+            v.dead = nullptr;   // a new World has no dead bodies
+            v.opres = nullptr;  // and every map obstacle is spawned (HP carried over)
+            v.hp = hp;
+            v.sobst = sobst;
+            v.sbox = sbox;
+            v.sobj = sobj;
+            v.spre = spre;
+            v.pos = L.lpos;
+            v.life = L.llife;
+            v.weap = L.lweap;
+            v.pres = L.lpres;
+            v.s = 1;
+            obs_write_env(d, v, obs_out, e, threadIdx.x, 64);
+            wave_sync();
+        }
     }
 }
 
 __global__ void __launch_bounds__(64) k_reset(Dev d, int list_mode, const int* list, const int* count,
                                               const uint8_t* mask, int* err_out) {
-    reset_role(d, list_mode, list, count, mask, err_out, blockIdx.x, gridDim.x);
+    reset_role(d, list_mode, list, count, mask, err_out, blockIdx.x, gridDim.x, nullptr);
 }
 
 // Drop the envs a mask-mode reset just rebuilt from the pending list (src -> dst, dst count
