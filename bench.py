@@ -1,16 +1,17 @@
 #!/usr/bin/env python3
 """Benchmark: batched zombsole env-steps/s on MI355X (BASELINE.json metric).
 
-Workload (BASELINE.json configs[2], "C3"): synthetic 64x64 `bridge64` map,
-extermination rules, MultiagentZombsoleEnv semantics with 2 agents + 10
-zombies per env, 21x21x3 int64 channel observations for every agent written to
-HBM each step, uniform Discrete(7) policy generated on device
-(splitmix64(seed, step, agent)), gym TimeLimit 1000, next-step autoreset.
-65 536 envs over 8 GPUs = 8 192 envs per GPU; envs are independent, so each
-rank owns a contiguous global env range (seeds = global index) and no data-path
-collective runs ("weak" scaling: per-GPU work fixed as GPUs are added).
+Workload (BASELINE.json metric: "65 536 parallel 64x64 envs at 1/2/4/8 MI355X";
+configs[2], "C3", at 8 GPUs): synthetic 64x64 `bridge64` map, extermination
+rules, MultiagentZombsoleEnv semantics with 2 agents + 10 zombies per env,
+21x21x3 int64 channel observations for every agent written to HBM each step,
+uniform Discrete(7) policy generated on device (splitmix64(seed, step, agent)),
+gym TimeLimit 1000, next-step autoreset.  The 65 536 envs are split over the N
+GPUs ("strong" scaling: 65 536 on 1 GPU, 8 192 per GPU on 8); envs are
+independent, so each rank owns a contiguous global env range (seeds = global
+index) and no data-path collective runs.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--envs-per-gpu 8192]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--envs 65536]
     torchrun --nproc-per-node N bench.py --gpus N ...
 
 Prints ONE JSON line (rank 0).
@@ -33,7 +34,8 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=20)
-    p.add_argument("--envs-per-gpu", type=int, default=8192)
+    p.add_argument("--envs", type=int, default=65536, help="total envs over all ranks (strong scaling)")
+    p.add_argument("--envs-per-gpu", type=int, default=0, help="fixed envs per rank instead (weak scaling)")
     p.add_argument("--map", default="bridge64")
     p.add_argument("--agents", type=int, default=2)
     p.add_argument("--zombies", type=int, default=10)
@@ -48,9 +50,10 @@ def parse():
 def algorithmic_bytes(E, A, occ_bytes, obs_bytes_per_env, mt_words):
     """SURVEY.md §8(d) per env-step figures, split by kernel.
 
-    k_tick: entity SoA read+write (E x 12 B x 2) + MT state (8 B) + MT words consumed x 4 B
-            + occupancy bitmap read (W*H/8 B) + actions (A x 12 B) + rewards (8A) + 3 flag bytes
-    k_obs : observation bytes written (A x 3 x 21 x 21 x 8 B for int64)
+    tick: entity SoA read+write (E x 12 B x 2) + MT state (8 B) + MT words consumed x 4 B
+          + occupancy bitmap read (W*H/8 B) + actions (A x 12 B) + rewards (8A) + 3 flag bytes
+    obs : observation bytes written (A x 3 x 21 x 21 x 8 B for int64)
+    The step launch (k_step) carries both when it writes the observations itself (fobs).
     """
     tick = 2 * E * 12 + 8 + 4 * mt_words + occ_bytes + A * 12 + 8 * A + 3
     return tick, obs_bytes_per_env
@@ -64,7 +67,7 @@ def cpu_baseline(args, builder_fn):
     except AttributeError:
         threads = os.cpu_count() or 1
     threads = max(1, min(threads, int(os.environ.get("OMP_NUM_THREADS", "16") or 16), 16))
-    n_envs = min(args.envs_per_gpu, 8192)
+    n_envs = 8192
     b = builder_fn(1)
     t0 = time.perf_counter()
     n, _ = run_batch(b, 0, n_envs, args.cpu_steps, 7, threads=threads)
@@ -101,8 +104,13 @@ def main():
                                      minimum_zombies=0, max_episode_steps=args.max_episode_steps,
                                      obs_dtype=dtype, lanes_per_env=args.lanes_per_env)
 
-    n_local = args.envs_per_gpu
-    env0 = rank * n_local
+    if args.envs_per_gpu:
+        n_local, env0, scaling = args.envs_per_gpu, rank * args.envs_per_gpu, "weak"
+        total_envs = n_local * world
+    else:
+        total_envs, scaling = args.envs, "strong"
+        env0 = rank * total_envs // world
+        n_local = (rank + 1) * total_envs // world - env0
     eng = Engine(builder(n_local), device=dev)
     eng.seed([env0 + i for i in range(n_local)])
     eng.reset()
@@ -134,7 +142,6 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    total_envs = n_local * world
     value = total_envs * args.steps / elapsed
 
     # roofline of the dominant kernel (HIP-event durations on the engine's stream)
@@ -146,8 +153,12 @@ def main():
     tick_ms = prof["tick_ms"] / max(prof["tick_n"], 1)
     obs_ms = prof["obs_ms"] / max(prof["obs_n"], 1)
     reset_ms = prof["reset_ms"] / max(prof["reset_n"], 1)
-    if tick_ms >= obs_ms:
-        dom, dom_ms, dom_b = "k_tick", tick_ms, tick_b
+    fused = prof["reset_n"] == 0  # reset work runs inside the step launch (k_step)
+    fobs = prof["obs_n"] == 0      # the step launch writes the observations itself
+    step_name = "k_step" if fused else "k_tick"
+    step_b = tick_b + (obs_b if fobs else 0)
+    if fobs or tick_ms >= obs_ms:
+        dom, dom_ms, dom_b = step_name, tick_ms, step_b
     else:
         dom, dom_ms, dom_b = "k_obs", obs_ms, obs_b
     achieved = dom_b * n_local / (dom_ms * 1e-3) / 1e9
@@ -162,20 +173,21 @@ def main():
     out = {
         "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "int32", "data": "synthetic",
-        "config": {"workload": "C3 shard: %d %dx%d '%s' envs per GPU (%d total), extermination, %d agents + %d "
-                               "zombies, uniform Discrete(7) policy on device, 21x21x3 %s obs per agent, "
-                               "TimeLimit %d, next-step autoreset" % (
-                                   n_local, m.size[0], m.size[1], args.map, total_envs, args.agents,
-                                   args.zombies, args.obs_dtype, args.max_episode_steps),
+        "scaling": scaling, "vs_baseline": None, "dtype": "int32", "data": "synthetic",
+        "config": {"workload": "%d parallel %dx%d '%s' envs over %d GPU(s) (%d per GPU), extermination, %d agents + "
+                               "%d zombies, MultiagentZombsoleEnv rewards, uniform Discrete(7) policy on device, "
+                               "21x21x3 %s obs per agent written to HBM every step, TimeLimit %d, next-step "
+                               "autoreset" % (total_envs, m.size[0], m.size[1], args.map, world, n_local,
+                                              args.agents, args.zombies, args.obs_dtype, args.max_episode_steps),
                    "envs_per_gpu": n_local, "total_envs": total_envs, "map": args.map,
                    "agents": args.agents, "zombies": args.zombies, "obs_dtype": args.obs_dtype,
                    "parallelism": "env-sharded x%d (no data-path collective)" % world},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
                      "algorithmic_bytes_per_launch": dom_b * n_local,
-                     "avg_launch_ms": dom_ms, "k_tick_ms": tick_ms, "k_obs_ms": obs_ms,
-                     "k_reset_ms": reset_ms},
+                     "avg_launch_ms": dom_ms, "step_launch_ms": tick_ms, "k_obs_ms": obs_ms,
+                     "k_reset_ms": reset_ms, "step_launch_writes_obs": bool(fobs),
+                     "step_launch_resets": bool(fused)},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -1,7 +1,7 @@
 // engine.hip — MI355X-native batched zombsole step engine (gfx950) and its C ABI.
 //
 // k_tick (zs_tick.hpp) steps 64/G envs per wave with G lanes per env and the env's hot
-// state in LDS; k_obs encodes the observations cell-parallel, one workgroup per env;
+// state in LDS; k_obs (zs_obs.hpp) encodes the observations, one wave per env;
 // k_seed / k_gen_actions / k_get_state / k_set_state are the small helpers behind the ABI.
 //
 // Semantics follow the reference exactly (parity: tests/); every sqrt range
@@ -17,108 +17,22 @@
 #include "zs_device.hpp"
 
 #include "zs_reset.hpp"
+#include "zs_obs.hpp"
 
 // One launch per step: workgroups [0, n_reset) rebuild the envs of the pending list (next-step
 // autoreset, World rebuilt as in game.py:151-169), the others tick every other env (zs_tick.hpp).
 // An env is either pending (reset work only; the tick reports it as reset without touching its
 // state) or stepping (tick only), so the two roles never share an env.
 template <int G>
-__global__ void __launch_bounds__(64) k_step(Dev d, int n_reset, const int32_t* actions, double* rew,
+__global__ void __launch_bounds__(64, ZS_STEP_WAVES) k_step(Dev d, int n_reset, const int32_t* actions, double* rew,
                                              uint8_t* done_out, uint8_t* trunc_out, uint8_t* listed_out,
                                              uint8_t* reset_out, int* reset_list, int* reset_count,
                                              const int* cur_list, const int* cur_count, int* err_out, void* obs_out) {
     if ((int)blockIdx.x < n_reset)
         reset_role(d, 1, cur_list, cur_count, nullptr, err_out, blockIdx.x, n_reset, d.fobs ? obs_out : nullptr);
     else
-        tick_wg<G>(d, blockIdx.x - n_reset, actions, rew, done_out, trunc_out, listed_out, reset_out, reset_list,
+        tick_wg<G>(d, xcd_remap(blockIdx.x - n_reset, gridDim.x - n_reset), actions, rew, done_out, trunc_out, listed_out, reset_out, reset_list,
                    reset_count, obs_out);
-}
-
-// ---------------------------------------------------------------------------
-// observations (gym/observation.py:36-173): one workgroup per env.  The env's entity slots
-// are scattered into an LDS cell grid first, then every thread encodes cells of the
-// agents' windows (or of the whole map) and streams the int64/int32/int16 planes out.
-// ---------------------------------------------------------------------------
-template <typename T>
-__global__ void __launch_bounds__(256) k_obs(Dev d, T* out, const uint8_t* mask, int grid_bytes) {
-    extern __shared__ __align__(16) uint8_t sgrid[];
-    const int e = blockIdx.x;
-    if (mask && !mask[e]) return;
-    const int tid = threadIdx.x;
-    if (grid_bytes) {
-        uint4* g4 = (uint4*)sgrid;
-        for (int i = tid; i < grid_bytes / 16; i += blockDim.x) g4[i] = make_uint4(0, 0, 0, 0);
-        __syncthreads();
-        for (int s = tid; s < d.E; s += blockDim.x)
-            if (d.present[(size_t)s * d.N + e]) {
-                int32_t p = d.pos[(size_t)s * d.N + e];
-                sgrid[unpack_y(p) * d.W + unpack_x(p)] = (uint8_t)(s + 1);
-            }
-        __syncthreads();
-    }
-    const bool world = d.obs_scope == ZS_OBS_WORLD;
-    const int nobs = world ? 1 : (d.reward_mode == ZS_REWARD_MULTI ? d.A : 1);
-    const int hh = world ? d.H : d.obs_w, ww = world ? d.W : d.obs_w, half = d.obs_w / 2;
-    const int C = d.obs_enc == ZS_ENC_CHANNELS ? 3 : 1;
-    const long plane = (long)hh * ww;
-    T* o = out + (size_t)e * nobs * C * plane;
-    const uint32_t* pres = d.obst_present + (size_t)e * d.OW;
-    const uint32_t* deadb = d.dead + (size_t)e * d.DW;
-    for (long idx = tid; idx < nobs * plane; idx += blockDim.x) {
-        int a = (int)(idx / plane);
-        int cell = (int)(idx - (long)a * plane);
-        int r = cell / ww, q = cell - r * ww;
-        int x, y;
-        if (world) {
-            x = q;
-            y = r;
-        } else {
-            int32_t ap = d.pos[(size_t)a * d.N + e];
-            x = unpack_x(ap) - half + q;
-            y = unpack_y(ap) - half + r;
-        }
-        int code, life, weapon = 0;
-        if (x < 0 || y < 0 || x >= d.W || y >= d.H) {  // Wall(position) out of bounds
-            code = ZS_THING_WALL;
-            life = 200;
-        } else {
-            int mc = y * d.W + x;
-            int s = -1;
-            if (grid_bytes) {
-                s = (int)sgrid[mc] - 1;
-            } else {
-                int32_t pk = pack_xy(x, y);
-                for (int k = 0; k < d.E && s < 0; k++)
-                    if (d.present[(size_t)k * d.N + e] && d.pos[(size_t)k * d.N + e] == pk) s = k;
-            }
-            if (s >= 0) {
-                life = d.life[(size_t)s * d.N + e];
-                weapon = d.weapon[(size_t)s * d.N + e];
-                code = s < d.A ? (d.obs_enc == ZS_ENC_CHANNELS ? d.agent_codes[s] : ZS_THING_AGENT)
-                               : (s < d.A + d.P ? ZS_THING_PLAYER : ZS_THING_ZOMBIE);
-            } else {
-                int oi = d.cellmap[mc];
-                if (oi >= 0 && ((pres[oi >> 5] >> (oi & 31)) & 1u)) {
-                    code = d.obst_kind[oi];
-                    life = d.obst_hp[(size_t)e * d.O + oi];
-                } else {
-                    life = 0;
-                    code = ((deadb[mc >> 5] >> (mc & 31)) & 1u)        ? ZS_THING_DEADBODY
-                           : ((d.objbits[mc >> 5] >> (mc & 31)) & 1u) ? ZS_THING_OBJECTIVE
-                                                                        : ZS_THING_NONE;
-                }
-            }
-        }
-        T* oa = o + (size_t)a * C * plane + cell;
-        if (C == 1) {
-            int64_t adj = life < 100 ? life : 100;
-            oa[0] = (T)(256 * (int64_t)code + 16 * (int64_t)weapon + floordiv100(15 * adj));
-        } else {
-            oa[0] = (T)code;
-            oa[plane] = (T)life;
-            oa[2 * plane] = (T)weapon;
-        }
-    }
 }
 
 // ---------------------------------------------------------------------------
@@ -325,7 +239,8 @@ struct zs_handle {
     Dev d;
     int G;          // lanes per env in k_tick
     size_t lds;     // k_tick dynamic LDS bytes
-    int obs_grid;   // k_obs LDS cell-grid bytes (0 = scan fallback)
+    ObsLayout obs_l;  // k_obs per-wave LDS image
+    int obs_wpg;      // k_obs waves (envs) per workgroup
     int state_words;
     std::vector<void*> allocs;
     int32_t* d_state;
@@ -337,6 +252,8 @@ struct zs_handle {
     int rpar = 0;
     size_t reset_lds = 0;
     int fused = 0;  // zs_step runs reset work and the tick in one launch (k_step)
+    int resident = 0;  // step-launch workgroups resident per CU (layout choice)
+    int want = 0;      // workgroups per CU the launch has (capped at 32)
     // diagnostics: HIP events bracketing every k_tick / k_obs launch on its stream
     int prof = 0;
     std::vector<hipEvent_t> ev_pool;
@@ -428,9 +345,11 @@ static int validate(const zs_config* c) {
     return ZS_OK;
 }
 
-// Pick lanes-per-env G, the LDS RNG window and the LDS candidate list so one workgroup's
-// image fits the 64 KiB dynamic-LDS budget.
-// workgroups of the step launch resident at once on 256 CUs decide how much LDS one may take
+// Layout of the step launch.  Workgroups of the launch resident at once on the 256 CUs decide how
+// much LDS one may take: among the layouts that fit 64 KiB, take the one with the most resident
+// workgroups (at most 32 one-wave workgroups per CU), then the largest optional LDS copies (RNG
+// window beyond 64 words, spawn candidates, spawn lists).  A fused launch (reset work + tick in
+// one) allocates max(tick image, reset image) for every workgroup.
 static const int kResetWGs = 256;  // reset-work workgroups of a fused step launch
 
 static bool getenv_off(const char* name) {
@@ -438,52 +357,37 @@ static bool getenv_off(const char* name) {
     return f && atoi(f) == 0;
 }
 
-static int choose_layout(zs_handle* h, int want_g, bool fobs_ok) {
+static int choose_layout(zs_handle* h, int want_g, bool fused, int obs_bytes) {
     Dev& d = h->d;
     const int kMax = 64 * 1024;
     int g0 = want_g > 0 ? want_g : 16;  // measured: G=16 and 32 beat 8 and 64 at C3 (tools/sweep_lanes.sh)
     int cand_full = (d.W * d.H <= 65535) ? d.ncand : 0;
     int lists = (d.nps + d.nzs <= 4096) ? d.nps + d.nzs : 0;
-    d.fobs = 0;
-    if (fobs_ok) {
-        // tick + observation image in one workgroup: keep every workgroup of the launch resident
-        // (160 KB LDS per CU), dropping the optional LDS copies (spawn lists, candidates) first
-        int ne = 64 / g0;
-        int wgs = (d.N + ne - 1) / ne + std::min(d.N, kResetWGs);
-        int per_cu = std::max(1, (wgs + 255) / 256);
-        int budget = std::min(kMax, std::max(16 * 1024, 160 * 1024 / per_cu));
+    for (int G = g0; G <= 64; G *= 2) {
+        int ne = 64 / G;
+        int wgs = (d.N + ne - 1) / ne + (fused ? std::min(d.N, kResetWGs) : 0);
+        int want = getenv_off("ZS_LDS_BUDGET") ? 1 : std::min(32, std::max(1, (wgs + 255) / 256));
+        int best_res = -1;
         for (int cand : {cand_full, 0})
             for (int lst : {lists, 0})
-                for (int rw : {256, 128, 64}) {
-                    TickLayout L = tick_layout(ne, d.E, d.DW, rw, cand, lst, d.A, 1, d.O);
-                    if (L.bytes <= budget) {
-                        h->G = g0;
+                for (int rw : {512, 256, 128, 64}) {
+                    int bytes = tick_layout(ne, d.E, d.DW, rw, cand, lst, d.A, obs_bytes).bytes;
+                    if (fused) bytes = std::max(bytes, reset_lds_bytes(d.E, d.DW, d.ncand, lst, obs_bytes));
+                    if (bytes > kMax) continue;
+                    int res = std::min(want, 160 * 1024 / bytes);
+                    h->want = want;
+                    if (res > best_res) {
+                        best_res = res;
+                        h->G = G;
                         d.rw_cap = rw;
                         d.rw_step = std::min(rw, 64);
                         d.cand_cap = cand;
                         d.lists_cap = lst;
-                        d.fobs = 1;
-                        h->lds = L.bytes;
-                        return ZS_OK;
+                        h->lds = bytes;
+                        h->resident = res;
                     }
                 }
-    }
-    for (int G = g0; G <= 64; G *= 2) {
-        int ne = 64 / G;
-        for (int cand : {cand_full, 0}) {
-            for (int rw : {512, 256, 128, 64}) {
-                TickLayout L = tick_layout(ne, d.E, d.DW, rw, cand, lists, d.A);
-                if (L.bytes <= kMax) {
-                    h->G = G;
-                    d.rw_cap = rw;
-                    d.rw_step = std::min(rw, 64);
-                    d.cand_cap = cand;
-                    d.lists_cap = lists;
-                    h->lds = L.bytes;
-                    return ZS_OK;
-                }
-            }
-        }
+        if (best_res > 0) return ZS_OK;
     }
     return fail(ZS_EINVAL, "entity table / map too large for the LDS image of one env");
 }
@@ -547,8 +451,8 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
         int cell = m.obstacle_xy[2 * i + 1] * d.W + m.obstacle_xy[2 * i];
         obstbits[cell >> 5] |= 1u << (cell & 31);
     }
-    // fused observations need obstacle index == rank of its cell among obstacle cells (row-major
-    // file order, as every map-file parse produces); boxbits / oprefix make the lookup LDS-only
+    // the observation store loop finds an obstacle's index as the rank of its cell among obstacle
+    // cells (zs_obs.hpp), valid when the obstacles are in row-major order (every map-file parse)
     bool rank_order = true;
     for (int i = 1; i < d.O; i++)
         if (m.obstacle_xy[2 * i + 1] * d.W + m.obstacle_xy[2 * i] <=
@@ -563,9 +467,15 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
     std::vector<int32_t> oprefix(d.DW, 0);
     for (int w = 1; w < d.DW; w++) oprefix[w] = oprefix[w - 1] + __builtin_popcount(obstbits[w - 1]);
     std::vector<uint32_t> objbits(d.DW, 0);
+    std::vector<int32_t> scell((size_t)d.W * d.H, 0);  // k_obs static per-cell word (zs_obs.hpp)
     for (int i = 0; i < m.n_objectives; i++) {
         int cell = m.objective_xy[2 * i + 1] * d.W + m.objective_xy[2 * i];
         objbits[cell >> 5] |= 1u << (cell & 31);
+        scell[cell] |= (int32_t)SC_OBJ_BIT;
+    }
+    for (int i = 0; i < d.O; i++) {
+        int cell = m.obstacle_xy[2 * i + 1] * d.W + m.obstacle_xy[2 * i];
+        scell[cell] |= (int32_t)((uint32_t)(i + 1) | ((uint32_t)m.obstacle_kind[i] << SC_KIND_SHIFT));
     }
     auto packlist = [](const int32_t* xy, int n) {
         std::vector<int32_t> v(n);
@@ -588,12 +498,13 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
     } while (0)
     int16_t* p_cellmap;
     uint32_t *p_objbits, *p_obstbits, *p_boxbits;
-    int32_t* p_oprefix;
+    int32_t *p_scell, *p_oprefix;
     int32_t *p_oxy, *p_ps, *p_zs, *p_aw, *p_ac, *p_bt;
     uint8_t* p_okind;
     TRY(dupload(h, &p_cellmap, cellmap));
     TRY(dupload(h, &p_objbits, objbits));
     TRY(dupload(h, &p_obstbits, obstbits));
+    TRY(dupload(h, &p_scell, scell));
     TRY(dupload(h, &p_boxbits, boxbits));
     TRY(dupload(h, &p_oprefix, oprefix));
     TRY(dupload(h, &p_oxy, oxy));
@@ -606,6 +517,7 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
     d.cellmap = p_cellmap;
     d.objbits = p_objbits;
     d.obstbits = p_obstbits;
+    d.scell = p_scell;
     d.boxbits = p_boxbits;
     d.oprefix = p_oprefix;
     d.obst_xy = p_oxy;
@@ -641,13 +553,45 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
     TRY(dalloc(h, &h->d_rlist[0], N));
     TRY(dalloc(h, &h->d_rlist[1], N));
     TRY(dalloc(h, &h->d_rcount, 2));
-    // workgroup: 64 envs (one wave) unless the LDS image of the entity table is too large
-    // the reset work's observation staging reuses its 2 x 624-word twist buffer
-    const bool fobs_ok = rank_order && (4 * d.DW + d.O) <= 2 * ZS_MT_N && !getenv_off("ZS_FOBS");
-    TRY(choose_layout(h, cfg->lanes_per_env, fobs_ok));
-    h->reset_lds = (size_t)reset_lds_bytes(d.E, d.DW, d.ncand, d.lists_cap);
-    if (d.fobs && h->reset_lds > h->lds) TRY(choose_layout(h, cfg->lanes_per_env, false));  // fobs needs k_step
-    h->reset_lds = (size_t)reset_lds_bytes(d.E, d.DW, d.ncand, d.lists_cap);
+    {
+        // observation images: k_obs (four envs per workgroup when their images fit 64 KiB, else one;
+        // window map and staged HP while one image fits 32 KiB) and, when the step launch writes the
+        // observations itself (fobs), one env's image inside the tick / reset LDS (HP staged when the
+        // image still fits the MT twist buffer it aliases).  ZS_OBS_WIN=0 forces the per-cell
+        // entity scan (parity tests of that path).
+        const bool world = d.obs_scope == ZS_OBS_WORLD;
+        const int nobs = obs_count(d.obs_scope, d.reward_mode, d.A);
+        const int plane = world ? d.W * d.H : d.obs_w * d.obs_w;
+        const bool win = !getenv_off("ZS_OBS_WIN");
+        ObsLayout L = obs_layout(nobs, plane, d.E, d.DW, d.OW, d.O, win, true);
+        if (L.bytes > 32 * 1024) L = obs_layout(nobs, plane, d.E, d.DW, d.OW, d.O, win, false);
+        if (L.bytes > 32 * 1024) L = obs_layout(nobs, plane, d.E, d.DW, d.OW, d.O, false, false);
+        if (L.bytes > 64 * 1024) {
+            free_all(h);
+            delete h;
+            return fail(ZS_EINVAL, "map too large for the observation kernel's LDS image");
+        }
+        // static tables (4 x DW words) beside the images: per k_obs workgroup, and inside the step
+        // launch's image region; ZS_OBS_STAT=0 forces the per-cell static words (parity tests)
+        d.obs_stat = (rank_order && d.DW <= 1024 && !getenv_off("ZS_OBS_STAT")) ? 4 * d.DW : 0;
+        h->obs_l = L;
+        h->obs_wpg = d.obs_stat * 4 + 4 * L.bytes <= 64 * 1024 ? 4 : 1;
+        d.obsl = L;
+        d.fobs = L.bytes + 4 * d.obs_stat <= 16 * 1024 && !getenv_off("ZS_FOBS");
+    }
+    // Fused step launch (reset work + tick in one) when the whole launch is resident at once: then
+    // the step is one latency-bound round and the reset work hides under the ticks (measured: 8192
+    // envs, 1 round, fused 0.097 ms vs 0.13 ms).  With many rounds per CU (65536 envs) the reset
+    // image and the reset role's registers cost every tick workgroup occupancy, so the reset work
+    // runs as its own short launch (0.54 ms vs 0.59 ms).  ZS_FUSED=0/1 forces either.
+    {
+        const int obs_b = d.fobs ? d.obsl.bytes + 4 * d.obs_stat : 0;
+        TRY(choose_layout(h, cfg->lanes_per_env, true, obs_b));
+        const char* fz = getenv("ZS_FUSED");
+        h->fused = fz ? atoi(fz) != 0 : h->resident >= h->want;
+        if (!h->fused) TRY(choose_layout(h, cfg->lanes_per_env, false, obs_b));
+        h->reset_lds = (size_t)reset_lds_bytes(d.E, d.DW, d.ncand, d.lists_cap, obs_b);
+    }
     if (h->reset_lds > 160 * 1024) {
         free_all(h);
         delete h;
@@ -660,19 +604,11 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
         delete h;
         return fail(ZS_EHIP, "cannot raise k_reset's dynamic LDS limit");
     }
-    // one launch for reset work + tick when the reset image fits the tick's LDS allocation
-    // (otherwise the tick's occupancy would pay for the larger reset image)
-    h->fused = h->reset_lds <= h->lds ? 1 : 0;
-    if (getenv_off("ZS_FUSED")) h->fused = 0;
-    if (!h->fused) d.fobs = 0;
     if (getenv("ZS_VERBOSE"))
-        fprintf(stderr, "zs_create: N=%d E=%d G=%d tick_lds=%zu reset_lds=%zu rw_cap=%d cand_cap=%d lists_cap=%d "
-                        "fused=%d fobs=%d\n", d.N, d.E, h->G, h->lds, h->reset_lds, d.rw_cap, d.cand_cap, d.lists_cap,
-                h->fused, d.fobs);
-    {
-        int gb = ((d.W * d.H + 15) / 16) * 16;
-        h->obs_grid = gb <= 64 * 1024 ? gb : 0;
-    }
+        fprintf(stderr, "zs_create: N=%d E=%d G=%d step_lds=%zu resident=%d reset_lds=%zu rw_cap=%d cand_cap=%d "
+                        "lists_cap=%d fused=%d fobs=%d obs_img=%d k_obs_img=%d x%d\n", d.N, d.E, h->G, h->lds,
+                h->resident, h->reset_lds, d.rw_cap, d.cand_cap, d.lists_cap, h->fused, d.fobs, d.obsl.bytes,
+                h->obs_l.bytes, h->obs_wpg);
     if (d.O > 0) {
         size_t n = N * d.O;
         hipLaunchKernelGGL(k_init_obstacles, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, d);
@@ -735,12 +671,15 @@ static int launch_obs(zs_handle* h, void* obs, const uint8_t* mask, hipStream_t 
     if (!obs) return ZS_OK;
     int i0 = -1, i1 = -1;
     if (h->prof) HIPCHK(hipEventRecord(prof_event(h, &i0), s));
+    const unsigned grid = (unsigned)((d.N + h->obs_wpg - 1) / h->obs_wpg);
+    const dim3 blk(64 * h->obs_wpg);
+    const size_t lds = (size_t)d.obs_stat * 4 + (size_t)h->obs_wpg * h->obs_l.bytes;
     if (d.obs_dtype == ZS_DTYPE_I64)
-        hipLaunchKernelGGL(k_obs<int64_t>, dim3(d.N), dim3(256), h->obs_grid, s, d, (int64_t*)obs, mask, h->obs_grid);
+        hipLaunchKernelGGL(k_obs<int64_t>, dim3(grid), blk, lds, s, d, (int64_t*)obs, mask, h->obs_l, d.obs_stat);
     else if (d.obs_dtype == ZS_DTYPE_I32)
-        hipLaunchKernelGGL(k_obs<int32_t>, dim3(d.N), dim3(256), h->obs_grid, s, d, (int32_t*)obs, mask, h->obs_grid);
+        hipLaunchKernelGGL(k_obs<int32_t>, dim3(grid), blk, lds, s, d, (int32_t*)obs, mask, h->obs_l, d.obs_stat);
     else
-        hipLaunchKernelGGL(k_obs<int16_t>, dim3(d.N), dim3(256), h->obs_grid, s, d, (int16_t*)obs, mask, h->obs_grid);
+        hipLaunchKernelGGL(k_obs<int16_t>, dim3(grid), blk, lds, s, d, (int16_t*)obs, mask, h->obs_l, d.obs_stat);
     HIPCHK(hipGetLastError());
     if (h->prof) {
         HIPCHK(hipEventRecord(prof_event(h, &i1), s));
@@ -767,7 +706,7 @@ static int launch_tick(zs_handle* h, const int32_t* actions, double* rew, uint8_
                            (const int*)(h->d_rcount + p), h->d_err, obs);                                             \
     else                                                                                                              \
         hipLaunchKernelGGL(k_tick<GG>, dim3(grid), dim3(64), h->lds, s, d, actions, rew, done, trunc, listed,        \
-                           reset_out, rlist, rcount)
+                           reset_out, rlist, rcount, obs)
     switch (h->G) {
     case 1: ZS_TICK(1); break;
     case 2: ZS_TICK(2); break;
@@ -786,14 +725,14 @@ static int launch_tick(zs_handle* h, const int32_t* actions, double* rew, uint8_
     return ZS_OK;
 }
 
-static int launch_reset(zs_handle* h, int list_mode, const uint8_t* mask, hipStream_t s) {
+static int launch_reset(zs_handle* h, int list_mode, const uint8_t* mask, void* obs, hipStream_t s) {
     const Dev& d = h->d;
     unsigned grid = (unsigned)std::min(d.N, list_mode ? 512 : 4096);
     int p = h->rpar;
     int i0 = -1, i1 = -1;
     if (h->prof) HIPCHK(hipEventRecord(prof_event(h, &i0), s));
     hipLaunchKernelGGL(k_reset, dim3(grid), dim3(64), h->reset_lds, s, d, list_mode, h->d_rlist[p], h->d_rcount + p,
-                       mask, h->d_err);
+                       mask, h->d_err, obs);
     HIPCHK(hipGetLastError());
     if (h->prof) {
         HIPCHK(hipEventRecord(prof_event(h, &i1), s));
@@ -807,7 +746,7 @@ extern "C" int zs_reset(zs_handle* h, const uint8_t* env_mask_dev, void* obs_dev
     hipStream_t s = (hipStream_t)stream;
     HIPCHK(hipSetDevice(h->device));
     HIPCHK(hipMemsetAsync(h->d_err, 0, sizeof(int), s));
-    int rc = launch_reset(h, 0, env_mask_dev, s);
+    int rc = launch_reset(h, 0, env_mask_dev, nullptr, s);
     if (rc) return rc;
     // the pending-reset list must hold exactly the envs still pending: drop the ones just rebuilt
     {
@@ -851,7 +790,7 @@ extern "C" int zs_step(zs_handle* h, const int32_t* actions_dev, void* obs_dev, 
     //    when the LDS images allow, else a k_reset launch first
     int q = 1 - h->rpar, rc = ZS_OK;
     if (!h->fused) {
-        rc = launch_reset(h, 1, nullptr, s);
+        rc = launch_reset(h, 1, nullptr, h->d.fobs ? obs_dev : nullptr, s);
         if (rc) return rc;
     }
     // 2) tick every other env; envs that end now are queued on list[q] for the next call

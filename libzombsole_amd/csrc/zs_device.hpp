@@ -18,6 +18,11 @@
 
 #include "../../include/zombsole_mi355x.h"
 
+// minimum waves per SIMD the one-wave step / tick / reset kernels are compiled for (register budget)
+#ifndef ZS_STEP_WAVES
+#define ZS_STEP_WAVES 1
+#endif
+
 #define ZS_MT_N 624
 #define ZS_MT_M 397
 #define ZS_RING_WORDS (2 * ZS_MT_N)
@@ -36,6 +41,37 @@ enum {
     S_NSCAL
 };
 
+// one env's observation image in LDS (zs_obs.hpp)
+struct ObsLayout {
+    int win;     // window-map bytes (0: no window map, entities found by a per-cell scan)
+    int off_pos, off_life, off_cw, off_dead, off_opres, off_hp;
+    int hp_cap;  // obstacle HP staged in LDS (else read from HBM)
+    int bytes;   // one env's image
+};
+
+__host__ __device__ inline ObsLayout obs_layout(int nobs, int plane, int E, int DW, int OW, int O, bool winmap,
+                                                bool stage_hp) {
+    ObsLayout L;
+    int o = 0;
+    L.win = winmap ? ((nobs * plane + 15) / 16) * 16 : 0;
+    o += L.win;
+    L.off_pos = o;
+    o += E * 4;
+    L.off_life = o;
+    o += E * 4;
+    L.off_cw = o;
+    o += E * 4;
+    L.off_dead = o;
+    o += DW * 4;
+    L.off_opres = o;
+    o += OW * 4;
+    L.off_hp = o;
+    L.hp_cap = stage_hp ? O : 0;
+    o += L.hp_cap * 4;
+    L.bytes = ((o + 15) / 16) * 16;
+    return L;
+}
+
 struct Dev {
     int N, W, H, O, A, P, Z, E, OW, DW, ncand, nps, nzs, nobj;
     int rw_cap;      // RNG window words staged in LDS per env (tick kernel)
@@ -43,6 +79,8 @@ struct Dev {
     int cand_cap;    // spawn-candidate entries staged in LDS per env (0 = global scratch)
     int lists_cap;   // static spawn-list entries staged in LDS per workgroup (0 = read from global)
     int fobs;        // observations are written by the step launch itself (tick and reset work)
+    ObsLayout obsl;  // one env's observation image (zs_obs.hpp)
+    int obs_stat;    // static observation tables staged beside the image (4 * DW words), 0 = none
     int rules, reward_mode, obs_scope, obs_enc, obs_w, obs_dtype, max_steps;
     int initial_zombies, minimum_zombies;
     uint32_t flags;
@@ -50,7 +88,8 @@ struct Dev {
     const int16_t* cellmap;
     const uint32_t* obstbits;  // static obstacle occupancy bitmap [DW]
     const uint32_t* objbits;
-    const uint32_t* boxbits;   // static: cell holds a Box (map file) [DW]
+    const int32_t* scell;      // static: per-cell obstacle index + 1 | code << 16 | objective << 20 (zs_obs.hpp)
+    const uint32_t* boxbits;   // static: cell holds a Box [DW]
     const int32_t* oprefix;    // static: obstacles in cells < 32*w (obstacle index = cell rank) [DW]
     const int32_t* obst_xy;  // packed x | y << 16
     const uint8_t* obst_kind;
@@ -163,4 +202,33 @@ __device__ __forceinline__ int64_t floordiv100(int64_t a) {  // Python a // 100
     int64_t q = a / 100;
     if ((a % 100) != 0 && a < 0) q -= 1;
     return q;
+}
+
+// Explicit LDS (address space 3) pointer types for every view into the workgroup's image, so the
+// compiler always emits ds_* instructions (a pointer that might be LDS or global degrades to
+// flat accesses and pushes the lane context to scratch).
+#define ZS_LDS __attribute__((address_space(3)))
+typedef ZS_LDS uint32_t lu32;
+typedef ZS_LDS int32_t li32;
+typedef ZS_LDS uint16_t lu16;
+typedef ZS_LDS uint8_t lu8;
+
+// Stage n global words into LDS: lane `lane0` of a team of `step` lanes copies elements
+// lane0, lane0 + step, ...  All loads of a chunk of 8 are issued before any LDS store, so one
+// memory latency is paid per chunk instead of one per element.
+template <typename T, typename LT, typename Idx>
+__device__ __forceinline__ void stage_in(const T* src, int n, int lane0, int step, LT* dst, Idx dst_index) {
+    for (int b = lane0; b < n; b += 8 * step) {
+        T v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            int i = b + u * step;
+            v[u] = src[i < n ? i : n - 1];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            int i = b + u * step;
+            if (i < n) dst[dst_index(i)] = v[u];
+        }
+    }
 }

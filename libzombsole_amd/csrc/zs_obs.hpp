@@ -1,0 +1,346 @@
+// zs_obs.hpp — the observation encoder (gym/observation.py:36-173), one wave per env.
+//
+// Observations are the bulk of the bytes a step moves (21 KB per env-step at C3, int64), so the
+// encoder is shaped as a store stream with as little per-cell work as possible:
+//   * one wave owns one env and writes its whole [nobs][C][h][w] block, so every store
+//     instruction of the wave covers 64 consecutive cells of one plane (512 B of int64);
+//   * the env's dynamic state is staged once into a wave-private LDS image: a "window map"
+//     (one byte per observed cell: entity slot + 1, scattered from the <= E entity positions —
+//     the reference's `things` lookup, observation.py:57-66, without a per-cell search), the
+//     entities' positions, (code, weapon, present) and life, the dead-body bitmap, obstacle
+//     presence and (when it fits) obstacle HP;
+//   * the static map (obstacle index and kind, objective flag) is one int32 per cell shared by
+//     all envs and served from L1/L2.
+// The same two steps (obs_build, obs_stream) run in three places: k_obs (zs_reset, zs_observe,
+// and steps whose image does not fit the step launch), the step launch's tick workgroups right
+// after an env's tick, and its reset work right after an env's rebuild — so a step writes its
+// observations while other workgroups of the same launch are still ticking.
+// Per cell: out of bounds -> Wall(200) (observation.py:69-76); entity (things first); present
+// obstacle (Box / Wall with its HP); dead body; objective; empty.
+#pragma once
+#include "zs_device.hpp"
+
+// static per-cell word: bits 0..15 obstacle index + 1 (0 = none), 16..18 obstacle code, bit 20 objective
+#define SC_OBST_MASK 0xffffu
+#define SC_KIND_SHIFT 16
+#define SC_OBJ_BIT (1u << 20)
+
+// observations per env
+__host__ __device__ inline int obs_count(int scope, int reward_mode, int A) {
+    return scope == ZS_OBS_WORLD ? 1 : (reward_mode == ZS_REWARD_MULTI ? A : 1);
+}
+
+// workgroup b of nb -> XCD-contiguous virtual workgroup id (a bijection on [0, nb)).  The hardware
+// deals workgroups round-robin to the 8 XCDs; this gives each XCD a contiguous range of envs, so
+// the env-minor entity rows one XCD's L2 holds are the rows its own waves read.
+__device__ __forceinline__ int xcd_remap(int b, int nb) {
+    const int q = nb >> 3, r = nb & 7, x = b & 7, k = b >> 3;
+    return x * q + (x < r ? x : r) + k;
+}
+
+__device__ __forceinline__ int floordiv100_i32(int a) {  // Python a // 100
+    int q = a / 100;
+    if (q * 100 != a && a < 0) q -= 1;
+    return q;
+}
+
+template <typename T>
+__device__ __forceinline__ void obs_store(T* o, int plane, int cell, bool ch, int code, int life, int weapon) {
+    if (!ch) {
+        const int adj = life < 100 ? life : 100;
+        // 15 * adj // 100 (Python floor division); 32-bit fast path for every reachable life
+        const int64_t f = adj >= -(1 << 26) ? (int64_t)floordiv100_i32(15 * adj) : floordiv100(15 * (int64_t)adj);
+        o[cell] = (T)(256 * (int64_t)code + 16 * (int64_t)weapon + f);
+    } else {
+        o[cell] = (T)code;
+        o[plane + cell] = (T)life;
+        o[2 * plane + cell] = (T)weapon;
+    }
+}
+
+// Fill env e's image (all 64 lanes of the wave).  ent(s, pos, life, weapon, present) reads entity
+// slot s from wherever the caller holds it (HBM, or the tick / reset LDS image).
+template <typename Ent>
+__device__ __forceinline__ void obs_build(const Dev& d, const ObsLayout& L, lu8* img, int e, Ent ent) {
+    const int lane = threadIdx.x & 63;
+    const int E = d.E, A = d.A;
+    const bool world = d.obs_scope == ZS_OBS_WORLD;
+    const int nobs = obs_count(d.obs_scope, d.reward_mode, A);
+    const int hh = world ? d.H : d.obs_w, ww = world ? d.W : d.obs_w, half = d.obs_w / 2;
+    const int plane = hh * ww;
+    const bool ch = d.obs_enc == ZS_ENC_CHANNELS;
+    li32* pos = (li32*)(img + L.off_pos);
+    li32* life = (li32*)(img + L.off_life);
+    li32* cw = (li32*)(img + L.off_cw);
+    for (int w = lane; w < L.win / 4; w += 64) ((lu32*)img)[w] = 0u;
+    for (int s = lane; s < E; s += 64) {
+        int p, lf, wp, pr;
+        ent(s, p, lf, wp, pr);
+        const int code = s < A ? (ch ? d.agent_codes[s] : ZS_THING_AGENT) : (s < A + d.P ? ZS_THING_PLAYER : ZS_THING_ZOMBIE);
+        pos[s] = p;
+        life[s] = lf;
+        cw[s] = code | (wp << 8) | (pr << 16);
+    }
+    stage_in(d.dead + (size_t)e * d.DW, d.DW, lane, 64, (lu32*)(img + L.off_dead), [](int w) { return w; });
+    stage_in(d.obst_present + (size_t)e * d.OW, d.OW, lane, 64, (lu32*)(img + L.off_opres), [](int w) { return w; });
+    if (L.hp_cap) stage_in(d.obst_hp + (size_t)e * d.O, d.O, lane, 64, (li32*)(img + L.off_hp), [](int w) { return w; });
+    wave_sync();
+    if (L.win) {  // scatter the present entities into the window map
+        for (int s = lane; s < E; s += 64) {
+            if (!((cw[s] >> 16) & 1)) continue;
+            const int32_t p = pos[s];
+            const int x = unpack_x(p), y = unpack_y(p);
+            for (int a = 0; a < nobs; a++) {
+                int ox = 0, oy = 0;
+                if (!world) {
+                    const int32_t ap = pos[a];
+                    ox = unpack_x(ap) - half;
+                    oy = unpack_y(ap) - half;
+                }
+                const int dx = x - ox, dy = y - oy;
+                if (dx >= 0 && dy >= 0 && dx < ww && dy < hh) img[a * plane + dy * ww + dx] = (uint8_t)(s + 1);
+            }
+        }
+        wave_sync();
+    }
+}
+
+// static tables (LDS, 4 x DW words): [0, DW) obstacle bits, [DW, 2DW) box bits, [2DW, 3DW)
+// objective bits, [3DW, 4DW) obstacles in cells below word w.  With the map's obstacles in
+// row-major order (every map-file parse) the obstacle index of a cell is its rank, so these replace
+// the per-cell static words and keep the store loop free of global loads: any global load inside
+// it would make the wave wait (vmcnt is in order) for every store it has issued before.
+__device__ __forceinline__ void obs_stage_static(const Dev& d, lu32* st, int t0, int nt) {
+    stage_in(d.obstbits, d.DW, t0, nt, st, [](int w) { return w; });
+    stage_in(d.boxbits, d.DW, t0, nt, st + d.DW, [](int w) { return w; });
+    stage_in(d.objbits, d.DW, t0, nt, st + 2 * d.DW, [](int w) { return w; });
+    stage_in((const uint32_t*)d.oprefix, d.DW, t0, nt, st + 3 * d.DW, [](int w) { return w; });
+}
+
+// Stream env e's observations from its image: lane handles cells lane, lane + 64, ... of every
+// observation.  out = the base of the [N][nobs][C][h][w] tensor.
+//
+// Fast path (static tables in st, HP and window map in the image): every lookup is an LDS read and
+// the cell's value is selected branch-free.  The registered width (21) is a compile-time constant.
+__device__ __forceinline__ void obs_cell_fast(const Dev& d, const ObsLayout& L, const lu32* st, const lu8* img,
+                                              const lu8* wm, int cell, int x, int y, int& code, int& lf, int& weapon) {
+    const int DW = d.DW, W = d.W, H = d.H;
+    const li32* life = (const li32*)(img + L.off_life);
+    const li32* cw = (const li32*)(img + L.off_cw);
+    const lu32* dead = (const lu32*)(img + L.off_dead);
+    const lu32* opres = (const lu32*)(img + L.off_opres);
+    const li32* hp = (const li32*)(img + L.off_hp);
+    const bool inb = (unsigned)x < (unsigned)W && (unsigned)y < (unsigned)H;
+    const int c = inb ? y * W + x : 0, w = c >> 5;
+    const uint32_t bit = 1u << (c & 31);
+    const int sb = wm[cell];  // entity slot + 1, or 0
+    const int sidx = sb ? sb - 1 : 0;
+    const int v = cw[sidx], elife = life[sidx];
+    const uint32_t ob = st[w], bx = st[DW + w], objw = st[2 * DW + w], dw = dead[w];
+    const bool isob = (ob & bit) != 0u;
+    const int oi = isob ? (int)st[3 * DW + w] + __popc(ob & (bit - 1u)) : 0;
+    const uint32_t opw = opres[oi >> 5];
+    const int ohp = hp[oi];
+    const bool obp = isob && ((opw >> (oi & 31)) & 1u);
+    code = (dw & bit) ? ZS_THING_DEADBODY : (objw & bit) ? ZS_THING_OBJECTIVE : ZS_THING_NONE;
+    code = obp ? ((bx & bit) ? ZS_THING_BOX : ZS_THING_WALL) : code;
+    code = sb ? (v & 255) : code;
+    code = inb ? code : ZS_THING_WALL;
+    lf = sb ? elife : (obp ? ohp : 0);
+    lf = inb ? lf : 200;
+    weapon = (inb && sb) ? ((v >> 8) & 255) : 0;
+}
+
+template <typename T, int WW>
+__device__ __forceinline__ void obs_stream_fast(const Dev& d, const ObsLayout& L, const lu32* st, const lu8* img, T* out,
+                                                int e) {
+    const int lane = threadIdx.x & 63;
+    const bool world = d.obs_scope == ZS_OBS_WORLD;
+    const int nobs = obs_count(d.obs_scope, d.reward_mode, d.A);
+    const bool ch = d.obs_enc == ZS_ENC_CHANNELS;
+    const li32* pos = (const li32*)(img + L.off_pos);
+    if (WW > 0) {  // registered width: compile-time plane and row stepping
+        constexpr int PLANE = WW > 0 ? WW * WW : 1, SR = WW > 0 ? 64 / WW : 0, SQ = 64 - SR * WW;
+        const int C = ch ? 3 : 1;
+        for (int a = 0; a < nobs; a++) {
+            const int32_t ap = pos[a];
+            const int ox = unpack_x(ap) - WW / 2, oy = unpack_y(ap) - WW / 2;
+            const lu8* wm = img + a * PLANE;
+            T* o = out + ((size_t)e * nobs + a) * C * PLANE;
+            int r = lane / (WW > 0 ? WW : 1), q = lane - r * WW;
+            for (int cell = lane; cell < PLANE; cell += 64) {
+                int code, lf, weapon;
+                obs_cell_fast(d, L, st, img, wm, cell, ox + q, oy + r, code, lf, weapon);
+                obs_store(o, PLANE, cell, ch, code, lf, weapon);
+                q += SQ;
+                r += SR;
+                if (q >= WW) {
+                    q -= WW;
+                    r++;
+                }
+            }
+        }
+        return;
+    }
+    const int W = d.W, H = d.H;
+    const int ww = world ? W : d.obs_w, hh = world ? H : d.obs_w, half = ww / 2;
+    const int plane = hh * ww, C = ch ? 3 : 1;
+    const int step_r = 64 / ww, step_q = 64 - step_r * ww;
+    for (int a = 0; a < nobs; a++) {
+        int ox = 0, oy = 0;
+        if (!world) {
+            const int32_t ap = pos[a];
+            ox = unpack_x(ap) - half;
+            oy = unpack_y(ap) - half;
+        }
+        T* o = out + ((size_t)e * nobs + a) * C * plane;
+        const lu8* wm = img + a * plane;
+        int r = lane / ww, q = lane - (lane / ww) * ww;
+        for (int cell = lane; cell < plane; cell += 64) {
+            int code, lf, weapon;
+            obs_cell_fast(d, L, st, img, wm, cell, ox + q, oy + r, code, lf, weapon);
+            obs_store(o, plane, cell, ch, code, lf, weapon);
+            q += step_q;
+            r += step_r;
+            if (q >= ww) {
+                q -= ww;
+                r++;
+            }
+        }
+    }
+}
+
+// General path: per-cell static words from L1/L2, HP from HBM when not staged, the per-cell
+// entity scan when there is no window map.
+template <typename T>
+__device__ __forceinline__ void obs_stream_gen(const Dev& d, const ObsLayout& L, const lu8* img, T* out, int e) {
+    const int lane = threadIdx.x & 63;
+    const int E = d.E;
+    const bool world = d.obs_scope == ZS_OBS_WORLD;
+    const int nobs = obs_count(d.obs_scope, d.reward_mode, d.A);
+    const int hh = world ? d.H : d.obs_w, ww = world ? d.W : d.obs_w, half = d.obs_w / 2;
+    const bool ch = d.obs_enc == ZS_ENC_CHANNELS;
+    const int plane = hh * ww, C = ch ? 3 : 1;
+    const li32* pos = (const li32*)(img + L.off_pos);
+    const li32* life = (const li32*)(img + L.off_life);
+    const li32* cw = (const li32*)(img + L.off_cw);
+    const lu32* dead = (const lu32*)(img + L.off_dead);
+    const lu32* opres = (const lu32*)(img + L.off_opres);
+    const li32* hp = (const li32*)(img + L.off_hp);
+    const int step_r = 64 / ww, step_q = 64 - step_r * ww;
+    for (int a = 0; a < nobs; a++) {
+        int ox = 0, oy = 0;
+        if (!world) {
+            const int32_t ap = pos[a];
+            ox = unpack_x(ap) - half;
+            oy = unpack_y(ap) - half;
+        }
+        T* o = out + ((size_t)e * nobs + a) * C * plane;
+        int r = lane / ww, q = lane - (lane / ww) * ww;
+        for (int cell = lane; cell < plane; cell += 64) {
+            const int x = ox + q, y = oy + r;
+            int code = ZS_THING_WALL, lf = 200, weapon = 0;
+            if (x >= 0 && y >= 0 && x < d.W && y < d.H) {
+                const int c = y * d.W + x;
+                int s = -1;
+                if (L.win) {
+                    s = (int)img[a * plane + cell] - 1;
+                } else {
+                    const int32_t pk = pack_xy(x, y);
+                    for (int k = 0; k < E && s < 0; k++)
+                        if (((cw[k] >> 16) & 1) && pos[k] == pk) s = k;
+                }
+                if (s >= 0) {
+                    const int v = cw[s];
+                    code = v & 255;
+                    weapon = (v >> 8) & 255;
+                    lf = life[s];
+                } else {
+                    const uint32_t sc = (uint32_t)d.scell[c];
+                    const int oi = (int)(sc & SC_OBST_MASK) - 1;
+                    lf = 0;
+                    if (oi >= 0 && ((opres[oi >> 5] >> (oi & 31)) & 1u)) {
+                        code = (int)((sc >> SC_KIND_SHIFT) & 7u);
+                        lf = L.hp_cap ? hp[oi] : d.obst_hp[(size_t)e * d.O + oi];
+                    } else {
+                        code = ((dead[c >> 5] >> (c & 31)) & 1u) ? ZS_THING_DEADBODY
+                               : (sc & SC_OBJ_BIT)              ? ZS_THING_OBJECTIVE
+                                                                : ZS_THING_NONE;
+                    }
+                }
+            }
+            obs_store(o, plane, cell, ch, code, lf, weapon);
+            q += step_q;
+            r += step_r;
+            if (q >= ww) {
+                q -= ww;
+                r++;
+            }
+        }
+    }
+}
+
+// st == nullptr: no static tables staged (maps whose obstacles are not in row-major order)
+template <typename T>
+__device__ __forceinline__ void obs_stream(const Dev& d, const ObsLayout& L, const lu32* st, const lu8* img, T* out,
+                                           int e) {
+    if (st && L.hp_cap && L.win && d.O > 0) {
+        if (d.obs_scope != ZS_OBS_WORLD && d.obs_w == 21) obs_stream_fast<T, 21>(d, L, st, img, out, e);
+        else obs_stream_fast<T, 0>(d, L, st, img, out, e);
+    } else {
+        obs_stream_gen<T>(d, L, img, out, e);
+    }
+}
+
+__device__ __forceinline__ void obs_stream_any(const Dev& d, const ObsLayout& L, const lu32* st, const lu8* img,
+                                               void* out, int e) {
+    if (d.obs_dtype == ZS_DTYPE_I64) obs_stream(d, L, st, img, (int64_t*)out, e);
+    else if (d.obs_dtype == ZS_DTYPE_I32) obs_stream(d, L, st, img, (int32_t*)out, e);
+    else obs_stream(d, L, st, img, (int16_t*)out, e);
+}
+
+// k_obs: blockDim/64 envs per workgroup, one env per wave, wave-private LDS images after the
+// workgroup's static tables (stat_words = 4 * DW, or 0).
+template <typename T>
+__global__ void __launch_bounds__(256) k_obs(Dev d, T* out, const uint8_t* mask, ObsLayout L, int stat_words) {
+    extern __shared__ __align__(16) uint8_t smem[];
+    const int wave = threadIdx.x >> 6, wpg = blockDim.x >> 6;
+#if defined(ZS_OBS_EXP) && (ZS_OBS_EXP & 8)  // diagnostic build: the store probe's loop (C3 shape)
+    {
+        const int e8 = xcd_remap(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6), lane8 = threadIdx.x & 63;
+        if (e8 >= d.N) return;
+        for (int a = 0; a < 2; a++) {
+            T* o = out + ((size_t)e8 * 2 + a) * 3 * 441;
+            for (int c = lane8; c < 441; c += 64) {
+                o[c] = c;
+                o[441 + c] = e8;
+                o[2 * 441 + c] = a;
+            }
+        }
+        return;
+    }
+#endif
+    lu32* st = (lu32*)smem;
+#if defined(ZS_OBS_EXP) && (ZS_OBS_EXP & 4)  // diagnostic build: no static tables
+    if (d.N < 0)
+#endif
+    if (stat_words) {
+        obs_stage_static(d, st, threadIdx.x, blockDim.x);
+        __syncthreads();
+    }
+    const int e = xcd_remap(blockIdx.x, gridDim.x) * wpg + wave;
+    if (e >= d.N) return;
+    if (mask && !mask[e]) return;
+    lu8* img = (lu8*)(smem + stat_words * 4 + wave * L.bytes);
+    const int N = d.N;
+#if defined(ZS_OBS_EXP) && (ZS_OBS_EXP & 2)  // diagnostic build: no staging (image left as is)
+    if (N < 0)
+#endif
+    obs_build(d, L, img, e, [&](int s, int& p, int& lf, int& wp, int& pr) {
+        p = d.pos[(size_t)s * N + e];
+        lf = d.life[(size_t)s * N + e];
+        wp = d.weapon[(size_t)s * N + e];
+        pr = d.present[(size_t)s * N + e];
+    });
+    obs_stream(d, L, stat_words ? st : nullptr, img, out, e);
+}

@@ -147,10 +147,11 @@ struct ResetLds {
     lu32* tw;
 };
 
-__host__ __device__ inline int reset_lds_bytes(int E, int DW, int ncand, int lists_cap) {
+// the twist buffer doubles as the observation image of the env just rebuilt (obs_bytes)
+__host__ __device__ inline int reset_lds_bytes(int E, int DW, int ncand, int lists_cap, int obs_bytes = 0) {
     int o = DW * 4 + ncand * 4 + 2 * E * 4 + 4 * E + lists_cap * 4 + (E + 8) * 4;
     o = ((o + 15) / 16) * 16;
-    return o + 2 * ZS_MT_N * 4;
+    return o + (obs_bytes > 2 * ZS_MT_N * 4 ? obs_bytes : 2 * ZS_MT_N * 4);
 }
 
 __device__ __forceinline__ bool rbm_test(const ResetLds& L, int cell) { return (L.bm[cell >> 5] >> (cell & 31)) & 1u; }
@@ -376,42 +377,26 @@ __device__ __forceinline__ void reset_role(const Dev& d, int list_mode, const in
         int e = list_mode ? list[idx] : idx;
         if (!list_mode && mask && !mask[e]) continue;
         reset_env_wave(d, L, e, list_mode, err_out);
-        if (obs_out) {  // fobs: the new world's observations, from the LDS image (twist buffer reused)
-            lu32* sobst = L.tw;
-            lu32* sbox = sobst + d.DW;
-            lu32* sobj = sbox + d.DW;
-            li32* spre = (li32*)(sobj + d.DW);
-            li32* hp = spre + d.DW;
+        if (obs_out) {  // fobs: the new world's observations, the image aliasing the twist buffer
             wave_sync();
-            stage_in(d.obstbits, d.DW, threadIdx.x, 64, sobst, [](int w) { return w; });
-            stage_in(d.boxbits, d.DW, threadIdx.x, 64, sbox, [](int w) { return w; });
-            stage_in(d.objbits, d.DW, threadIdx.x, 64, sobj, [](int w) { return w; });
-            stage_in(d.oprefix, d.DW, threadIdx.x, 64, spre, [](int w) { return w; });
-            stage_in(d.obst_hp + (size_t)e * d.O, d.O, threadIdx.x, 64, hp, [](int w) { return w; });
-            wave_sync();
-            ObsImg v;
-            v.occ = L.bm;
-            v.dead = nullptr;   // a new World has no dead bodies
-            v.opres = nullptr;  // and every map obstacle is spawned (HP carried over)
-            v.hp = hp;
-            v.sobst = sobst;
-            v.sbox = sbox;
-            v.sobj = sobj;
-            v.spre = spre;
-            v.pos = L.lpos;
-            v.life = L.llife;
-            v.weap = L.lweap;
-            v.pres = L.lpres;
-            v.s = 1;
-            obs_write_env(d, v, obs_out, e, threadIdx.x, 64);
+            lu8* img = (lu8*)L.tw;
+            lu32* st = d.obs_stat ? (lu32*)((lu8*)L.tw + d.obsl.bytes) : nullptr;
+            if (st) obs_stage_static(d, st, threadIdx.x, 64);
+            obs_build(d, d.obsl, img, e, [&](int s, int& p, int& lf, int& wp, int& pr) {
+                p = L.lpos[s];
+                lf = L.llife[s];
+                wp = L.lweap[s];
+                pr = L.lpres[s];
+            });
+            obs_stream_any(d, d.obsl, st, img, obs_out, e);
             wave_sync();
         }
     }
 }
 
-__global__ void __launch_bounds__(64) k_reset(Dev d, int list_mode, const int* list, const int* count,
-                                              const uint8_t* mask, int* err_out) {
-    reset_role(d, list_mode, list, count, mask, err_out, blockIdx.x, gridDim.x, nullptr);
+__global__ void __launch_bounds__(64, ZS_STEP_WAVES) k_reset(Dev d, int list_mode, const int* list, const int* count,
+                                              const uint8_t* mask, int* err_out, void* obs_out) {
+    reset_role(d, list_mode, list, count, mask, err_out, blockIdx.x, gridDim.x, obs_out);
 }
 
 // Drop the envs a mask-mode reset just rebuilt from the pending list (src -> dst, dst count

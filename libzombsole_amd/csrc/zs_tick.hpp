@@ -16,37 +16,9 @@
 // The sqrt range tests of the reference are replaced by exact integer d^2 tests.
 #pragma once
 #include "zs_device.hpp"
+#include "zs_obs.hpp"
 
 #define NOTHING ((int)0x80000000)
-
-// Explicit LDS (address space 3) pointer types for every view into the workgroup's image, so the
-// compiler always emits ds_* instructions (a pointer that might be LDS or global degrades to
-// flat accesses and pushes the lane context to scratch).
-#define ZS_LDS __attribute__((address_space(3)))
-typedef ZS_LDS uint32_t lu32;
-typedef ZS_LDS int32_t li32;
-typedef ZS_LDS uint16_t lu16;
-typedef ZS_LDS uint8_t lu8;
-
-// Stage n global words into LDS: lane `lane0` of a team of `step` lanes copies elements
-// lane0, lane0 + step, ...  All loads of a chunk of 8 are issued before any LDS store, so one
-// memory latency is paid per chunk instead of one per element.
-template <typename T, typename LT, typename Idx>
-__device__ __forceinline__ void stage_in(const T* src, int n, int lane0, int step, LT* dst, Idx dst_index) {
-    for (int b = lane0; b < n; b += 8 * step) {
-        T v[8];
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-            int i = b + u * step;
-            v[u] = src[i < n ? i : n - 1];
-        }
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-            int i = b + u * step;
-            if (i < n) dst[dst_index(i)] = v[u];
-        }
-    }
-}
 
 enum { K_NONE = 0, K_MOVE = 1, K_ATTACK = 2, K_HEAL = 3, K_DEFER = 4 };
 
@@ -97,17 +69,18 @@ __device__ unsigned long long g_stamp_wg[ZS_STAMP_WGS * ZS_NPHASE];
 __constant__ int c_adj_dx[4] = {0, 0, 1, -1};
 __constant__ int c_adj_dy[4] = {1, -1, 0, 0};
 
-// LDS footprint of one workgroup (host and device agree on this layout)
+// LDS footprint of one workgroup (host and device agree on this layout).  The entity columns the
+// observations need (pos, life, weapon, present) sit before `region`; everything in `region` is
+// dead once the tick's state is stored, so the observation image of the env being encoded and the
+// MT twist buffer alias it.
 struct TickLayout {
     int ne;                                  // envs per workgroup
     int off_lists;                           // static spawn lists (player then zombie), shared by the WG
     int off_misc;                            // per-env scalars / tracker, [MISC_*][ne] int32
-    int off_lst, off_bm, off_rw, off_cand;   // byte offsets
-    int off_pos, off_life, off_tgt;
-    int off_weap, off_pres, off_order, off_rank, off_kind, off_perm, off_moved;
-    // observation image (fobs): per env dead-body bits [DW], obstacle present bits [OW], obstacle
-    // HP [O]; per workgroup the static obstacle / box / objective bitmaps and obstacle prefix counts
-    int off_dead, off_opres, off_hp, off_sobst, off_sbox, off_sobj, off_spre;
+    int off_lst;
+    int off_pos, off_life, off_weap, off_pres;
+    int off_region;                          // = off_bm
+    int off_bm, off_rw, off_cand, off_tgt, off_order, off_rank, off_kind, off_perm, off_moved;
     int bytes;
 };
 
@@ -115,7 +88,7 @@ struct TickLayout {
 enum { MISC_T = 0, MISC_DEATHS, MISC_ZD, MISC_EPSTEPS, MISC_PREVZD, MISC_SERIAL, MISC_ODIRTY, MISC_NONPOS, MISC_N };
 
 __host__ __device__ inline TickLayout tick_layout(int ne, int E, int DW, int rw_cap, int cand_cap, int lists_cap,
-                                                  int A, int fobs = 0, int O = 0) {
+                                                  int A, int obs_bytes = 0) {
     TickLayout L;
     L.ne = ne;
     int o = 0;
@@ -125,23 +98,24 @@ __host__ __device__ inline TickLayout tick_layout(int ne, int E, int DW, int rw_
     o += (MISC_N + 2 * A) * ne * 4;
     L.off_lst = o;
     o += ne * 4;
-    int region = o;
-    L.off_bm = o;
-    o += DW * ne * 4;
-    L.off_rw = o;
-    o += rw_cap * ne * 4;
     L.off_pos = o;
     o += E * ne * 4;
     L.off_life = o;
     o += E * ne * 4;
-    L.off_tgt = o;
-    o += E * ne * 4;
-    L.off_cand = o;
-    o += ((cand_cap * ne * 2 + 3) / 4) * 4;
     L.off_weap = o;
     o += E * ne;
     L.off_pres = o;
     o += E * ne;
+    o = ((o + 15) / 16) * 16;
+    const int region = o;
+    L.off_region = L.off_bm = o;
+    o += DW * ne * 4;
+    L.off_rw = o;
+    o += rw_cap * ne * 4;
+    L.off_tgt = o;
+    o += E * ne * 4;
+    L.off_cand = o;
+    o += ((cand_cap * ne * 2 + 3) / 4) * 4;
     L.off_order = o;
     o += E * ne;
     L.off_rank = o;
@@ -153,26 +127,9 @@ __host__ __device__ inline TickLayout tick_layout(int ne, int E, int DW, int rw_
     L.off_moved = o;
     o += E * ne;
     o = ((o + 15) / 16) * 16;
-    L.off_dead = L.off_opres = L.off_hp = L.off_sobst = L.off_sbox = L.off_sobj = L.off_spre = o;
-    if (fobs) {
-        int OW = (O + 31) / 32;
-        L.off_dead = o;
-        o += DW * ne * 4;
-        L.off_opres = o;
-        o += OW * ne * 4;
-        L.off_hp = o;
-        o += O * ne * 4;
-        L.off_sobst = o;
-        o += DW * 4;
-        L.off_sbox = o;
-        o += DW * 4;
-        L.off_sobj = o;
-        o += DW * 4;
-        L.off_spre = o;
-        o += DW * 4;
-    }
-    // the MT twist buffer (2 x 624 words) aliases the per-env region after state is stored
+    // the MT twist buffer (2 x 624 words) and one env's observation image alias the region
     if (o - region < 2 * ZS_MT_N * 4) o = region + 2 * ZS_MT_N * 4;
+    if (o - region < obs_bytes) o = region + obs_bytes;
     L.bytes = o;
     return L;
 }
@@ -195,9 +152,6 @@ struct Grp {
     lu8* lkind;
     lu8* lperm;
     lu8* lmoved;
-    lu32* ldead;   // fobs: LDS mirrors the leader keeps in step with its global writes
-    lu32* lopres;
-    li32* lhp;
     // leader registers
     uint32_t st0;  // ring state at the start of the LDS window
     int wpos, wlen;
@@ -297,7 +251,7 @@ __device__ __forceinline__ int target_maxlife(const Dev& d, int tgt) {
 }
 __device__ __forceinline__ int target_life(const Dev& d, const Grp& c, int tgt) {
     if (tgt >= 0) return LL(c, tgt);
-    return d.fobs ? (int)c.lhp[IX(c, -tgt - 1)] : d.obst_hp[(size_t)c.e * d.O + (-tgt - 1)];
+    return d.obst_hp[(size_t)c.e * d.O + (-tgt - 1)];
 }
 __device__ __forceinline__ void set_target_life(const Dev& d, Grp& c, int tgt, int v) {
     if (tgt >= 0) {
@@ -306,7 +260,6 @@ __device__ __forceinline__ void set_target_life(const Dev& d, Grp& c, int tgt, i
     }
     int oi = -tgt - 1;
     d.obst_hp[(size_t)c.e * d.O + oi] = v;
-    if (d.fobs) c.lhp[IX(c, oi)] = v;
     uint32_t* w = &d.obst_nonpos[(size_t)c.e * d.OW + (oi >> 5)];
     uint32_t bit = 1u << (oi & 31);
     *w = v <= 0 ? (*w | bit) : (*w & ~bit);
@@ -774,7 +727,6 @@ __device__ __forceinline__ void env_step_leader(const Dev& d, Grp& c, const int3
             uint32_t dead = *pw & d.obst_nonpos[(size_t)c.e * d.OW + w];
             if (dead) {
                 *pw &= ~dead;
-                if (d.fobs) c.lopres[IX(c, w)] &= ~dead;
                 c.deaths += __popc(dead);
                 while (dead) {
                     int oi = 32 * w + __ffs(dead) - 1;
@@ -794,7 +746,6 @@ __device__ __forceinline__ void env_step_leader(const Dev& d, Grp& c, const int3
             if (LL(c, s) <= 0) {
                 int p = LP(c, s), cell = unpack_y(p) * d.W + unpack_x(p);
                 deadbits[cell >> 5] |= 1u << (cell & 31);  // DeadBody decoration
-                if (d.fobs) c.ldead[IX(c, cell >> 5)] |= 1u << (cell & 31);
                 bm_clr(c, cell);
                 LPR(c, s) = 0;
                 c.deaths++;
@@ -870,105 +821,6 @@ __device__ __forceinline__ void env_step_leader(const Dev& d, Grp& c, const int3
 }
 
 // ---------------------------------------------------------------------------
-// Observations from an LDS image of one env (gym/observation.py:36-173): the thing at a cell
-// first, then the decoration; out of bounds = Wall(200).  The step launch (fobs) writes the
-// observations of the envs it ticks or resets with this; k_obs (engine.hip) covers zs_reset,
-// zs_observe and maps whose image does not fit.  Obstacle index = rank of its cell among the
-// map's obstacle cells (obstacles are in row-major file order), so no cell->obstacle table.
-// ---------------------------------------------------------------------------
-struct ObsImg {
-    const lu32* occ;    // occupancy bitmap word w at occ[w * s]
-    const lu32* dead;   // dead-body bitmap (nullptr: none)
-    const lu32* opres;  // obstacle present bits (nullptr: all present)
-    const li32* hp;     // obstacle HP, obstacle i at hp[i * s]
-    const lu32* sobst;  // static, per workgroup
-    const lu32* sbox;
-    const lu32* sobj;
-    const li32* spre;
-    const li32* pos;    // entity slot k at [k * s]
-    const li32* life;
-    const lu8* weap;
-    const lu8* pres;
-    int s;
-};
-
-__device__ __forceinline__ void obs_cell(const Dev& d, const ObsImg& v, int x, int y, int& code, int& life,
-                                         int& weapon) {
-    weapon = 0;
-    if (x < 0 || y < 0 || x >= d.W || y >= d.H) {
-        code = ZS_THING_WALL;
-        life = 200;
-        return;
-    }
-    const int cell = y * d.W + x, w = cell >> 5;
-    const uint32_t bit = 1u << (cell & 31);
-    life = 0;
-    if (v.occ[w * v.s] & bit) {
-        const uint32_t ob = v.sobst[w];
-        if (ob & bit) {
-            const int oi = v.spre[w] + __popc(ob & (bit - 1u));
-            if (!v.opres || ((v.opres[(oi >> 5) * v.s] >> (oi & 31)) & 1u)) {
-                code = (v.sbox[w] & bit) ? ZS_THING_BOX : ZS_THING_WALL;
-                life = v.hp[oi * v.s];
-                return;
-            }
-        }
-        const int32_t pk = pack_xy(x, y);
-        for (int k = 0; k < d.E; k++) {
-            if (v.pres[k * v.s] && v.pos[k * v.s] == pk) {
-                life = v.life[k * v.s];
-                weapon = v.weap[k * v.s];
-                code = k < d.A ? (d.obs_enc == ZS_ENC_CHANNELS ? d.agent_codes[k] : ZS_THING_AGENT)
-                               : (k < d.A + d.P ? ZS_THING_PLAYER : ZS_THING_ZOMBIE);
-                return;
-            }
-        }
-    }
-    code = (v.dead && (v.dead[w * v.s] & bit)) ? ZS_THING_DEADBODY
-           : (v.sobj[w] & bit)                  ? ZS_THING_OBJECTIVE
-                                                : ZS_THING_NONE;
-}
-
-// all observations of env e ([nobs][C][h][w] at out + e * per-env size) by lanes l0, l0+nl, ...
-template <typename T>
-__device__ __forceinline__ void obs_write_env_t(const Dev& d, const ObsImg& v, T* out, int e, int l0, int nl) {
-    const bool world = d.obs_scope == ZS_OBS_WORLD;
-    const int nobs = world ? 1 : (d.reward_mode == ZS_REWARD_MULTI ? d.A : 1);
-    const int hh = world ? d.H : d.obs_w, ww = world ? d.W : d.obs_w, half = d.obs_w / 2;
-    const bool ch = d.obs_enc == ZS_ENC_CHANNELS;
-    const int plane = hh * ww, C = ch ? 3 : 1;
-    T* oe = out + (size_t)e * nobs * C * plane;
-    for (int a = 0; a < nobs; a++) {
-        int ox = 0, oy = 0;
-        if (!world) {
-            const int32_t ap = v.pos[a * v.s];
-            ox = unpack_x(ap) - half;
-            oy = unpack_y(ap) - half;
-        }
-        T* o = oe + (size_t)a * C * plane;
-        for (int cell = l0; cell < plane; cell += nl) {
-            const int r = cell / ww, q = cell - r * ww;
-            int code, life, weapon;
-            obs_cell(d, v, ox + q, oy + r, code, life, weapon);
-            if (!ch) {
-                int64_t adj = life < 100 ? life : 100;
-                o[cell] = (T)(256 * (int64_t)code + 16 * (int64_t)weapon + floordiv100(15 * adj));
-            } else {
-                o[cell] = (T)code;
-                o[plane + cell] = (T)life;
-                o[2 * plane + cell] = (T)weapon;
-            }
-        }
-    }
-}
-
-__device__ __forceinline__ void obs_write_env(const Dev& d, const ObsImg& v, void* out, int e, int l0, int nl) {
-    if (d.obs_dtype == ZS_DTYPE_I64) obs_write_env_t(d, v, (int64_t*)out, e, l0, nl);
-    else if (d.obs_dtype == ZS_DTYPE_I32) obs_write_env_t(d, v, (int32_t*)out, e, l0, nl);
-    else obs_write_env_t(d, v, (int16_t*)out, e, l0, nl);
-}
-
-// ---------------------------------------------------------------------------
 // wave-cooperative MT19937 refill: every env of the workgroup whose next block is not ready
 // gets it twisted by all 64 lanes (3 dependency phases over the 624-word block).
 // ---------------------------------------------------------------------------
@@ -1012,7 +864,7 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
     const int base = wg * NE, e = base + g, N = d.N, E = d.E, A = d.A;
     const bool active = e < N;
     const bool leader = j == 0;
-    const TickLayout L = tick_layout(NE, E, d.DW, d.rw_cap, d.cand_cap, d.lists_cap, A, d.fobs, d.O);
+    const TickLayout L = tick_layout(NE, E, d.DW, d.rw_cap, d.cand_cap, d.lists_cap, A, d.fobs ? d.obsl.bytes + 4 * d.obs_stat : 0);
     lu32* lst = (lu32*)(smem + L.off_lst);
     Grp c;
     c.e = e;
@@ -1033,15 +885,6 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
     c.lkind = (lu8*)(smem + L.off_kind);
     c.lperm = (lu8*)(smem + L.off_perm);
     c.lmoved = (lu8*)(smem + L.off_moved);
-    c.ldead = (lu32*)(smem + L.off_dead);
-    c.lopres = (lu32*)(smem + L.off_opres);
-    c.lhp = (li32*)(smem + L.off_hp);
-    if (d.fobs) {  // static observation tables, once per workgroup
-        stage_in(d.obstbits, d.DW, lane, 64, (lu32*)(smem + L.off_sobst), [](int w) { return w; });
-        stage_in(d.boxbits, d.DW, lane, 64, (lu32*)(smem + L.off_sbox), [](int w) { return w; });
-        stage_in(d.objbits, d.DW, lane, 64, (lu32*)(smem + L.off_sobj), [](int w) { return w; });
-        stage_in(d.oprefix, d.DW, lane, 64, (li32*)(smem + L.off_spre), [](int w) { return w; });
-    }
     c.lists = (li32*)(smem + L.off_lists);
     if (d.lists_cap)  // the static spawn lists, staged once per workgroup
         for (int i = lane; i < d.nps + d.nzs; i += 64) c.lists[i] = i < d.nps ? d.pspawn[i] : d.zspawn[i - d.nps];
@@ -1105,11 +948,6 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
         }
         // occupancy bitmap
         stage_in(d.occ_bits + (size_t)e * d.DW, d.DW, j, G, c.bm, [&](int w) { return IX(c, w); });
-        if (d.fobs) {  // the env's dead bodies, obstacle presence and HP for its observations
-            stage_in(d.dead + (size_t)e * d.DW, d.DW, j, G, c.ldead, [&](int w) { return IX(c, w); });
-            stage_in(d.obst_present + (size_t)e * d.OW, d.OW, j, G, c.lopres, [&](int w) { return IX(c, w); });
-            stage_in(d.obst_hp + (size_t)e * d.O, d.O, j, G, c.lhp, [&](int w) { return IX(c, w); });
-        }
         // RNG window: the next words of this env's stream, tempered
         uint32_t st = d.rngst[e];
         uint32_t off = st & 1023u, slot = (st >> 10) & 1u, ready = (st >> 11) & 1u;
@@ -1221,32 +1059,35 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
     }
     wave_sync();
     STAMP(4);
-    if (d.fobs && stepping && obs_out) {  // this env's observations; envs reset this call get theirs from the reset work
-        ObsImg v;
-        v.occ = c.bm + g;
-        v.dead = c.ldead + g;
-        v.opres = c.lopres + g;
-        v.hp = c.lhp + g;
-        v.sobst = (const lu32*)(smem + L.off_sobst);
-        v.sbox = (const lu32*)(smem + L.off_sbox);
-        v.sobj = (const lu32*)(smem + L.off_sobj);
-        v.spre = (const li32*)(smem + L.off_spre);
-        v.pos = c.lpos + g;
-        v.life = c.llife + g;
-        v.weap = c.lweap + g;
-        v.pres = c.lpres + g;
-        v.s = NE;
-        obs_write_env(d, v, obs_out, e, j, G);
+    // observations of the envs ticked here (envs reset by this call get theirs from the reset work):
+    // the whole wave encodes one env at a time, its image aliasing the dead tick region
+    if (d.fobs && obs_out) {
+        const unsigned long long stepmask = __ballot(stepping && leader);  // bit g * G per stepping env
+        lu8* img = (lu8*)(smem + L.off_region);
+        lu32* st = d.obs_stat ? (lu32*)(smem + L.off_region + d.obsl.bytes) : nullptr;
+        if (st && stepmask) obs_stage_static(d, st, lane, 64);
+        for (int g2 = 0; g2 < NE; g2++) {
+            if (!((stepmask >> (g2 * G)) & 1ull)) continue;
+            obs_build(d, d.obsl, img, base + g2, [&](int s, int& p, int& lf, int& wp, int& pr) {
+                p = c.lpos[s * NE + g2];
+                lf = c.llife[s * NE + g2];
+                wp = c.lweap[s * NE + g2];
+                pr = c.lpres[s * NE + g2];
+            });
+            obs_stream_any(d, d.obsl, st, img, obs_out, base + g2);
+            wave_sync();
+        }
     }
     wave_sync();
-    coop_refill(d, base, min(NE, N - base), lst, (lu32*)(smem + L.off_bm));
     STAMP(5);
+    coop_refill(d, base, min(NE, N - base), lst, (lu32*)(smem + L.off_bm));
+    STAMP(6);
 }
 
 template <int G>
-__global__ void __launch_bounds__(64) k_tick(Dev d, const int32_t* actions, double* rew, uint8_t* done_out,
+__global__ void __launch_bounds__(64, ZS_STEP_WAVES) k_tick(Dev d, const int32_t* actions, double* rew, uint8_t* done_out,
                                              uint8_t* trunc_out, uint8_t* listed_out, uint8_t* reset_out,
-                                             int* reset_list, int* reset_count) {
-    tick_wg<G>(d, blockIdx.x, actions, rew, done_out, trunc_out, listed_out, reset_out, reset_list, reset_count,
-               nullptr);
+                                             int* reset_list, int* reset_count, void* obs_out) {
+    tick_wg<G>(d, xcd_remap(blockIdx.x, gridDim.x), actions, rew, done_out, trunc_out, listed_out, reset_out, reset_list,
+               reset_count, obs_out);
 }

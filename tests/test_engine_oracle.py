@@ -113,3 +113,28 @@ def test_multi_bots_survival_rich_int16():
                                                agent_weapons=["random", "gun"], observation_surroundings_width=11,
                                                obs_dtype=_abi.DTYPE_I16, max_episode_steps=70),
                64, 140, stream="rich")
+
+
+# Alternative kernel paths the engine picks by map / size (or that diagnostics force): each must be
+# bit-exact too.  The variables are read once, when the handle is created.
+PATHS = {
+    "unfused": {"ZS_FUSED": "0"},                  # separate k_reset launch, observations by k_obs
+    "obs_separate": {"ZS_FOBS": "0"},               # fused step launch, observations by k_obs
+    "obs_scan": {"ZS_OBS_WIN": "0"},                # per-cell entity scan instead of the window map
+    "obs_scan_separate": {"ZS_OBS_WIN": "0", "ZS_FOBS": "0"},
+    "obs_scell": {"ZS_OBS_STAT": "0"},              # per-cell static words instead of LDS bitmaps
+    "obs_scell_separate": {"ZS_OBS_STAT": "0", "ZS_FOBS": "0"},
+    "no_lds_budget": {"ZS_LDS_BUDGET": "0"},        # largest LDS copies instead of occupancy-first
+}
+
+
+@pytest.mark.parametrize("path", sorted(PATHS))
+def test_kernel_paths(path, monkeypatch):
+    for k, v in PATHS[path].items():
+        monkeypatch.setenv(k, v)
+    run_parity(c2, 96, 60, check_state_every=30)
+    run_parity(lambda n: _abi.single_env_config(n, "safehouse", ["terminator"], "city_for_safehouse", "0",
+                                                initial_zombies=20, minimum_zombies=20,
+                                                observation_scope="world", observation_position_encoding="channels",
+                                                max_episode_steps=50),
+               16, 60, check_state_every=30)

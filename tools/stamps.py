@@ -9,7 +9,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 SO = os.path.join(ROOT, "libzombsole_amd", "_build", "libzombsole_mi355x_stamps.so")
-PHASES = ["stage-in", "decide", "leader", "stage-out", "mt-refill", "-",
+PHASES = ["stage-in", "decide", "leader", "stage-out", "obs-write", "mt-refill",
           "  L:defer+shuffle", "  L:execute", "  L:order+cleanup", "  L:reward+rules", "-", "-",
           "R:setup+rng", "R:weapons", "R:spawn p+a", "R:zombie lives", "R:spawn z", "R:twist+out"]
 
@@ -49,7 +49,7 @@ def main():
         ssum, smax = eng.debug_stamps(len(PHASES))
         wgs = (n_envs + 64 // G - 1) // (64 // G)
         print("G=%2d  k_tick %.1f us  k_obs %.1f us  k_reset %.1f us" % (
-            G, 1e3 * prof["tick_ms"] / prof["tick_n"], 1e3 * prof["obs_ms"] / prof["obs_n"],
+            G, 1e3 * prof["tick_ms"] / max(prof["tick_n"], 1), 1e3 * prof["obs_ms"] / max(prof["obs_n"], 1),
             1e3 * prof["reset_ms"] / max(prof["reset_n"], 1)))
         for k, name in enumerate(PHASES):
             if name == "-":
