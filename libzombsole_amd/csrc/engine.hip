@@ -31,8 +31,8 @@ __global__ void __launch_bounds__(64, ZS_STEP_WAVES) k_step(Dev d, int n_reset, 
     if ((int)blockIdx.x < n_reset)
         reset_role(d, 1, cur_list, cur_count, nullptr, err_out, blockIdx.x, n_reset, d.fobs ? obs_out : nullptr);
     else
-        tick_wg<G>(d, xcd_remap(blockIdx.x - n_reset, gridDim.x - n_reset), actions, rew, done_out, trunc_out, listed_out, reset_out, reset_list,
-                   reset_count, obs_out);
+        tick_wg<G>(d, xcd_remap(blockIdx.x - n_reset, gridDim.x - n_reset), actions, rew, done_out, trunc_out,
+                   listed_out, reset_out, reset_list, reset_count, obs_out, 0, d.N);
 }
 
 // ---------------------------------------------------------------------------
@@ -241,6 +241,14 @@ struct zs_handle {
     size_t lds;     // k_tick dynamic LDS bytes
     ObsLayout obs_l;  // k_obs per-wave LDS image
     int obs_wpg;      // k_obs waves (envs) per workgroup
+    int obs_pipe = 0;      // k_obs_pipe<NOBS> usable (NOBS = 1, 2, 4), else 0
+    // step pipeline: the tick in `chunks` env ranges on the caller's stream, each range's observations
+    // on s_obs as soon as its tick is done
+    int chunks = 1;
+    hipStream_t s_obs = nullptr;
+    hipEvent_t ev_chunk[8] = {};
+    hipEvent_t ev_join = nullptr;
+    int obs_pipe_wgs = 8;  // its workgroups per CU
     int state_words;
     std::vector<void*> allocs;
     int32_t* d_state;
@@ -295,6 +303,15 @@ static int dupload(zs_handle* h, T** p, const std::vector<T>& v) {
 static void free_all(zs_handle* h) {
     for (void* p : h->allocs) (void)hipFree(p);
     h->allocs.clear();
+    for (hipEvent_t& ev : h->ev_chunk)
+        if (ev) {
+            (void)hipEventDestroy(ev);
+            ev = nullptr;
+        }
+    if (h->ev_join) (void)hipEventDestroy(h->ev_join);
+    h->ev_join = nullptr;
+    if (h->s_obs) (void)hipStreamDestroy(h->s_obs);
+    h->s_obs = nullptr;
     for (hipEvent_t ev : h->ev_pool) (void)hipEventDestroy(ev);
     h->ev_pool.clear();
 }
@@ -576,8 +593,20 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
         d.obs_stat = (rank_order && d.DW <= 1024 && !getenv_off("ZS_OBS_STAT")) ? 4 * d.DW : 0;
         h->obs_l = L;
         h->obs_wpg = d.obs_stat * 4 + 4 * L.bytes <= 64 * 1024 ? 4 : 1;
+        // k_obs_pipe: surroundings of width 21, 1/2/4 observations, static tables, staged HP, window
+        // map, every entity on its own lane, prefetch arrays large enough (ZS_OBS_PIPE=0 disables)
+        if (!world && d.obs_w == 21 && (nobs == 1 || nobs == 2 || nobs == 4) && d.obs_stat && L.hp_cap && L.win &&
+            d.O > 0 && d.E <= 64 && d.DW <= 64 * OBS_PF_D && d.O <= 64 * OBS_PF_H && d.OW <= 64 &&
+            d.obs_stat * 4 + 4 * L.bytes <= 64 * 1024 && !getenv_off("ZS_OBS_PIPE")) {
+            h->obs_pipe = nobs;
+            h->obs_pipe_wgs = std::max(1, std::min(8, 160 * 1024 / (d.obs_stat * 4 + 4 * L.bytes)));
+        }
+        // with the store-stream kernel available the observations are its job (measured faster than
+        // writing them from the tick workgroups at both 8192 and 65536 envs); ZS_FOBS=1 forces them
+        // into the step launch
         d.obsl = L;
         d.fobs = L.bytes + 4 * d.obs_stat <= 16 * 1024 && !getenv_off("ZS_FOBS");
+        if (h->obs_pipe && !(getenv("ZS_FOBS") && atoi(getenv("ZS_FOBS")) != 0)) d.fobs = 0;
     }
     // Fused step launch (reset work + tick in one) when the whole launch is resident at once: then
     // the step is one latency-bound round and the reset work hides under the ticks (measured: 8192
@@ -597,6 +626,22 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
         delete h;
         return fail(ZS_EINVAL, "map too large for the reset kernel's LDS image");
     }
+    // step pipeline over env chunks (zs_step): ZS_CHUNKS=K (2..8) runs the tick in K env ranges and
+    // streams each range's observations on a second stream.  Off by default: measured at 65536 envs,
+    // the persistent observation kernel holds every CU slot, so the overlapping ticks only contend
+    // (K=1 0.586 ms, K=2 0.628, K=4 0.637, K=8 0.697 per step).
+    {
+        const char* ck = getenv("ZS_CHUNKS");
+        h->chunks = 1;
+        if (ck && !h->fused && !d.fobs && h->obs_pipe) h->chunks = std::max(1, std::min(8, atoi(ck)));
+        if (d.N < 64 * h->chunks) h->chunks = 1;
+        if (h->chunks > 1) {
+            if (hipStreamCreateWithFlags(&h->s_obs, hipStreamNonBlocking) != hipSuccess) h->chunks = 1;
+            for (int c = 0; c < h->chunks && h->chunks > 1; c++)
+                if (hipEventCreateWithFlags(&h->ev_chunk[c], hipEventDisableTiming) != hipSuccess) h->chunks = 1;
+            if (h->chunks > 1 && hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) != hipSuccess) h->chunks = 1;
+        }
+    }
     if (h->reset_lds > 64 * 1024 &&
         hipFuncSetAttribute((const void*)k_reset, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->reset_lds) !=
             hipSuccess) {
@@ -606,9 +651,9 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
     }
     if (getenv("ZS_VERBOSE"))
         fprintf(stderr, "zs_create: N=%d E=%d G=%d step_lds=%zu resident=%d reset_lds=%zu rw_cap=%d cand_cap=%d "
-                        "lists_cap=%d fused=%d fobs=%d obs_img=%d k_obs_img=%d x%d\n", d.N, d.E, h->G, h->lds,
-                h->resident, h->reset_lds, d.rw_cap, d.cand_cap, d.lists_cap, h->fused, d.fobs, d.obsl.bytes,
-                h->obs_l.bytes, h->obs_wpg);
+                        "lists_cap=%d fused=%d fobs=%d obs_img=%d k_obs_img=%d x%d pipe=%d chunks=%d\n", d.N, d.E,
+                h->G, h->lds, h->resident, h->reset_lds, d.rw_cap, d.cand_cap, d.lists_cap, h->fused, d.fobs,
+                d.obsl.bytes, h->obs_l.bytes, h->obs_wpg, h->obs_pipe, h->chunks);
     if (d.O > 0) {
         size_t n = N * d.O;
         hipLaunchKernelGGL(k_init_obstacles, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, d);
@@ -666,11 +711,37 @@ extern "C" int zs_seed(zs_handle* h, int32_t env0, int32_t n, const uint64_t* se
     return ZS_OK;
 }
 
-static int launch_obs(zs_handle* h, void* obs, const uint8_t* mask, hipStream_t s) {
+static int launch_obs(zs_handle* h, void* obs, const uint8_t* mask, hipStream_t s, int env0 = 0, int env1 = -1) {
     const Dev& d = h->d;
     if (!obs) return ZS_OK;
     int i0 = -1, i1 = -1;
     if (h->prof) HIPCHK(hipEventRecord(prof_event(h, &i0), s));
+    if (env1 < 0) env1 = d.N;
+    if (!mask && h->obs_pipe) {  // every env of [env0, env1), registered shape: the prefetching store stream
+        const unsigned g = (unsigned)std::min((env1 - env0 + 3) / 4, 256 * h->obs_pipe_wgs);
+        const size_t lds = (size_t)d.obs_stat * 4 + 4 * (size_t)h->obs_l.bytes;
+#define ZS_PIPE(TT, NB) \
+    hipLaunchKernelGGL((k_obs_pipe<TT, NB>), dim3(g), dim3(256), lds, s, d, (TT*)obs, h->obs_l, env0, env1)
+#define ZS_PIPE_T(TT)                   \
+    if (h->obs_pipe == 1) ZS_PIPE(TT, 1); \
+    else if (h->obs_pipe == 2) ZS_PIPE(TT, 2); \
+    else ZS_PIPE(TT, 4)
+        if (d.obs_dtype == ZS_DTYPE_I64) {
+            ZS_PIPE_T(int64_t);
+        } else if (d.obs_dtype == ZS_DTYPE_I32) {
+            ZS_PIPE_T(int32_t);
+        } else {
+            ZS_PIPE_T(int16_t);
+        }
+#undef ZS_PIPE_T
+#undef ZS_PIPE
+        HIPCHK(hipGetLastError());
+        if (h->prof) {
+            HIPCHK(hipEventRecord(prof_event(h, &i1), s));
+            h->ev_obs.push_back({i0, i1});
+        }
+        return ZS_OK;
+    }
     const unsigned grid = (unsigned)((d.N + h->obs_wpg - 1) / h->obs_wpg);
     const dim3 blk(64 * h->obs_wpg);
     const size_t lds = (size_t)d.obs_stat * 4 + (size_t)h->obs_wpg * h->obs_l.bytes;
@@ -689,10 +760,12 @@ static int launch_obs(zs_handle* h, void* obs, const uint8_t* mask, hipStream_t 
 }
 
 static int launch_tick(zs_handle* h, const int32_t* actions, double* rew, uint8_t* done, uint8_t* trunc,
-                       uint8_t* listed, uint8_t* reset_out, int* rlist, int* rcount, void* obs, hipStream_t s) {
+                       uint8_t* listed, uint8_t* reset_out, int* rlist, int* rcount, void* obs, hipStream_t s,
+                       int env0 = 0, int env1 = -1) {
     const Dev& d = h->d;
     const int ne = 64 / h->G;
-    unsigned grid = (unsigned)((d.N + ne - 1) / ne);
+    if (env1 < 0) env1 = d.N;
+    unsigned grid = (unsigned)((env1 - env0 + ne - 1) / ne);
     int i0 = -1, i1 = -1;
     const int p = h->rpar;
     // fused: the first n_reset workgroups rebuild the envs of the pending list (ended at the previous
@@ -706,7 +779,7 @@ static int launch_tick(zs_handle* h, const int32_t* actions, double* rew, uint8_
                            (const int*)(h->d_rcount + p), h->d_err, obs);                                             \
     else                                                                                                              \
         hipLaunchKernelGGL(k_tick<GG>, dim3(grid), dim3(64), h->lds, s, d, actions, rew, done, trunc, listed,        \
-                           reset_out, rlist, rcount, obs)
+                           reset_out, rlist, rcount, obs, env0, env1)
     switch (h->G) {
     case 1: ZS_TICK(1); break;
     case 2: ZS_TICK(2); break;
@@ -795,6 +868,26 @@ extern "C" int zs_step(zs_handle* h, const int32_t* actions_dev, void* obs_dev, 
     }
     // 2) tick every other env; envs that end now are queued on list[q] for the next call
     HIPCHK(hipMemsetAsync(h->d_rcount + q, 0, sizeof(int), s));
+    const int K = (!h->fused && !h->d.fobs && obs_dev) ? h->chunks : 1;
+    if (K > 1) {
+        // 3) pipelined: the tick of chunk c + 1 (caller's stream) runs while the observations of chunk
+        //    c stream out on the engine's second stream; the caller's stream joins at the end
+        const int N = h->d.N;
+        for (int c = 0; c < K; c++) {
+            const int c0 = (int)((long)N * c / K) & ~63, c1 = c + 1 == K ? N : (int)((long)N * (c + 1) / K) & ~63;
+            rc = launch_tick(h, actions_dev, rewards_dev, done_dev, trunc_dev, listed_dev, reset_dev, h->d_rlist[q],
+                             h->d_rcount + q, nullptr, s, c0, c1);
+            if (rc) return rc;
+            HIPCHK(hipEventRecord(h->ev_chunk[c], s));
+            HIPCHK(hipStreamWaitEvent(h->s_obs, h->ev_chunk[c], 0));
+            rc = launch_obs(h, obs_dev, nullptr, h->s_obs, c0, c1);
+            if (rc) return rc;
+        }
+        HIPCHK(hipEventRecord(h->ev_join, h->s_obs));
+        HIPCHK(hipStreamWaitEvent(s, h->ev_join, 0));
+        h->rpar = q;
+        return ZS_OK;
+    }
     rc = launch_tick(h, actions_dev, rewards_dev, done_dev, trunc_dev, listed_dev, reset_dev, h->d_rlist[q],
                      h->d_rcount + q, obs_dev, s);
     if (rc) return rc;

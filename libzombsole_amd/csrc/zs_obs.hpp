@@ -305,25 +305,7 @@ template <typename T>
 __global__ void __launch_bounds__(256) k_obs(Dev d, T* out, const uint8_t* mask, ObsLayout L, int stat_words) {
     extern __shared__ __align__(16) uint8_t smem[];
     const int wave = threadIdx.x >> 6, wpg = blockDim.x >> 6;
-#if defined(ZS_OBS_EXP) && (ZS_OBS_EXP & 8)  // diagnostic build: the store probe's loop (C3 shape)
-    {
-        const int e8 = xcd_remap(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6), lane8 = threadIdx.x & 63;
-        if (e8 >= d.N) return;
-        for (int a = 0; a < 2; a++) {
-            T* o = out + ((size_t)e8 * 2 + a) * 3 * 441;
-            for (int c = lane8; c < 441; c += 64) {
-                o[c] = c;
-                o[441 + c] = e8;
-                o[2 * 441 + c] = a;
-            }
-        }
-        return;
-    }
-#endif
     lu32* st = (lu32*)smem;
-#if defined(ZS_OBS_EXP) && (ZS_OBS_EXP & 4)  // diagnostic build: no static tables
-    if (d.N < 0)
-#endif
     if (stat_words) {
         obs_stage_static(d, st, threadIdx.x, blockDim.x);
         __syncthreads();
@@ -333,9 +315,6 @@ __global__ void __launch_bounds__(256) k_obs(Dev d, T* out, const uint8_t* mask,
     if (mask && !mask[e]) return;
     lu8* img = (lu8*)(smem + stat_words * 4 + wave * L.bytes);
     const int N = d.N;
-#if defined(ZS_OBS_EXP) && (ZS_OBS_EXP & 2)  // diagnostic build: no staging (image left as is)
-    if (N < 0)
-#endif
     obs_build(d, L, img, e, [&](int s, int& p, int& lf, int& wp, int& pr) {
         p = d.pos[(size_t)s * N + e];
         lf = d.life[(size_t)s * N + e];
@@ -343,4 +322,120 @@ __global__ void __launch_bounds__(256) k_obs(Dev d, T* out, const uint8_t* mask,
         pr = d.present[(size_t)s * N + e];
     });
     obs_stream(d, L, stat_words ? st : nullptr, img, out, e);
+}
+
+// ---------------------------------------------------------------------------
+// k_obs_pipe: the store-stream form of k_obs for the registered shape (surroundings, width 21,
+// NOBS observations per env, static tables, staged HP).  A wave stays resident and walks envs
+// e0, e0 + waves, ...; the state of its next env is loaded into registers (prefetch) before the
+// current env's stores are issued, so the load latency hides under the store stream instead of
+// idling the wave slot (a wave that stages and then stores spends ~40 % of its life waiting on the
+// staging loads while holding its slot).  The store stream is fully unrolled (NOBS x 7 x C store
+// instructions), so the next iteration's wait for the prefetch is an exact vmcnt(#stores) that
+// lets the stores stay in flight.
+// ---------------------------------------------------------------------------
+#ifndef ZS_OBS_PIPE_WAVES
+#define ZS_OBS_PIPE_WAVES 4  // register budget: waves per SIMD the compiler must allow
+#endif
+#define OBS_PF_D 2   // prefetched dead-body words per lane   (DW <= 128: maps up to 4096 cells)
+#define OBS_PF_H 8   // prefetched obstacle HP words per lane (O <= 512)
+
+struct ObsPrefetch {
+    int32_t pos, life, wp, pr;        // lane s < E: entity slot s
+    uint32_t dead[OBS_PF_D];
+    uint32_t opres;                   // lane w < OW
+    int32_t hp[OBS_PF_H];
+};
+
+// Every load is unconditional (addresses clamped into the row): a load under a lane predicate
+// becomes a branch whose join needs the loaded value, i.e. a wait right after the prefetch.
+__device__ __forceinline__ void obs_prefetch(const Dev& d, int e, ObsPrefetch& f) {
+    const int lane = threadIdx.x & 63, N = d.N;
+    const int s = lane < d.E ? lane : d.E - 1;
+    f.pos = d.pos[(size_t)s * N + e];
+    f.life = d.life[(size_t)s * N + e];
+    f.wp = d.weapon[(size_t)s * N + e];
+    f.pr = d.present[(size_t)s * N + e];
+    const uint32_t* dr = d.dead + (size_t)e * d.DW;
+#pragma unroll
+    for (int i = 0; i < OBS_PF_D; i++) f.dead[i] = dr[min(lane + 64 * i, d.DW - 1)];
+    f.opres = d.obst_present[(size_t)e * d.OW + min(lane, d.OW - 1)];
+    const int32_t* hr = d.obst_hp + (size_t)e * d.O;
+#pragma unroll
+    for (int i = 0; i < OBS_PF_H; i++) f.hp[i] = hr[min(lane + 64 * i, d.O - 1)];
+}
+
+template <typename T, int NOBS>
+__global__ void __launch_bounds__(256, ZS_OBS_PIPE_WAVES) k_obs_pipe(Dev d, T* out, ObsLayout L, int env0, int env1) {
+    extern __shared__ __align__(16) uint8_t smem[];
+    constexpr int WW = 21, PLANE = WW * WW, PER = (PLANE + 63) / 64;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int stat_words = 4 * d.DW;
+    lu32* st = (lu32*)smem;
+    obs_stage_static(d, st, threadIdx.x, blockDim.x);
+    __syncthreads();
+    const int waves = gridDim.x * 4;
+    int e = env0 + xcd_remap(blockIdx.x, gridDim.x) * 4 + wave;
+    if (e >= env1) return;
+    lu8* img = (lu8*)(smem + stat_words * 4 + wave * L.bytes);
+    li32* pos = (li32*)(img + L.off_pos);
+    li32* life = (li32*)(img + L.off_life);
+    li32* cw = (li32*)(img + L.off_cw);
+    lu32* dead = (lu32*)(img + L.off_dead);
+    lu32* opres = (lu32*)(img + L.off_opres);
+    li32* hp = (li32*)(img + L.off_hp);
+    const bool ch = d.obs_enc == ZS_ENC_CHANNELS;
+    const int C = ch ? 3 : 1;
+    const int code_s = lane < d.A ? (ch ? d.agent_codes[lane < d.A ? lane : 0] : ZS_THING_AGENT)
+                                  : (lane < d.A + d.P ? ZS_THING_PLAYER : ZS_THING_ZOMBIE);
+    ObsPrefetch f;
+    obs_prefetch(d, e, f);
+    for (; e < env1; e += waves) {
+        // the image of env e from the registers
+        for (int w = lane; w < L.win / 4; w += 64) ((lu32*)img)[w] = 0u;
+        if (lane < d.E) {
+            pos[lane] = f.pos;
+            life[lane] = f.life;
+            cw[lane] = code_s | (f.wp << 8) | (f.pr << 16);
+        }
+#pragma unroll
+        for (int i = 0; i < OBS_PF_D; i++)
+            if (lane + 64 * i < d.DW) dead[lane + 64 * i] = f.dead[i];
+        if (lane < d.OW) opres[lane] = f.opres;
+#pragma unroll
+        for (int i = 0; i < OBS_PF_H; i++)
+            if (lane + 64 * i < d.O) hp[lane + 64 * i] = f.hp[i];
+        obs_prefetch(d, min(e + waves, env1 - 1), f);  // the next env (the last wave re-reads its own)
+        wave_sync();
+        // window map
+        if (lane < d.E && ((cw[lane] >> 16) & 1)) {
+            const int32_t p = pos[lane];
+            const int x = unpack_x(p), y = unpack_y(p);
+#pragma unroll
+            for (int a = 0; a < NOBS; a++) {
+                const int32_t ap = pos[a];
+                const int dx = x - (unpack_x(ap) - WW / 2), dy = y - (unpack_y(ap) - WW / 2);
+                if (dx >= 0 && dy >= 0 && dx < WW && dy < WW) img[a * PLANE + dy * WW + dx] = (uint8_t)(lane + 1);
+            }
+        }
+        wave_sync();
+        // the store stream
+#pragma unroll 1
+        for (int a = 0; a < NOBS; a++) {
+            const int32_t ap = pos[a];
+            const int ox = unpack_x(ap) - WW / 2, oy = unpack_y(ap) - WW / 2;
+            const lu8* wm = img + a * PLANE;
+            T* o = out + ((size_t)e * NOBS + a) * C * PLANE;
+#pragma unroll
+            for (int i = 0; i < PER; i++) {
+                const int cell = lane + 64 * i;
+                const int cc = cell < PLANE ? cell : PLANE - 1;
+                const int r = cc / WW, q = cc - r * WW;
+                int code, lf, weapon;
+                obs_cell_fast(d, L, st, img, wm, cc, ox + q, oy + r, code, lf, weapon);
+                if (cell < PLANE) obs_store(o, PLANE, cell, ch, code, lf, weapon);
+            }
+        }
+        wave_sync();
+    }
 }

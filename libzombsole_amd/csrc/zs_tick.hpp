@@ -854,15 +854,16 @@ __device__ __forceinline__ void coop_refill(const Dev& d, int base, int count, c
 // ---------------------------------------------------------------------------
 // k_tick: one workgroup = one wave = 64/G envs
 // ---------------------------------------------------------------------------
+// envs [env0, env1) of this launch; workgroup wg takes the NE envs from env0 + wg * NE
 template <int G>
 __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* actions, double* rew, uint8_t* done_out,
                                         uint8_t* trunc_out, uint8_t* listed_out, uint8_t* reset_out, int* reset_list,
-                                        int* reset_count, void* obs_out) {
+                                        int* reset_count, void* obs_out, int env0, int env1) {
     extern __shared__ __align__(16) uint8_t smem[];
     constexpr int NE = 64 / G;
     const int lane = threadIdx.x, g = lane / G, j = lane - g * G;
-    const int base = wg * NE, e = base + g, N = d.N, E = d.E, A = d.A;
-    const bool active = e < N;
+    const int base = env0 + wg * NE, e = base + g, N = d.N, E = d.E, A = d.A;
+    const bool active = e < env1;
     const bool leader = j == 0;
     const TickLayout L = tick_layout(NE, E, d.DW, d.rw_cap, d.cand_cap, d.lists_cap, A, d.fobs ? d.obsl.bytes + 4 * d.obs_stat : 0);
     lu32* lst = (lu32*)(smem + L.off_lst);
@@ -1080,14 +1081,14 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
     }
     wave_sync();
     STAMP(5);
-    coop_refill(d, base, min(NE, N - base), lst, (lu32*)(smem + L.off_bm));
+    coop_refill(d, base, min(NE, env1 - base), lst, (lu32*)(smem + L.off_bm));
     STAMP(6);
 }
 
 template <int G>
 __global__ void __launch_bounds__(64, ZS_STEP_WAVES) k_tick(Dev d, const int32_t* actions, double* rew, uint8_t* done_out,
                                              uint8_t* trunc_out, uint8_t* listed_out, uint8_t* reset_out,
-                                             int* reset_list, int* reset_count, void* obs_out) {
+                                             int* reset_list, int* reset_count, void* obs_out, int env0, int env1) {
     tick_wg<G>(d, xcd_remap(blockIdx.x, gridDim.x), actions, rew, done_out, trunc_out, listed_out, reset_out, reset_list,
-               reset_count, obs_out);
+               reset_count, obs_out, env0, env1);
 }

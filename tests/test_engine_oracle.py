@@ -118,12 +118,16 @@ def test_multi_bots_survival_rich_int16():
 # Alternative kernel paths the engine picks by map / size (or that diagnostics force): each must be
 # bit-exact too.  The variables are read once, when the handle is created.
 PATHS = {
-    "unfused": {"ZS_FUSED": "0"},                  # separate k_reset launch, observations by k_obs
-    "obs_separate": {"ZS_FOBS": "0"},               # fused step launch, observations by k_obs
+    "unfused": {"ZS_FUSED": "0"},                  # separate k_reset launch
+    "fused": {"ZS_FUSED": "1"},                    # reset work inside the step launch
+    "obs_in_step": {"ZS_FOBS": "1"},               # observations written by the step / reset launches
+    "obs_in_step_unfused": {"ZS_FOBS": "1", "ZS_FUSED": "0"},
+    "obs_k_obs": {"ZS_FOBS": "0", "ZS_OBS_PIPE": "0"},  # one-env-per-wave k_obs instead of k_obs_pipe
     "obs_scan": {"ZS_OBS_WIN": "0"},                # per-cell entity scan instead of the window map
-    "obs_scan_separate": {"ZS_OBS_WIN": "0", "ZS_FOBS": "0"},
+    "obs_scan_in_step": {"ZS_OBS_WIN": "0", "ZS_FOBS": "1"},
     "obs_scell": {"ZS_OBS_STAT": "0"},              # per-cell static words instead of LDS bitmaps
-    "obs_scell_separate": {"ZS_OBS_STAT": "0", "ZS_FOBS": "0"},
+    "obs_scell_in_step": {"ZS_OBS_STAT": "0", "ZS_FOBS": "1"},
+    "chunked": {"ZS_CHUNKS": "4", "ZS_FUSED": "0"},  # tick / observation pipeline over 4 env chunks
     "no_lds_budget": {"ZS_LDS_BUDGET": "0"},        # largest LDS copies instead of occupancy-first
 }
 
@@ -132,7 +136,7 @@ PATHS = {
 def test_kernel_paths(path, monkeypatch):
     for k, v in PATHS[path].items():
         monkeypatch.setenv(k, v)
-    run_parity(c2, 96, 60, check_state_every=30)
+    run_parity(c2, 256 if path == "chunked" else 96, 60, check_state_every=30)
     run_parity(lambda n: _abi.single_env_config(n, "safehouse", ["terminator"], "city_for_safehouse", "0",
                                                 initial_zombies=20, minimum_zombies=20,
                                                 observation_scope="world", observation_position_encoding="channels",
