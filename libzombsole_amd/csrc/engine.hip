@@ -249,6 +249,11 @@ struct zs_handle {
     hipEvent_t ev_chunk[8] = {};
     hipEvent_t ev_join = nullptr;
     int obs_pipe_wgs = 8;  // its workgroups per CU
+    // next-step reset work on a side stream, concurrent with the tick (the two touch disjoint envs);
+    // the caller's stream joins it before the observations
+    int reset_side = 0;
+    hipStream_t s_reset = nullptr;
+    hipEvent_t ev_rfork = nullptr, ev_rjoin = nullptr;
     int state_words;
     std::vector<void*> allocs;
     int32_t* d_state;
@@ -312,6 +317,11 @@ static void free_all(zs_handle* h) {
     h->ev_join = nullptr;
     if (h->s_obs) (void)hipStreamDestroy(h->s_obs);
     h->s_obs = nullptr;
+    if (h->ev_rfork) (void)hipEventDestroy(h->ev_rfork);
+    if (h->ev_rjoin) (void)hipEventDestroy(h->ev_rjoin);
+    h->ev_rfork = h->ev_rjoin = nullptr;
+    if (h->s_reset) (void)hipStreamDestroy(h->s_reset);
+    h->s_reset = nullptr;
     for (hipEvent_t ev : h->ev_pool) (void)hipEventDestroy(ev);
     h->ev_pool.clear();
 }
@@ -599,7 +609,11 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
             d.O > 0 && d.E <= 64 && d.DW <= 64 * OBS_PF_D && d.O <= 64 * OBS_PF_H && d.OW <= 64 &&
             d.obs_stat * 4 + 4 * L.bytes <= 64 * 1024 && !getenv_off("ZS_OBS_PIPE")) {
             h->obs_pipe = nobs;
-            h->obs_pipe_wgs = std::max(1, std::min(8, 160 * 1024 / (d.obs_stat * 4 + 4 * L.bytes)));
+            // two workgroups (8 waves) per CU: measured at 65536 envs, 0.350 ms per launch against 0.375
+            // at 8 and 0.38 at 3-4 (a smaller set of env blocks in flight at once); one contiguous env
+            // range per wave instead of the strided walk measured slower (0.383)
+            h->obs_pipe_wgs = std::max(1, std::min(2, 160 * 1024 / (d.obs_stat * 4 + 4 * L.bytes)));
+            if (getenv("ZS_OBS_WGS")) h->obs_pipe_wgs = std::max(1, std::min(32, atoi(getenv("ZS_OBS_WGS"))));
         }
         // with the store-stream kernel available the observations are its job (measured faster than
         // writing them from the tick workgroups at both 8192 and 65536 envs); ZS_FOBS=1 forces them
@@ -619,7 +633,13 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
         const char* fz = getenv("ZS_FUSED");
         h->fused = fz ? atoi(fz) != 0 : h->resident >= h->want;
         if (!h->fused) TRY(choose_layout(h, cfg->lanes_per_env, false, obs_b));
-        h->reset_lds = (size_t)reset_lds_bytes(d.E, d.DW, d.ncand, d.lists_cap, obs_b);
+        // the reset launch stages the static spawn lists whenever they fit (no serial global loads in
+        // its candidate filters); a fused launch shares the tick's choice
+        d.rlists_cap = d.lists_cap;
+        if (!h->fused && d.nps + d.nzs <= 4096 &&
+            reset_lds_bytes(d.E, d.DW, d.ncand, d.nps + d.nzs, obs_b) <= 64 * 1024 && !getenv_off("ZS_RESET_LISTS"))
+            d.rlists_cap = d.nps + d.nzs;
+        h->reset_lds = (size_t)reset_lds_bytes(d.E, d.DW, d.ncand, d.rlists_cap, obs_b);
     }
     if (h->reset_lds > 160 * 1024) {
         free_all(h);
@@ -642,6 +662,12 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
             if (h->chunks > 1 && hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) != hipSuccess) h->chunks = 1;
         }
     }
+    // side-stream reset work (unfused steps; ZS_RESET_STREAM=0 keeps it on the caller's stream)
+    if (!h->fused && !getenv_off("ZS_RESET_STREAM")) {
+        h->reset_side = hipStreamCreateWithFlags(&h->s_reset, hipStreamNonBlocking) == hipSuccess &&
+                        hipEventCreateWithFlags(&h->ev_rfork, hipEventDisableTiming) == hipSuccess &&
+                        hipEventCreateWithFlags(&h->ev_rjoin, hipEventDisableTiming) == hipSuccess;
+    }
     if (h->reset_lds > 64 * 1024 &&
         hipFuncSetAttribute((const void*)k_reset, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->reset_lds) !=
             hipSuccess) {
@@ -651,9 +677,10 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
     }
     if (getenv("ZS_VERBOSE"))
         fprintf(stderr, "zs_create: N=%d E=%d G=%d step_lds=%zu resident=%d reset_lds=%zu rw_cap=%d cand_cap=%d "
-                        "lists_cap=%d fused=%d fobs=%d obs_img=%d k_obs_img=%d x%d pipe=%d chunks=%d\n", d.N, d.E,
-                h->G, h->lds, h->resident, h->reset_lds, d.rw_cap, d.cand_cap, d.lists_cap, h->fused, d.fobs,
-                d.obsl.bytes, h->obs_l.bytes, h->obs_wpg, h->obs_pipe, h->chunks);
+                        "lists_cap=%d fused=%d fobs=%d obs_img=%d k_obs_img=%d x%d pipe=%d pipe_wgs=%d chunks=%d reset_side=%d\n",
+                d.N, d.E, h->G, h->lds, h->resident, h->reset_lds, d.rw_cap, d.cand_cap, d.lists_cap, h->fused,
+                d.fobs, d.obsl.bytes, h->obs_l.bytes, h->obs_wpg, h->obs_pipe, h->obs_pipe_wgs, h->chunks,
+                h->reset_side);
     if (d.O > 0) {
         size_t n = N * d.O;
         hipLaunchKernelGGL(k_init_obstacles, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, d);
@@ -800,7 +827,9 @@ static int launch_tick(zs_handle* h, const int32_t* actions, double* rew, uint8_
 
 static int launch_reset(zs_handle* h, int list_mode, const uint8_t* mask, void* obs, hipStream_t s) {
     const Dev& d = h->d;
-    unsigned grid = (unsigned)std::min(d.N, list_mode ? 512 : 4096);
+    // enough one-wave workgroups that a step's resets (~850 at 65536 envs, bridge64) run in one round
+    static const int rgrid = getenv("ZS_RESET_GRID") ? std::max(1, atoi(getenv("ZS_RESET_GRID"))) : 2048;
+    unsigned grid = (unsigned)std::min(d.N, list_mode ? rgrid : 4096);
     int p = h->rpar;
     int i0 = -1, i1 = -1;
     if (h->prof) HIPCHK(hipEventRecord(prof_event(h, &i0), s));
@@ -862,14 +891,24 @@ extern "C" int zs_step(zs_handle* h, const int32_t* actions_dev, void* obs_dev, 
     // 1) rebuild the envs that ended at the previous call (list[p]); fused into the tick launch
     //    when the LDS images allow, else a k_reset launch first
     int q = 1 - h->rpar, rc = ZS_OK;
+    bool side = false;
     if (!h->fused) {
-        rc = launch_reset(h, 1, nullptr, h->d.fobs ? obs_dev : nullptr, s);
+        side = h->reset_side != 0;
+        hipStream_t rs = s;
+        if (side) {  // fork: the reset work sees everything the caller queued before this call
+            HIPCHK(hipEventRecord(h->ev_rfork, s));
+            HIPCHK(hipStreamWaitEvent(h->s_reset, h->ev_rfork, 0));
+            rs = h->s_reset;
+        }
+        rc = launch_reset(h, 1, nullptr, h->d.fobs ? obs_dev : nullptr, rs);
         if (rc) return rc;
+        if (side) HIPCHK(hipEventRecord(h->ev_rjoin, h->s_reset));
     }
     // 2) tick every other env; envs that end now are queued on list[q] for the next call
     HIPCHK(hipMemsetAsync(h->d_rcount + q, 0, sizeof(int), s));
     const int K = (!h->fused && !h->d.fobs && obs_dev) ? h->chunks : 1;
     if (K > 1) {
+        if (side) HIPCHK(hipStreamWaitEvent(s, h->ev_rjoin, 0));
         // 3) pipelined: the tick of chunk c + 1 (caller's stream) runs while the observations of chunk
         //    c stream out on the engine's second stream; the caller's stream joins at the end
         const int N = h->d.N;
@@ -892,7 +931,9 @@ extern "C" int zs_step(zs_handle* h, const int32_t* actions_dev, void* obs_dev, 
                      h->d_rcount + q, obs_dev, s);
     if (rc) return rc;
     h->rpar = q;
-    // 3) observations of every env (already written by the step launch when fobs)
+    // join the reset work, then 3) observations of every env (already written by the step launch
+    // when fobs)
+    if (side) HIPCHK(hipStreamWaitEvent(s, h->ev_rjoin, 0));
     if (h->d.fobs) return ZS_OK;
     return launch_obs(h, obs_dev, nullptr, s);
 }

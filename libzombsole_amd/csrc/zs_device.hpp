@@ -78,6 +78,7 @@ struct Dev {
     int rw_step;     // words prefetched for a plain step (resets prefetch rw_cap)
     int cand_cap;    // spawn-candidate entries staged in LDS per env (0 = global scratch)
     int lists_cap;   // static spawn-list entries staged in LDS per workgroup (0 = read from global)
+    int rlists_cap;  // the same for the reset work (k_reset has its own LDS budget; = lists_cap when fused)
     int fobs;        // observations are written by the step launch itself (tick and reset work)
     ObsLayout obsl;  // one env's observation image (zs_obs.hpp)
     int obs_stat;    // static observation tables staged beside the image (4 * DW words), 0 = none

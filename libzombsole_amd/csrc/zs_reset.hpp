@@ -21,27 +21,45 @@ struct WaveRng {
     uint32_t st;          // ring state of the register block's word 0 (uniform)
     int pos;              // next unconsumed word within the block (uniform, 0..WR_BLOCK)
     uint32_t word[WR_Q];  // word[q] = tempered stream word q*64 + lane of the block
-    uint32_t* ring;
-    lu32* tw;             // 2 x 624 words of LDS for the cooperative twist
+    uint32_t* ring;       // the env's ring in HBM (read once at the start, dirty slots written at the end)
+    lu32* lr;             // its LDS copy, 2 x 624 words: every draw and twist of the reset works here
+    int dirty;            // bit s: LDS slot s was twisted and must be written back
 };
 
+// stage the env's ring into LDS: the current slot, and the next one when it is already twisted
+__device__ __forceinline__ void wave_rng_stage(WaveRng& r, uint32_t st) {
+    const uint32_t slot = (st >> 10) & 1u, ready = (st >> 11) & 1u;
+    const int lane = threadIdx.x;
+    stage_in(r.ring + slot * ZS_MT_N, ZS_MT_N, lane, 64, r.lr + slot * ZS_MT_N, [](int k) { return k; });
+    if (ready)
+        stage_in(r.ring + (slot ^ 1u) * ZS_MT_N, ZS_MT_N, lane, 64, r.lr + (slot ^ 1u) * ZS_MT_N, [](int k) { return k; });
+    r.dirty = 0;
+    wave_sync();
+}
+
+// next block of the stream (LDS slot ^ 1) from the current one (_randommodule.c genrand_uint32's
+// twist), cooperatively in three dependency phases
 __device__ __forceinline__ void wave_twist(WaveRng& r, uint32_t slot) {
     const int lane = threadIdx.x;
-    const uint32_t* src = r.ring + slot * ZS_MT_N;
-    uint32_t* dst = r.ring + (slot ^ 1u) * ZS_MT_N;
-    stage_in(src, ZS_MT_N, lane, 64, r.tw, [](int k) { return k; });
-    wave_sync();
-    lu32* nw = r.tw + ZS_MT_N;
-    for (int k = lane; k < ZS_MT_N - ZS_MT_M; k += 64) nw[k] = mt_f(r.tw[k], r.tw[k + 1], r.tw[k + ZS_MT_M]);
+    const lu32* src = r.lr + slot * ZS_MT_N;
+    lu32* nw = r.lr + (slot ^ 1u) * ZS_MT_N;
+    for (int k = lane; k < ZS_MT_N - ZS_MT_M; k += 64) nw[k] = mt_f(src[k], src[k + 1], src[k + ZS_MT_M]);
     wave_sync();
     for (int k = (ZS_MT_N - ZS_MT_M) + lane; k < 2 * (ZS_MT_N - ZS_MT_M); k += 64)
-        nw[k] = mt_f(r.tw[k], r.tw[k + 1], nw[k + ZS_MT_M - ZS_MT_N]);
+        nw[k] = mt_f(src[k], src[k + 1], nw[k + ZS_MT_M - ZS_MT_N]);
     wave_sync();
     for (int k = 2 * (ZS_MT_N - ZS_MT_M) + lane; k < ZS_MT_N; k += 64)
-        nw[k] = mt_f(r.tw[k], k + 1 < ZS_MT_N ? r.tw[k + 1] : nw[0], nw[k + ZS_MT_M - ZS_MT_N]);
+        nw[k] = mt_f(src[k], k + 1 < ZS_MT_N ? src[k + 1] : nw[0], nw[k + ZS_MT_M - ZS_MT_N]);
     wave_sync();
-    for (int k = lane; k < ZS_MT_N; k += 64) dst[k] = nw[k];
-    __syncthreads();  // the new block's global stores complete before the wave re-reads it
+    r.dirty |= 1 << (slot ^ 1u);
+}
+
+// write the twisted slots back to the env's ring in HBM (no wait: the next reader is a later launch)
+__device__ __forceinline__ void wave_rng_flush(const WaveRng& r) {
+    const int lane = threadIdx.x;
+    for (int sl = 0; sl < 2; sl++)
+        if ((r.dirty >> sl) & 1)
+            for (int k = lane; k < ZS_MT_N; k += 64) r.ring[sl * ZS_MT_N + k] = r.lr[sl * ZS_MT_N + k];
 }
 
 // load the WR_BLOCK words that start at ring state st (twisting the next block first if needed)
@@ -60,10 +78,8 @@ __device__ __forceinline__ void wave_rng_load(WaveRng& r, uint32_t st) {
 #pragma unroll
     for (int q = 0; q < WR_Q; q++) {
         uint32_t p = off + q * 64 + threadIdx.x;
-        r.word[q] = p < ZS_MT_N ? r.ring[slot * ZS_MT_N + p] : r.ring[(slot ^ 1u) * ZS_MT_N + p - ZS_MT_N];
+        r.word[q] = mt_temper(p < ZS_MT_N ? r.lr[slot * ZS_MT_N + p] : r.lr[(slot ^ 1u) * ZS_MT_N + p - ZS_MT_N]);
     }
-#pragma unroll
-    for (int q = 0; q < WR_Q; q++) r.word[q] = mt_temper(r.word[q]);
     r.st = st_pack(off, slot, ready);
     r.pos = 0;
 }
@@ -72,7 +88,7 @@ __device__ __forceinline__ uint32_t wr_sub(const WaveRng& r, int q) {
     return q == 0 ? r.word[0] : q == 1 ? r.word[1] : q == 2 ? r.word[2] : r.word[3];
 }
 
-#define WR_H 4  // rejection hypotheses resolved per round
+#define WR_H 4  // rejection hypotheses evaluated per batch (one ballot each)
 
 // `count` consecutive draws _randbelow(b_t), b_t = n - t * dstep (dstep 0: a fixed bound; 1: the
 // decreasing bounds of a Fisher-Yates pass), all in wave-uniform control flow.  Draw t consumes
@@ -80,9 +96,10 @@ __device__ __forceinline__ uint32_t wr_sub(const WaveRng& r, int q) {
 //
 // One round per 64-word sub-block: lane l evaluates its word under each hypothesis "h words of
 // this round before me were rejected" (then it serves draw t = idx - h, idx = l - start), one
-// ballot per hypothesis; the scalar unit walks the chain of first rejections h = 0, 1, 2, ...
-// (up to WR_H per round).  A second pass lets every accepted lane store its draw's value into
-// out[t] for t < krec.  Returns nothing; advances r past the consumed words.
+// ballot per hypothesis, WR_H hypotheses per batch; the scalar unit walks the chain of first
+// rejections h = 0, 1, 2, ... and evaluates further batches until the chain reaches the end of the
+// sub-block (or of the draws), so a round resolves any number of rejections.  Every accepted lane
+// then stores its draw's value into out[t] for t < krec.  Advances r past the consumed words.
 __device__ __forceinline__ void wave_draws(WaveRng& r, int n, int dstep, int count, int krec, lu32* out) {
     const int lane = threadIdx.x;
     int done = 0;
@@ -91,33 +108,39 @@ __device__ __forceinline__ void wave_draws(WaveRng& r, int n, int dstep, int cou
         const int q = r.pos >> 6, base = q << 6, start = r.pos - base;
         const uint32_t w = wr_sub(r, q);
         const int idx = lane - start;
-        unsigned long long rej[WR_H], live[WR_H];
-#pragma unroll
-        for (int h = 0; h < WR_H; h++) {
-            int t = done + idx - h;            // draw this word serves under hypothesis h
-            bool lv = idx >= h && t < count;
-            int b = n - t * dstep;
-            int kk = 32 - __clz(max(b, 1));
-            bool rj = lv && (w >> (32 - kk)) >= (uint32_t)b;
-            rej[h] = __ballot(rj);
-            live[h] = __ballot(lv);
-        }
-        // resolve the chain of rejections
         unsigned long long rmask = 0;
         int c = start, end = start;
+        for (int hb = 0; c < 64; hb += WR_H) {
+            unsigned long long rej[WR_H], live[WR_H];
 #pragma unroll
-        for (int h = 0; h < WR_H; h++) {
-            const unsigned long long from = c >= 64 ? 0ull : (~0ull << c);
-            unsigned long long m = rej[h] & from, lm = live[h] & from;
-            if (!m) {  // every live word from c on is accepted
-                end = lm ? 64 - __clzll((long long)lm) : c;
-                c = 65;  // resolved
-                break;
+            for (int u = 0; u < WR_H; u++) {
+                const int h = hb + u;
+                int t = done + idx - h;  // draw this word serves under hypothesis h
+                bool lv = idx >= h && t < count;
+                int b = n - t * dstep;
+                int kk = 32 - __clz(max(b, 1));
+                bool rj = lv && (w >> (32 - kk)) >= (uint32_t)b;
+                rej[u] = __ballot(rj);
+                live[u] = __ballot(lv);
             }
-            int p = __ffsll((long long)m) - 1;
-            rmask |= 1ull << p;
-            c = p + 1;
-            end = c;
+            // walk the chain of rejections through this batch
+            bool resolved = false;
+#pragma unroll
+            for (int u = 0; u < WR_H; u++) {
+                const unsigned long long from = ~0ull << c;  // c < 64 here
+                unsigned long long m = rej[u] & from, lm = live[u] & from;
+                if (!m) {  // every live word from c on is accepted
+                    end = lm ? 64 - __clzll((long long)lm) : c;
+                    resolved = true;
+                    break;
+                }
+                int p = __ffsll((long long)m) - 1;
+                rmask |= 1ull << p;
+                c = p + 1;
+                end = c;
+                if (c >= 64) break;
+            }
+            if (resolved) break;
         }
         // accepted lanes in [start, end) store the value of the draw they served
         const bool mine = lane >= start && lane < end && !((rmask >> lane) & 1ull);
@@ -169,7 +192,7 @@ __device__ __forceinline__ int wave_spawn(const Dev& d, const ResetLds& L, WaveR
         int cell = -1;
         if (i < total) {
             if (nlist) {
-                int32_t p = d.lists_cap ? L.lists[(which ? d.nps : 0) + i] : (which ? d.zspawn[i] : d.pspawn[i]);
+                int32_t p = d.rlists_cap ? L.lists[(which ? d.nps : 0) + i] : (which ? d.zspawn[i] : d.pspawn[i]);
                 cell = unpack_y(p) * d.W + unpack_x(p);
             } else {
                 cell = (i % d.H) * d.W + i / d.H;  // x-major (core.py:45-47)
@@ -233,9 +256,10 @@ __device__ __forceinline__ void reset_env_wave(const Dev& d, const ResetLds& L, 
     }
     WaveRng r;
     r.ring = d.ring + (size_t)e * ZS_RING_WORDS;
-    r.tw = L.tw;
-    wave_sync();
-    wave_rng_load(r, d.rngst[e]);
+    r.lr = L.tw;
+    const uint32_t st_in = d.rngst[e];
+    wave_rng_stage(r, st_in);
+    wave_rng_load(r, st_in);
     RST(1);
     // players: Player() picks a random weapon unless its module gives one (things.py:113-116);
     // agents: WeaponFactory.create_player_weapon (weapons.py:28-45).  Each random pick is one
@@ -307,6 +331,7 @@ __device__ __forceinline__ void reset_env_wave(const Dev& d, const ResetLds& L, 
         wave_twist(r, (stf >> 10) & 1u);
         stf |= 1u << 11;
     }
+    wave_rng_flush(r);
     // write the new world back
     for (int s = lane; s < E; s += 64) {
         d.pos[(size_t)s * N + e] = L.lpos[s];
@@ -365,12 +390,12 @@ __device__ __forceinline__ void reset_role(const Dev& d, int list_mode, const in
     L.lslots = (lu8*)(smem + o);
     o += d.E;
     L.lists = (li32*)(smem + o);
-    o += d.lists_cap * 4;
+    o += d.rlists_cap * 4;
     L.jbuf = (lu32*)(smem + o);
     o += (d.E + 8) * 4;
     o = ((o + 15) / 16) * 16;
     L.tw = (lu32*)(smem + o);
-    if (d.lists_cap)
+    if (d.rlists_cap)
         for (int i = threadIdx.x; i < d.nps + d.nzs; i += 64) L.lists[i] = i < d.nps ? d.pspawn[i] : d.zspawn[i - d.nps];
     wave_sync();
     for (int idx = wg; idx < n; idx += nwg) {

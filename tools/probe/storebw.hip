@@ -1,8 +1,13 @@
 // Store-bandwidth probe for the observation write shape (diagnostic, not part of the product).
 // 65536 envs x [2 agents][3 channels][441 cells] int64 = 1.39 GB per pass, written as
-//   k_cells8 : one wave per env, lane = cell, 3 x 8 B stores per cell (k_obs's shape)
-//   k_pairs16: one wave per env, lane = 2 adjacent values, 16 B stores over the env's flat block
-//   k_flat16 : grid-stride 16 B per lane over the whole buffer (memset shape)
+//   cells8   : one wave per env, lane = cell, 3 x 8 B stores per cell (k_obs's shape)
+//   cells8nt : the same with nontemporal stores
+//   pairs16  : one wave per env, lane = 2 adjacent values, 16 B stores over the env's flat block
+//   pairs16nt: the same, nontemporal
+//   lds16    : one wave per env, values written to an LDS copy of the env block (8 B per cell and
+//              channel, k_obs's compute shape), then streamed out 16 B per lane
+//   flat16   : grid-stride 16 B per lane over the whole buffer (memset shape)
+//   p_*      : persistent grids (256 x K workgroups walking envs) of the same bodies
 // hipcc --offload-arch=gfx950 -O3 -o storebw tools/probe/storebw.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -11,67 +16,75 @@
 
 constexpr int NE = 65536, NA = 2, PL = 441, PER = NA * 3 * PL;  // int64 values per env
 
-__global__ void __launch_bounds__(256) k_cells8(int64_t* out, int n) {
-    int e = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (e >= n) return;
+template <bool NT>
+__device__ __forceinline__ void st8(int64_t* p, int64_t v) {
+    if (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
+template <bool NT>
+__device__ __forceinline__ void body_cells8(int64_t* out, int e, int lane) {
     for (int a = 0; a < NA; a++) {
         int64_t* o = out + ((size_t)e * NA + a) * 3 * PL;
         for (int c = lane; c < PL; c += 64) {
-            o[c] = c;
-            o[PL + c] = e;
-            o[2 * PL + c] = a;
+            st8<NT>(o + c, c);
+            st8<NT>(o + PL + c, e);
+            st8<NT>(o + 2 * PL + c, a);
         }
     }
 }
 
-__device__ __forceinline__ int xremap(int b, int nb) {
-    const int q = nb >> 3, r = nb & 7, x = b & 7, k = b >> 3;
-    return x * q + (x < r ? x : r) + k;
-}
-
-// k_cells8 with XCD-contiguous env ranges
-__global__ void __launch_bounds__(256) k_cells8x(int64_t* out, int n) {
-    int e = xremap(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (e >= n) return;
-    for (int a = 0; a < NA; a++) {
-        int64_t* o = out + ((size_t)e * NA + a) * 3 * PL;
-        for (int c = lane; c < PL; c += 64) {
-            o[c] = c;
-            o[PL + c] = e;
-            o[2 * PL + c] = a;
-        }
+template <bool NT>
+__device__ __forceinline__ void body_pairs16(int64_t* out, int e, int lane) {
+    // env block starts 8-B aligned only for odd e (PER is even: 2646 values = 21168 B, 16-B aligned)
+    typedef long long v2i64 __attribute__((ext_vector_type(2)));
+    v2i64* o = (v2i64*)(out + (size_t)e * PER);
+    for (int i = lane; i < PER / 2; i += 64) {
+        v2i64 v = {(long long)i, (long long)e};
+        if (NT) __builtin_nontemporal_store(v, o + i);
+        else o[i] = v;
     }
 }
 
-// k_cells8 after staging RB bytes of per-env state into LDS (the encoder's read side)
-constexpr int RB = 2304;
-__global__ void __launch_bounds__(256) k_cells8r(int64_t* out, const int* st, int n) {
-    __shared__ int img[4][RB / 4];
+__device__ __forceinline__ void body_lds16(int64_t* out, int e, int lane, int64_t* img) {
+    for (int a = 0; a < NA; a++) {
+        for (int c = lane; c < PL; c += 64) {
+            img[a * 3 * PL + c] = c;
+            img[a * 3 * PL + PL + c] = e;
+            img[a * 3 * PL + 2 * PL + c] = a;
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    const longlong2* s = (const longlong2*)img;
+    longlong2* o = (longlong2*)(out + (size_t)e * PER);
+    for (int i = lane; i < PER / 2; i += 64) o[i] = s[i];
+    __builtin_amdgcn_wave_barrier();
+}
+
+template <int K>
+__global__ void __launch_bounds__(256) k_one(int64_t* out, int n) {
+    __shared__ int64_t img[K == 4 ? 4 : 1][K == 4 ? PER : 1];
     int w = threadIdx.x >> 6, e = blockIdx.x * 4 + w, lane = threadIdx.x & 63;
     if (e >= n) return;
-    const int* src = st + (size_t)e * (RB / 4);
-    int v[RB / 4 / 64];
-#pragma unroll
-    for (int i = 0; i < RB / 4 / 64; i++) v[i] = src[lane + 64 * i];
-#pragma unroll
-    for (int i = 0; i < RB / 4 / 64; i++) img[w][lane + 64 * i] = v[i];
-    __builtin_amdgcn_wave_barrier();
-    for (int a = 0; a < NA; a++) {
-        int64_t* o = out + ((size_t)e * NA + a) * 3 * PL;
-        for (int c = lane; c < PL; c += 64) {
-            int x = img[w][(c * 7) % (RB / 4)];
-            o[c] = x;
-            o[PL + c] = e;
-            o[2 * PL + c] = a;
-        }
-    }
+    if (K == 0) body_cells8<false>(out, e, lane);
+    if (K == 1) body_cells8<true>(out, e, lane);
+    if (K == 2) body_pairs16<false>(out, e, lane);
+    if (K == 3) body_pairs16<true>(out, e, lane);
+    if (K == 4) body_lds16(out, e, lane, img[w]);
 }
 
-__global__ void __launch_bounds__(256) k_pairs16(int64_t* out, int n) {
-    int e = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (e >= n) return;
-    longlong2* o = (longlong2*)(out + (size_t)e * PER);
-    for (int i = lane; i < PER / 2; i += 64) o[i] = make_longlong2(i, e);
+template <int K>
+__global__ void __launch_bounds__(256) k_pers(int64_t* out, int n) {
+    __shared__ int64_t img[K == 4 ? 4 : 1][K == 4 ? PER : 1];
+    int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int e = blockIdx.x * 4 + w; e < n; e += gridDim.x * 4) {
+        if (K == 0) body_cells8<false>(out, e, lane);
+        if (K == 1) body_cells8<true>(out, e, lane);
+        if (K == 2) body_pairs16<false>(out, e, lane);
+        if (K == 3) body_pairs16<true>(out, e, lane);
+        if (K == 4) body_lds16(out, e, lane, img[w]);
+    }
 }
 
 __global__ void __launch_bounds__(256) k_flat16(int64_t* out, size_t n2) {
@@ -87,25 +100,35 @@ int main() {
     hipEvent_t a, b;
     CHK(hipEventCreate(&a));
     CHK(hipEventCreate(&b));
-    int* st;
-    CHK(hipMalloc(&st, (size_t)NE * RB));
-    CHK(hipMemset(st, 1, (size_t)NE * RB));
-    const char* names[5] = {"cells8", "pairs16", "flat16", "cells8x", "cells8r"};
-    for (int k = 0; k < 5; k++) {
+    struct V { const char* name; int kind; int grid; };
+    V vs[] = {{"cells8", 0, NE / 4},  {"cells8nt", 1, NE / 4},  {"pairs16", 2, NE / 4}, {"pairs16nt", 3, NE / 4},
+              {"lds16", 4, NE / 4},   {"p_cells8", 10, 256 * 8}, {"p_cells8nt", 11, 256 * 8},
+              {"p_pairs16", 12, 256 * 8}, {"p_pairs16nt", 13, 256 * 8}, {"p_lds16", 14, 256 * 2},
+              {"p_pairs16_g4", 12, 256 * 4}, {"p_pairs16_g16", 12, 256 * 16}, {"flat16", 20, 256 * 32}};
+    for (const V& v : vs) {
         for (int rep = 0; rep < 2; rep++) {
             CHK(hipEventRecord(a));
             for (int it = 0; it < 20; it++) {
-                if (k == 0) hipLaunchKernelGGL(k_cells8, dim3(NE / 4), dim3(256), 0, 0, d, NE);
-                else if (k == 1) hipLaunchKernelGGL(k_pairs16, dim3(NE / 4), dim3(256), 0, 0, d, NE);
-                else if (k == 2) hipLaunchKernelGGL(k_flat16, dim3(256 * 32), dim3(256), 0, 0, d, bytes / 16);
-                else if (k == 3) hipLaunchKernelGGL(k_cells8x, dim3(NE / 4), dim3(256), 0, 0, d, NE);
-                else hipLaunchKernelGGL(k_cells8r, dim3(NE / 4), dim3(256), 0, 0, d, st, NE);
+                switch (v.kind) {
+                case 0: hipLaunchKernelGGL(k_one<0>, dim3(v.grid), dim3(256), 0, 0, d, NE); break;
+                case 1: hipLaunchKernelGGL(k_one<1>, dim3(v.grid), dim3(256), 0, 0, d, NE); break;
+                case 2: hipLaunchKernelGGL(k_one<2>, dim3(v.grid), dim3(256), 0, 0, d, NE); break;
+                case 3: hipLaunchKernelGGL(k_one<3>, dim3(v.grid), dim3(256), 0, 0, d, NE); break;
+                case 4: hipLaunchKernelGGL(k_one<4>, dim3(v.grid), dim3(256), 0, 0, d, NE); break;
+                case 10: hipLaunchKernelGGL(k_pers<0>, dim3(v.grid), dim3(256), 0, 0, d, NE); break;
+                case 11: hipLaunchKernelGGL(k_pers<1>, dim3(v.grid), dim3(256), 0, 0, d, NE); break;
+                case 12: hipLaunchKernelGGL(k_pers<2>, dim3(v.grid), dim3(256), 0, 0, d, NE); break;
+                case 13: hipLaunchKernelGGL(k_pers<3>, dim3(v.grid), dim3(256), 0, 0, d, NE); break;
+                case 14: hipLaunchKernelGGL(k_pers<4>, dim3(v.grid), dim3(256), 0, 0, d, NE); break;
+                default: hipLaunchKernelGGL(k_flat16, dim3(v.grid), dim3(256), 0, 0, d, bytes / 16); break;
+                }
             }
+            CHK(hipGetLastError());
             CHK(hipEventRecord(b));
             CHK(hipEventSynchronize(b));
             float ms;
             CHK(hipEventElapsedTime(&ms, a, b));
-            if (rep) printf("%-10s %8.1f us/pass  %6.2f TB/s (written)\n", names[k], ms * 1e3 / 20,
+            if (rep) printf("%-14s grid %6d %8.1f us/pass  %6.2f TB/s (written)\n", v.name, v.grid, ms * 1e3 / 20,
                             bytes / (ms / 20 * 1e-3) / 1e12);
         }
     }
