@@ -29,22 +29,48 @@ METRIC = "env-steps/sec (whole node), 65 536 parallel 64×64 envs at 1/2/4/8 MI3
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 
 
+# C2 4 096 envs on 1 GPU; C3 (headline) 65 536 envs over the node's GPUs; C4
+# synthetic city128 safehouse, 4 agents + 50 zombies (minimum 50), 16 384 envs; C5 Multiagent 4
+# agents + 20 zombies, 65 536 envs, observations all-gathered every step.
+PRESETS = {
+    "c2": dict(envs=4096, map="bridge64", agents=2, zombies=10, min_zombies=0, rules="extermination", gather=False,
+               obs_dtype="int64"),
+    "c3": dict(envs=65536, map="bridge64", agents=2, zombies=10, min_zombies=0, rules="extermination", gather=False,
+               obs_dtype="int64"),
+    "c4": dict(envs=16384, map="city128", agents=4, zombies=50, min_zombies=50, rules="safehouse", gather=False,
+               obs_dtype="int64"),
+    # C5 gathers compact int16 observations (lossless, 1/4 of the xGMI bytes)
+    "c5": dict(envs=65536, map="bridge64", agents=4, zombies=20, min_zombies=0, rules="extermination", gather=True,
+               obs_dtype="int16"),
+}
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=20)
-    p.add_argument("--envs", type=int, default=65536, help="total envs over all ranks (strong scaling)")
+    p.add_argument("--envs", type=int, default=None, help="total envs over all ranks (strong scaling)")
     p.add_argument("--envs-per-gpu", type=int, default=0, help="fixed envs per rank instead (weak scaling)")
-    p.add_argument("--map", default="bridge64")
-    p.add_argument("--agents", type=int, default=2)
-    p.add_argument("--zombies", type=int, default=10)
+    p.add_argument("--config", default="c3", choices=sorted(PRESETS),
+                   help="BASELINE.json configs[1..4] (SURVEY.md §8(d) C2..C5); c3 = the headline metric")
+    p.add_argument("--map", default=None)
+    p.add_argument("--agents", type=int, default=None)
+    p.add_argument("--zombies", type=int, default=None)
+    p.add_argument("--min-zombies", type=int, default=None)
+    p.add_argument("--rules", default=None)
+    p.add_argument("--gather", action="store_true", default=None,
+                   help="all-gather the observation shards every step (C5's RCCL exchange)")
     p.add_argument("--max-episode-steps", type=int, default=1000)
-    p.add_argument("--obs-dtype", default="int64", choices=["int64", "int32", "int16"])
+    p.add_argument("--obs-dtype", default=None, choices=["int64", "int32", "int16"])
     p.add_argument("--lanes-per-env", type=int, default=0, help="k_tick lanes per env (0 = engine default)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-steps", type=int, default=2000)
-    return p.parse_args()
+    a = p.parse_args()
+    for k, v in PRESETS[a.config].items():
+        if getattr(a, k) is None:
+            setattr(a, k, v)
+    return a
 
 
 def algorithmic_bytes(E, A, occ_bytes, obs_bytes_per_env, mt_words):
@@ -69,13 +95,18 @@ def cpu_baseline(args, builder_fn):
     threads = max(1, min(threads, int(os.environ.get("OMP_NUM_THREADS", "16") or 16), 16))
     n_envs = 8192
     b = builder_fn(1)
+    steps = args.cpu_steps
+    if args.config != "c3":  # heavier configs: size the sample from a short probe (~2 s wall)
+        t0 = time.perf_counter()
+        run_batch(b, 0, n_envs, 20, 7, threads=threads)
+        steps = max(20, min(steps, int(20 * 2.0 / max(time.perf_counter() - t0, 1e-3))))
     t0 = time.perf_counter()
-    n, _ = run_batch(b, 0, n_envs, args.cpu_steps, 7, threads=threads)
+    n, _ = run_batch(b, 0, n_envs, steps, 7, threads=threads)
     dt = time.perf_counter() - t0
     return {"value": n / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
             "sample": "C oracle (oracle/zs_oracle.c, OpenMP over envs), %d envs x %d steps of the same "
                       "workload (same map/agents/zombies/policy/obs, autoreset, TimeLimit), %.1f s wall x %d "
-                      "threads = %.0f thread-s" % (n_envs, args.cpu_steps, dt, threads, dt * threads)}
+                      "threads = %.0f thread-s" % (n_envs, steps, dt, threads, dt * threads)}
 
 
 def main():
@@ -100,8 +131,8 @@ def main():
     agent_ids = [str(i) for i in range(args.agents)]
 
     def builder(n):
-        return _abi.multi_env_config(n, "extermination", [], args.map, agent_ids, initial_zombies=args.zombies,
-                                     minimum_zombies=0, max_episode_steps=args.max_episode_steps,
+        return _abi.multi_env_config(n, args.rules, [], args.map, agent_ids, initial_zombies=args.zombies,
+                                     minimum_zombies=args.min_zombies, max_episode_steps=args.max_episode_steps,
                                      obs_dtype=dtype, lanes_per_env=args.lanes_per_env)
 
     if args.envs_per_gpu:
@@ -116,11 +147,29 @@ def main():
     eng.reset()
     torch.cuda.synchronize()
 
+    gather = None
+    if args.gather and world > 1:
+        # C5: every step's observation shards + (rewards, done, truncated) packed per env, all-gathered
+        # over RCCL into preallocated node-wide tensors (a centralised learner's input)
+        A = args.agents
+        pack = torch.empty((n_local, 8 * A + 2), dtype=torch.uint8, device="cuda")
+        g_obs = torch.empty((world * n_local,) + tuple(eng.obs.shape[1:]), dtype=eng.obs.dtype, device="cuda")
+        g_pack = torch.empty((world * n_local, 8 * A + 2), dtype=torch.uint8, device="cuda")
+
+        def gather():
+            pack[:, :8 * A].copy_(eng.rewards.view(torch.uint8).view(n_local, 8 * A))
+            pack[:, 8 * A] = eng.done.view(torch.uint8)
+            pack[:, 8 * A + 1] = eng.trunc.view(torch.uint8)
+            dist.all_gather_into_tensor(g_obs, eng.obs)
+            dist.all_gather_into_tensor(g_pack, pack)
+
     step = 0
     for _ in range(args.warmup):
         step += 1
         eng.gen_actions(step, 7)
         eng.step()
+        if gather:
+            gather()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -133,6 +182,8 @@ def main():
         step += 1
         eng.gen_actions(step, 7)
         eng.step()
+        if gather:
+            gather()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -176,14 +227,20 @@ def main():
         "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True,
         "scaling": scaling, "vs_baseline": None, "dtype": "int32", "data": "synthetic",
-        "config": {"workload": "%d parallel %dx%d '%s' envs over %d GPU(s) (%d per GPU), extermination, %d agents + "
-                               "%d zombies, MultiagentZombsoleEnv rewards, uniform Discrete(7) policy on device, "
-                               "21x21x3 %s obs per agent written to HBM every step, TimeLimit %d, next-step "
-                               "autoreset" % (total_envs, m.size[0], m.size[1], args.map, world, n_local,
-                                              args.agents, args.zombies, args.obs_dtype, args.max_episode_steps),
-                   "envs_per_gpu": n_local, "total_envs": total_envs, "map": args.map,
-                   "agents": args.agents, "zombies": args.zombies, "obs_dtype": args.obs_dtype,
-                   "parallelism": "env-sharded x%d (no data-path collective)" % world},
+        "config": {"workload": "%s: %d parallel %dx%d '%s' envs over %d GPU(s) (%d per GPU), %s, %d agents + "
+                               "%d zombies (minimum %d), MultiagentZombsoleEnv rewards, uniform Discrete(7) policy "
+                               "on device, 21x21x3 %s obs per agent written to HBM every step%s, TimeLimit %d, "
+                               "next-step autoreset" % (
+                                   args.config.upper(), total_envs, m.size[0], m.size[1], args.map, world, n_local,
+                                   args.rules, args.agents, args.zombies, args.min_zombies, args.obs_dtype,
+                                   " and all-gathered over RCCL with rewards/done/truncated" if gather else "",
+                                   args.max_episode_steps),
+                   "preset": args.config, "envs_per_gpu": n_local, "total_envs": total_envs, "map": args.map,
+                   "rules": args.rules, "agents": args.agents, "zombies": args.zombies,
+                   "minimum_zombies": args.min_zombies, "obs_dtype": args.obs_dtype,
+                   "parallelism": "env-sharded x%d (%s)" % (
+                       world, "RCCL all-gather of obs + rewards/done per step" if gather
+                       else "no data-path collective")},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
                      "algorithmic_bytes_per_step": dom_b * n_local,

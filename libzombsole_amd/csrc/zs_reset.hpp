@@ -13,148 +13,7 @@
 // from an env mask (zs_reset).
 #pragma once
 #include "zs_tick.hpp"
-
-#define WR_Q 4               // words per lane held in registers
-#define WR_BLOCK (64 * WR_Q)  // words per register block
-
-struct WaveRng {
-    uint32_t st;          // ring state of the register block's word 0 (uniform)
-    int pos;              // next unconsumed word within the block (uniform, 0..WR_BLOCK)
-    uint32_t word[WR_Q];  // word[q] = tempered stream word q*64 + lane of the block
-    uint32_t* ring;       // the env's ring in HBM (read once at the start, dirty slots written at the end)
-    lu32* lr;             // its LDS copy, 2 x 624 words: every draw and twist of the reset works here
-    int dirty;            // bit s: LDS slot s was twisted and must be written back
-};
-
-// stage the env's ring into LDS: the current slot, and the next one when it is already twisted
-__device__ __forceinline__ void wave_rng_stage(WaveRng& r, uint32_t st) {
-    const uint32_t slot = (st >> 10) & 1u, ready = (st >> 11) & 1u;
-    const int lane = threadIdx.x;
-    stage_in(r.ring + slot * ZS_MT_N, ZS_MT_N, lane, 64, r.lr + slot * ZS_MT_N, [](int k) { return k; });
-    if (ready)
-        stage_in(r.ring + (slot ^ 1u) * ZS_MT_N, ZS_MT_N, lane, 64, r.lr + (slot ^ 1u) * ZS_MT_N, [](int k) { return k; });
-    r.dirty = 0;
-    wave_sync();
-}
-
-// next block of the stream (LDS slot ^ 1) from the current one (_randommodule.c genrand_uint32's
-// twist), cooperatively in three dependency phases
-__device__ __forceinline__ void wave_twist(WaveRng& r, uint32_t slot) {
-    const int lane = threadIdx.x;
-    const lu32* src = r.lr + slot * ZS_MT_N;
-    lu32* nw = r.lr + (slot ^ 1u) * ZS_MT_N;
-    for (int k = lane; k < ZS_MT_N - ZS_MT_M; k += 64) nw[k] = mt_f(src[k], src[k + 1], src[k + ZS_MT_M]);
-    wave_sync();
-    for (int k = (ZS_MT_N - ZS_MT_M) + lane; k < 2 * (ZS_MT_N - ZS_MT_M); k += 64)
-        nw[k] = mt_f(src[k], src[k + 1], nw[k + ZS_MT_M - ZS_MT_N]);
-    wave_sync();
-    for (int k = 2 * (ZS_MT_N - ZS_MT_M) + lane; k < ZS_MT_N; k += 64)
-        nw[k] = mt_f(src[k], k + 1 < ZS_MT_N ? src[k + 1] : nw[0], nw[k + ZS_MT_M - ZS_MT_N]);
-    wave_sync();
-    r.dirty |= 1 << (slot ^ 1u);
-}
-
-// write the twisted slots back to the env's ring in HBM (no wait: the next reader is a later launch)
-__device__ __forceinline__ void wave_rng_flush(const WaveRng& r) {
-    const int lane = threadIdx.x;
-    for (int sl = 0; sl < 2; sl++)
-        if ((r.dirty >> sl) & 1)
-            for (int k = lane; k < ZS_MT_N; k += 64) r.ring[sl * ZS_MT_N + k] = r.lr[sl * ZS_MT_N + k];
-}
-
-// load the WR_BLOCK words that start at ring state st (twisting the next block first if needed)
-__device__ __forceinline__ void wave_rng_load(WaveRng& r, uint32_t st) {
-    uint32_t off = st & 1023u, slot = (st >> 10) & 1u, ready = (st >> 11) & 1u;
-    if (off >= ZS_MT_N) {
-        if (!ready) wave_twist(r, slot);
-        slot ^= 1u;
-        off = 0;
-        ready = 0;
-    }
-    if (off + WR_BLOCK > ZS_MT_N && !ready) {
-        wave_twist(r, slot);
-        ready = 1;
-    }
-#pragma unroll
-    for (int q = 0; q < WR_Q; q++) {
-        uint32_t p = off + q * 64 + threadIdx.x;
-        r.word[q] = mt_temper(p < ZS_MT_N ? r.lr[slot * ZS_MT_N + p] : r.lr[(slot ^ 1u) * ZS_MT_N + p - ZS_MT_N]);
-    }
-    r.st = st_pack(off, slot, ready);
-    r.pos = 0;
-}
-
-__device__ __forceinline__ uint32_t wr_sub(const WaveRng& r, int q) {
-    return q == 0 ? r.word[0] : q == 1 ? r.word[1] : q == 2 ? r.word[2] : r.word[3];
-}
-
-#define WR_H 4  // rejection hypotheses evaluated per batch (one ballot each)
-
-// `count` consecutive draws _randbelow(b_t), b_t = n - t * dstep (dstep 0: a fixed bound; 1: the
-// decreasing bounds of a Fisher-Yates pass), all in wave-uniform control flow.  Draw t consumes
-// words until one word w gives (w >> (32 - bitlen(b_t))) < b_t (random.py:239-249).
-//
-// One round per 64-word sub-block: lane l evaluates its word under each hypothesis "h words of
-// this round before me were rejected" (then it serves draw t = idx - h, idx = l - start), one
-// ballot per hypothesis, WR_H hypotheses per batch; the scalar unit walks the chain of first
-// rejections h = 0, 1, 2, ... and evaluates further batches until the chain reaches the end of the
-// sub-block (or of the draws), so a round resolves any number of rejections.  Every accepted lane
-// then stores its draw's value into out[t] for t < krec.  Advances r past the consumed words.
-__device__ __forceinline__ void wave_draws(WaveRng& r, int n, int dstep, int count, int krec, lu32* out) {
-    const int lane = threadIdx.x;
-    int done = 0;
-    while (done < count) {
-        if (r.pos >= WR_BLOCK) wave_rng_load(r, st_advance(r.st, WR_BLOCK));
-        const int q = r.pos >> 6, base = q << 6, start = r.pos - base;
-        const uint32_t w = wr_sub(r, q);
-        const int idx = lane - start;
-        unsigned long long rmask = 0;
-        int c = start, end = start;
-        for (int hb = 0; c < 64; hb += WR_H) {
-            unsigned long long rej[WR_H], live[WR_H];
-#pragma unroll
-            for (int u = 0; u < WR_H; u++) {
-                const int h = hb + u;
-                int t = done + idx - h;  // draw this word serves under hypothesis h
-                bool lv = idx >= h && t < count;
-                int b = n - t * dstep;
-                int kk = 32 - __clz(max(b, 1));
-                bool rj = lv && (w >> (32 - kk)) >= (uint32_t)b;
-                rej[u] = __ballot(rj);
-                live[u] = __ballot(lv);
-            }
-            // walk the chain of rejections through this batch
-            bool resolved = false;
-#pragma unroll
-            for (int u = 0; u < WR_H; u++) {
-                const unsigned long long from = ~0ull << c;  // c < 64 here
-                unsigned long long m = rej[u] & from, lm = live[u] & from;
-                if (!m) {  // every live word from c on is accepted
-                    end = lm ? 64 - __clzll((long long)lm) : c;
-                    resolved = true;
-                    break;
-                }
-                int p = __ffsll((long long)m) - 1;
-                rmask |= 1ull << p;
-                c = p + 1;
-                end = c;
-                if (c >= 64) break;
-            }
-            if (resolved) break;
-        }
-        // accepted lanes in [start, end) store the value of the draw they served
-        const bool mine = lane >= start && lane < end && !((rmask >> lane) & 1ull);
-        const int hl = __popcll(rmask & ((1ull << lane) - 1ull));
-        const int t = done + idx - hl;
-        if (mine && t < krec) {
-            int b = n - t * dstep;
-            out[t] = w >> (32 - (32 - __clz(b)));
-        }
-        done += (end - start) - __popcll(rmask);
-        r.pos = base + end;
-    }
-    wave_sync();
-}
+#include "zs_wave_rng.hpp"
 
 struct ResetLds {
     lu32* bm;       // occupancy bitmap [DW]
@@ -207,7 +66,7 @@ __device__ __forceinline__ int wave_spawn(const Dev& d, const ResetLds& L, WaveR
     // random.shuffle: for i = n-1 .. 1, j = _randbelow(i+1), swap.  Iterations i >= n-k decide the
     // k popped cells; the rest only consume their draws.
     const int ndraw = max(n - 1, 0), nswap = min(k, ndraw);
-    wave_draws(r, n, 1, ndraw, nswap, L.jbuf);
+    wave_draws(r, n, 1, ndraw, nswap, [&](int t, uint32_t v) { L.jbuf[t] = v; });
     if (lane == 0)
         for (int t = 0; t < nswap; t++) {
             int i = n - 1 - t, j = (int)L.jbuf[t];
@@ -259,7 +118,7 @@ __device__ __forceinline__ void reset_env_wave(const Dev& d, const ResetLds& L, 
     r.lr = L.tw;
     const uint32_t st_in = d.rngst[e];
     wave_rng_stage(r, st_in);
-    wave_rng_load(r, st_in);
+    rng_block_load(r, st_in);
     RST(1);
     // players: Player() picks a random weapon unless its module gives one (things.py:113-116);
     // agents: WeaponFactory.create_player_weapon (weapons.py:28-45).  Each random pick is one
@@ -267,7 +126,7 @@ __device__ __forceinline__ void reset_env_wave(const Dev& d, const ResetLds& L, 
     int nrw = 0;
     for (int p = 0; p < P; p++) nrw += d.bot_types[p] != ZS_BOT_TERMINATOR && d.bot_types[p] != ZS_BOT_SNIPER;
     for (int a = 0; a < A; a++) nrw += d.agent_weapons[a] == ZS_WEAPON_RANDOM;
-    if (nrw) wave_draws(r, 5, 0, nrw, nrw, L.jbuf);
+    if (nrw) wave_draws(r, 5, 0, nrw, nrw, [&](int t, uint32_t v) { L.jbuf[t] = v; });
     if (lane == 0) {
         int t = 0;
         for (int p = 0; p < P; p++) {
@@ -310,7 +169,7 @@ __device__ __forceinline__ void reset_env_wave(const Dev& d, const ResetLds& L, 
         int nz = d.initial_zombies;
         for (int b0 = 0; b0 < nz; b0 += d.E + 8) {  // randint(50, 100) = 50 + _randbelow(51) each
             int cnt = min(nz - b0, d.E + 8);
-            wave_draws(r, 51, 0, cnt, cnt, L.jbuf);
+            wave_draws(r, 51, 0, cnt, cnt, [&](int t, uint32_t v) { L.jbuf[t] = v; });
             for (int i = lane; i < cnt; i += 64) {
                 L.llife[A + P + b0 + i] = 50 + (int)L.jbuf[i];
                 L.lweap[A + P + b0 + i] = ZS_WEAPON_CLAWS;

@@ -1,0 +1,156 @@
+// zs_wave_rng.hpp — one env's CPython MT19937 stream consumed by a whole wave.
+//
+// Long runs of draws (the Fisher-Yates passes of World.spawn_in_random, core.py:40-66, whose
+// candidate lists reach thousands of cells) are resolved 64 words at a time: the stream is held
+// one word per lane, every _randbelow (random.py:239-249) rejection chain is walked with ballots,
+// and a block of 624 words that runs out is twisted cooperatively.  Two stream holders:
+//   WaveRng (k_reset): the env's ring staged in LDS for the whole reset, flushed at the end;
+//   GRng    (k_tick's cooperative respawn): the ring read from HBM (L1-bypassing loads) and
+//           twisted in registers (no LDS: the tick's LDS is its occupancy).
+#pragma once
+#include "zs_device.hpp"
+
+#define WR_Q 4               // words per lane held in registers
+#define WR_BLOCK (64 * WR_Q)  // words per register block
+
+struct WaveRng {
+    uint32_t st;          // ring state of the register block's word 0 (uniform)
+    int pos;              // next unconsumed word within the block (uniform, 0..WR_BLOCK)
+    uint32_t word[WR_Q];  // word[q] = tempered stream word q*64 + lane of the block
+    uint32_t* ring;       // the env's ring in HBM (read once at the start, dirty slots written at the end)
+    lu32* lr;             // its LDS copy, 2 x 624 words: every draw and twist of the reset works here
+    int dirty;            // bit s: LDS slot s was twisted and must be written back
+};
+
+// stage the env's ring into LDS: the current slot, and the next one when it is already twisted
+__device__ __forceinline__ void wave_rng_stage(WaveRng& r, uint32_t st) {
+    const uint32_t slot = (st >> 10) & 1u, ready = (st >> 11) & 1u;
+    const int lane = threadIdx.x;
+    stage_in(r.ring + slot * ZS_MT_N, ZS_MT_N, lane, 64, r.lr + slot * ZS_MT_N, [](int k) { return k; });
+    if (ready)
+        stage_in(r.ring + (slot ^ 1u) * ZS_MT_N, ZS_MT_N, lane, 64, r.lr + (slot ^ 1u) * ZS_MT_N, [](int k) { return k; });
+    r.dirty = 0;
+    wave_sync();
+}
+
+// next block of the stream (LDS slot ^ 1) from the current one (_randommodule.c genrand_uint32's
+// twist), cooperatively in three dependency phases
+__device__ __forceinline__ void wave_twist(WaveRng& r, uint32_t slot) {
+    const int lane = threadIdx.x;
+    const lu32* src = r.lr + slot * ZS_MT_N;
+    lu32* nw = r.lr + (slot ^ 1u) * ZS_MT_N;
+    for (int k = lane; k < ZS_MT_N - ZS_MT_M; k += 64) nw[k] = mt_f(src[k], src[k + 1], src[k + ZS_MT_M]);
+    wave_sync();
+    for (int k = (ZS_MT_N - ZS_MT_M) + lane; k < 2 * (ZS_MT_N - ZS_MT_M); k += 64)
+        nw[k] = mt_f(src[k], src[k + 1], nw[k + ZS_MT_M - ZS_MT_N]);
+    wave_sync();
+    for (int k = 2 * (ZS_MT_N - ZS_MT_M) + lane; k < ZS_MT_N; k += 64)
+        nw[k] = mt_f(src[k], k + 1 < ZS_MT_N ? src[k + 1] : nw[0], nw[k + ZS_MT_M - ZS_MT_N]);
+    wave_sync();
+    r.dirty |= 1 << (slot ^ 1u);
+}
+
+// write the twisted slots back to the env's ring in HBM (no wait: the next reader is a later launch)
+__device__ __forceinline__ void wave_rng_flush(const WaveRng& r) {
+    const int lane = threadIdx.x;
+    for (int sl = 0; sl < 2; sl++)
+        if ((r.dirty >> sl) & 1)
+            for (int k = lane; k < ZS_MT_N; k += 64) r.ring[sl * ZS_MT_N + k] = r.lr[sl * ZS_MT_N + k];
+}
+
+// load the WR_BLOCK words that start at ring state st (twisting the next block first if needed)
+__device__ __forceinline__ void rng_block_load(WaveRng& r, uint32_t st) {
+    uint32_t off = st & 1023u, slot = (st >> 10) & 1u, ready = (st >> 11) & 1u;
+    if (off >= ZS_MT_N) {
+        if (!ready) wave_twist(r, slot);
+        slot ^= 1u;
+        off = 0;
+        ready = 0;
+    }
+    if (off + WR_BLOCK > ZS_MT_N && !ready) {
+        wave_twist(r, slot);
+        ready = 1;
+    }
+#pragma unroll
+    for (int q = 0; q < WR_Q; q++) {
+        uint32_t p = off + q * 64 + threadIdx.x;
+        r.word[q] = mt_temper(p < ZS_MT_N ? r.lr[slot * ZS_MT_N + p] : r.lr[(slot ^ 1u) * ZS_MT_N + p - ZS_MT_N]);
+    }
+    r.st = st_pack(off, slot, ready);
+    r.pos = 0;
+}
+
+template <class R>
+__device__ __forceinline__ uint32_t wr_sub(const R& r, int q) {
+    return q == 0 ? r.word[0] : q == 1 ? r.word[1] : q == 2 ? r.word[2] : r.word[3];
+}
+
+#define WR_H 4  // rejection hypotheses evaluated per batch (one ballot each)
+
+// `count` consecutive draws _randbelow(b_t), b_t = n - t * dstep (dstep 0: a fixed bound; 1: the
+// decreasing bounds of a Fisher-Yates pass), all in wave-uniform control flow.  Draw t consumes
+// words until one word w gives (w >> (32 - bitlen(b_t))) < b_t (random.py:239-249).
+//
+// One round per 64-word sub-block: lane l evaluates its word under each hypothesis "h words of
+// this round before me were rejected" (then it serves draw t = idx - h, idx = l - start), one
+// ballot per hypothesis, WR_H hypotheses per batch; the scalar unit walks the chain of first
+// rejections h = 0, 1, 2, ... and evaluates further batches until the chain reaches the end of the
+// sub-block (or of the draws), so a round resolves any number of rejections.  Every accepted lane
+// then hands its draw's value to put(t, value) for t < krec.  Advances r past the consumed words.
+template <class R, class Put>
+__device__ __forceinline__ void wave_draws(R& r, int n, int dstep, int count, int krec, Put put) {
+    const int lane = threadIdx.x;
+    int done = 0;
+    while (done < count) {
+        if (r.pos >= WR_BLOCK) rng_block_load(r, st_advance(r.st, WR_BLOCK));
+        const int q = r.pos >> 6, base = q << 6, start = r.pos - base;
+        const uint32_t w = wr_sub(r, q);
+        const int idx = lane - start;
+        unsigned long long rmask = 0;
+        int c = start, end = start;
+        for (int hb = 0; c < 64; hb += WR_H) {
+            unsigned long long rej[WR_H], live[WR_H];
+#pragma unroll
+            for (int u = 0; u < WR_H; u++) {
+                const int h = hb + u;
+                int t = done + idx - h;  // draw this word serves under hypothesis h
+                bool lv = idx >= h && t < count;
+                int b = n - t * dstep;
+                int kk = 32 - __clz(max(b, 1));
+                bool rj = lv && (w >> (32 - kk)) >= (uint32_t)b;
+                rej[u] = __ballot(rj);
+                live[u] = __ballot(lv);
+            }
+            // walk the chain of rejections through this batch
+            bool resolved = false;
+#pragma unroll
+            for (int u = 0; u < WR_H; u++) {
+                const unsigned long long from = ~0ull << c;  // c < 64 here
+                unsigned long long m = rej[u] & from, lm = live[u] & from;
+                if (!m) {  // every live word from c on is accepted
+                    end = lm ? 64 - __clzll((long long)lm) : c;
+                    resolved = true;
+                    break;
+                }
+                int p = __ffsll((long long)m) - 1;
+                rmask |= 1ull << p;
+                c = p + 1;
+                end = c;
+                if (c >= 64) break;
+            }
+            if (resolved) break;
+        }
+        // accepted lanes in [start, end) store the value of the draw they served
+        const bool mine = lane >= start && lane < end && !((rmask >> lane) & 1ull);
+        const int hl = __popcll(rmask & ((1ull << lane) - 1ull));
+        const int t = done + idx - hl;
+        if (mine && t < krec) {
+            int b = n - t * dstep;
+            put(t, w >> (32 - (32 - __clz(b))));
+        }
+        done += (end - start) - __popcll(rmask);
+        r.pos = base + end;
+    }
+    wave_sync();
+}
+

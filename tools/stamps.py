@@ -25,8 +25,12 @@ def main():
     from libzombsole_amd.engine import Engine
     n_envs = int(os.environ.get("N_ENVS", "8192"))
     for G in [int(g) for g in os.environ.get("GS", "1,2,4,8,16").split(",")]:
-        b = _abi.multi_env_config(n_envs, "extermination", [], "bridge64", ["0", "1"], initial_zombies=10,
-                                  minimum_zombies=0, max_episode_steps=1000, lanes_per_env=G)
+        A = int(os.environ.get("AGENTS", "2"))
+        b = _abi.multi_env_config(n_envs, os.environ.get("RULES", "extermination"), [],
+                                  os.environ.get("MAP", "bridge64"), [str(i) for i in range(A)],
+                                  initial_zombies=int(os.environ.get("ZOMBIES", "10")),
+                                  minimum_zombies=int(os.environ.get("MINZ", "0")), max_episode_steps=1000,
+                                  lanes_per_env=G)
         eng = Engine(b)
         eng.seed(list(range(n_envs)))
         eng.reset()
