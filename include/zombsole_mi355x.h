@@ -205,9 +205,10 @@ int zs_set_rng(zs_handle* h, int32_t env, const uint32_t* state_host, void* stre
  * launch is bracketed by HIP events on its stream.  zs_profile_read synchronizes
  * and returns out[0] = total k_tick ms, out[1] = k_tick launches, out[2] = total
  * k_obs ms, out[3] = k_obs launches, out[4] = total k_reset ms, out[5] = k_reset
- * launches, then clears the record. */
+ * launches, out[6] = total k_respawn ms, out[7] = k_respawn launches (deferred zombie
+ * respawns), then clears the record. */
 int zs_profile(zs_handle* h, int32_t enable);
-int zs_profile_read(zs_handle* h, double out[6]);
+int zs_profile_read(zs_handle* h, double out[8]);
 /* Diagnostic builds compiled with -DZS_STAMPS only (the product .so returns ZS_ESTATE):
  * per-phase k_tick cycle sums / maxima over all workgroup launches since the last call. */
 int zs_debug_stamps(zs_handle* h, uint64_t* sum_out, uint64_t* max_out, int32_t n);

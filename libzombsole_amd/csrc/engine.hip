@@ -270,7 +270,7 @@ struct zs_handle {
     // diagnostics: HIP events bracketing every k_tick / k_obs launch on its stream
     int prof = 0;
     std::vector<hipEvent_t> ev_pool;
-    std::vector<std::pair<int, int>> ev_tick, ev_obs, ev_reset;  // (start, end) indices into ev_pool
+    std::vector<std::pair<int, int>> ev_tick, ev_obs, ev_reset, ev_respawn;  // (start, end) indices into ev_pool
     size_t ev_next = 0;
 };
 
@@ -454,6 +454,13 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
     d.initial_zombies = cfg->initial_zombies;
     d.minimum_zombies = cfg->minimum_zombies;
     d.flags = cfg->flags;
+    // zombie respawn as wave work after the tick (k_respawn) when its shuffle is long: the tick's
+    // leader would draw one word per candidate serially.  ZS_DEFER_RESPAWN=0/1 forces either.
+    {
+        const int cands = m.n_zombie_spawns ? m.n_zombie_spawns : d.W * d.H;
+        const char* dr = getenv("ZS_DEFER_RESPAWN");
+        d.defer_respawn = d.minimum_zombies > 0 && (dr ? atoi(dr) != 0 : cands > 64);
+    }
 
     // static tables
     std::vector<int16_t> cellmap((size_t)d.W * d.H, -1);
@@ -580,6 +587,8 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
     TRY(dalloc(h, &h->d_rlist[0], N));
     TRY(dalloc(h, &h->d_rlist[1], N));
     TRY(dalloc(h, &h->d_rcount, 2));
+    TRY(dalloc(h, &d.resp_list, N));
+    TRY(dalloc(h, &d.resp_count, 1));
     {
         // observation images: k_obs (four envs per workgroup when their images fit 64 KiB, else one;
         // window map and staged HP while one image fits 32 KiB) and, when the step launch writes the
@@ -621,6 +630,7 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
         d.obsl = L;
         d.fobs = L.bytes + 4 * d.obs_stat <= 16 * 1024 && !getenv_off("ZS_FOBS");
         if (h->obs_pipe && !(getenv("ZS_FOBS") && atoi(getenv("ZS_FOBS")) != 0)) d.fobs = 0;
+        if (d.defer_respawn) d.fobs = 0;  // the observations must see k_respawn's zombies
     }
     // Fused step launch (reset work + tick in one) when the whole launch is resident at once: then
     // the step is one latency-bound round and the reset work hides under the ticks (measured: 8192
@@ -653,7 +663,7 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
     {
         const char* ck = getenv("ZS_CHUNKS");
         h->chunks = 1;
-        if (ck && !h->fused && !d.fobs && h->obs_pipe) h->chunks = std::max(1, std::min(8, atoi(ck)));
+        if (ck && !h->fused && !d.fobs && h->obs_pipe && !d.defer_respawn) h->chunks = std::max(1, std::min(8, atoi(ck)));
         if (d.N < 64 * h->chunks) h->chunks = 1;
         if (h->chunks > 1) {
             if (hipStreamCreateWithFlags(&h->s_obs, hipStreamNonBlocking) != hipSuccess) h->chunks = 1;
@@ -669,18 +679,20 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
                         hipEventCreateWithFlags(&h->ev_rjoin, hipEventDisableTiming) == hipSuccess;
     }
     if (h->reset_lds > 64 * 1024 &&
-        hipFuncSetAttribute((const void*)k_reset, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->reset_lds) !=
-            hipSuccess) {
+        (hipFuncSetAttribute((const void*)k_reset, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->reset_lds) !=
+             hipSuccess ||
+         hipFuncSetAttribute((const void*)k_respawn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->reset_lds) !=
+             hipSuccess)) {
         free_all(h);
         delete h;
         return fail(ZS_EHIP, "cannot raise k_reset's dynamic LDS limit");
     }
     if (getenv("ZS_VERBOSE"))
         fprintf(stderr, "zs_create: N=%d E=%d G=%d step_lds=%zu resident=%d reset_lds=%zu rw_cap=%d cand_cap=%d "
-                        "lists_cap=%d fused=%d fobs=%d obs_img=%d k_obs_img=%d x%d pipe=%d pipe_wgs=%d chunks=%d reset_side=%d\n",
+                        "lists_cap=%d fused=%d fobs=%d obs_img=%d k_obs_img=%d x%d pipe=%d pipe_wgs=%d chunks=%d reset_side=%d defer_respawn=%d\n",
                 d.N, d.E, h->G, h->lds, h->resident, h->reset_lds, d.rw_cap, d.cand_cap, d.lists_cap, h->fused,
                 d.fobs, d.obsl.bytes, h->obs_l.bytes, h->obs_wpg, h->obs_pipe, h->obs_pipe_wgs, h->chunks,
-                h->reset_side);
+                h->reset_side, d.defer_respawn);
     if (d.O > 0) {
         size_t n = N * d.O;
         hipLaunchKernelGGL(k_init_obstacles, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, d);
@@ -843,6 +855,21 @@ static int launch_reset(zs_handle* h, int list_mode, const uint8_t* mask, void* 
     return ZS_OK;
 }
 
+// the respawns the tick just deferred (k_respawn drains d.resp_list; count zeroed before the tick)
+static int launch_respawn(zs_handle* h, hipStream_t s) {
+    const Dev& d = h->d;
+    static const int grid = getenv("ZS_RESPAWN_GRID") ? std::max(1, atoi(getenv("ZS_RESPAWN_GRID"))) : 2048;
+    int i0 = -1, i1 = -1;
+    if (h->prof) HIPCHK(hipEventRecord(prof_event(h, &i0), s));
+    hipLaunchKernelGGL(k_respawn, dim3((unsigned)std::min(d.N, grid)), dim3(64), h->reset_lds, s, d);
+    HIPCHK(hipGetLastError());
+    if (h->prof) {
+        HIPCHK(hipEventRecord(prof_event(h, &i1), s));
+        h->ev_respawn.push_back({i0, i1});
+    }
+    return ZS_OK;
+}
+
 extern "C" int zs_reset(zs_handle* h, const uint8_t* env_mask_dev, void* obs_dev, void* stream) {
     if (!h) return fail(ZS_EINVAL, "null handle");
     hipStream_t s = (hipStream_t)stream;
@@ -906,6 +933,7 @@ extern "C" int zs_step(zs_handle* h, const int32_t* actions_dev, void* obs_dev, 
     }
     // 2) tick every other env; envs that end now are queued on list[q] for the next call
     HIPCHK(hipMemsetAsync(h->d_rcount + q, 0, sizeof(int), s));
+    if (h->d.defer_respawn) HIPCHK(hipMemsetAsync(h->d.resp_count, 0, sizeof(int), s));
     const int K = (!h->fused && !h->d.fobs && obs_dev) ? h->chunks : 1;
     if (K > 1) {
         if (side) HIPCHK(hipStreamWaitEvent(s, h->ev_rjoin, 0));
@@ -931,6 +959,10 @@ extern "C" int zs_step(zs_handle* h, const int32_t* actions_dev, void* obs_dev, 
                      h->d_rcount + q, obs_dev, s);
     if (rc) return rc;
     h->rpar = q;
+    if (h->d.defer_respawn) {
+        rc = launch_respawn(h, s);
+        if (rc) return rc;
+    }
     // join the reset work, then 3) observations of every env (already written by the step launch
     // when fobs)
     if (side) HIPCHK(hipStreamWaitEvent(s, h->ev_rjoin, 0));
@@ -1034,6 +1066,7 @@ extern "C" int zs_profile(zs_handle* h, int32_t enable) {
     h->ev_tick.clear();
     h->ev_obs.clear();
     h->ev_reset.clear();
+    h->ev_respawn.clear();
     h->ev_next = 0;
     return ZS_OK;
 }
@@ -1041,9 +1074,9 @@ extern "C" int zs_profile(zs_handle* h, int32_t enable) {
 extern "C" int zs_profile_read(zs_handle* h, double* out) {
     if (!h || !out) return fail(ZS_EINVAL, "null argument");
     HIPCHK(hipSetDevice(h->device));
-    double tot[3] = {0.0, 0.0, 0.0};
-    std::vector<std::pair<int, int>>* lists[3] = {&h->ev_tick, &h->ev_obs, &h->ev_reset};
-    for (int k = 0; k < 3; k++)
+    double tot[4] = {0.0, 0.0, 0.0, 0.0};
+    std::vector<std::pair<int, int>>* lists[4] = {&h->ev_tick, &h->ev_obs, &h->ev_reset, &h->ev_respawn};
+    for (int k = 0; k < 4; k++)
         for (auto& pr : *lists[k]) {
             HIPCHK(hipEventSynchronize(h->ev_pool[pr.second]));
             float ms = 0.f;
@@ -1056,9 +1089,12 @@ extern "C" int zs_profile_read(zs_handle* h, double* out) {
     out[3] = (double)h->ev_obs.size();
     out[4] = tot[2];
     out[5] = (double)h->ev_reset.size();
+    out[6] = tot[3];
+    out[7] = (double)h->ev_respawn.size();
     h->ev_tick.clear();
     h->ev_obs.clear();
     h->ev_reset.clear();
+    h->ev_respawn.clear();
     h->ev_next = 0;
     return ZS_OK;
 }

@@ -80,6 +80,7 @@ struct Dev {
     int lists_cap;   // static spawn-list entries staged in LDS per workgroup (0 = read from global)
     int rlists_cap;  // the same for the reset work (k_reset has its own LDS budget; = lists_cap when fused)
     int fobs;        // observations are written by the step launch itself (tick and reset work)
+    int defer_respawn;  // zombie respawn left to k_respawn (wave per env) instead of the tick's leader
     ObsLayout obsl;  // one env's observation image (zs_obs.hpp)
     int obs_stat;    // static observation tables staged beside the image (4 * DW words), 0 = none
     int rules, reward_mode, obs_scope, obs_enc, obs_w, obs_dtype, max_steps;
@@ -118,6 +119,8 @@ struct Dev {
     uint32_t* rngst;
     uint64_t* seeds;
     int32_t* cand;
+    int* resp_list;   // envs whose respawn the tick deferred to k_respawn [N]
+    int* resp_count;
 };
 
 __device__ __forceinline__ int32_t pack_xy(int x, int y) { return (int32_t)((uint32_t)(x & 0xffff) | ((uint32_t)y << 16)); }

@@ -91,6 +91,18 @@ __device__ __forceinline__ int wave_spawn(const Dev& d, const ResetLds& L, WaveR
     return placed;
 }
 
+// end of a wave's use of the stream: the next block twisted (k_tick's window needs it ready),
+// twisted slots written back; returns the stream state to store
+__device__ __forceinline__ uint32_t wave_rng_finish(WaveRng& r) {
+    uint32_t stf = st_advance(r.st, r.pos);
+    if (!((stf >> 11) & 1u)) {
+        wave_twist(r, (stf >> 10) & 1u);
+        stf |= 1u << 11;
+    }
+    wave_rng_flush(r);
+    return stf;
+}
+
 __device__ __forceinline__ void reset_env_wave(const Dev& d, const ResetLds& L, int e, int list_mode, int* err_out) {
     const int lane = threadIdx.x, N = d.N, E = d.E, A = d.A, P = d.P;
     RST_DECL
@@ -184,13 +196,7 @@ __device__ __forceinline__ void reset_env_wave(const Dev& d, const ResetLds& L, 
         atomicMax(err_out, rc);
     }
     RST(6);
-    // the stream must hold its next block for k_tick's window
-    uint32_t stf = st_advance(r.st, r.pos);
-    if (!((stf >> 11) & 1u)) {
-        wave_twist(r, (stf >> 10) & 1u);
-        stf |= 1u << 11;
-    }
-    wave_rng_flush(r);
+    const uint32_t stf = wave_rng_finish(r);
     // write the new world back
     for (int s = lane; s < E; s += 64) {
         d.pos[(size_t)s * N + e] = L.lpos[s];
@@ -222,14 +228,8 @@ __device__ __forceinline__ void reset_env_wave(const Dev& d, const ResetLds& L, 
     RST(7);
 }
 
-// The reset work of workgroup `wg` of `nwg`.  list_mode: envs list[0..*count) (next-step
-// autoreset; the list holds exactly the pending envs, see zs_reset's list filter).  Otherwise
-// every env with mask[e] (all if mask == NULL).
-__device__ __forceinline__ void reset_role(const Dev& d, int list_mode, const int* list, const int* count,
-                                           const uint8_t* mask, int* err_out, int wg, int nwg, void* obs_out) {
-    extern __shared__ __align__(16) uint8_t smem[];
-    const int n = list_mode ? *count : d.N;
-    if (wg >= n) return;
+// the reset work's LDS image (reset_lds_bytes), the static spawn lists staged when they fit
+__device__ __forceinline__ ResetLds reset_lds_carve(const Dev& d, uint8_t* smem) {
     ResetLds L;
     int o = 0;
     L.bm = (lu32*)(smem + o);
@@ -257,6 +257,18 @@ __device__ __forceinline__ void reset_role(const Dev& d, int list_mode, const in
     if (d.rlists_cap)
         for (int i = threadIdx.x; i < d.nps + d.nzs; i += 64) L.lists[i] = i < d.nps ? d.pspawn[i] : d.zspawn[i - d.nps];
     wave_sync();
+    return L;
+}
+
+// The reset work of workgroup `wg` of `nwg`.  list_mode: envs list[0..*count) (next-step
+// autoreset; the list holds exactly the pending envs, see zs_reset's list filter).  Otherwise
+// every env with mask[e] (all if mask == NULL).
+__device__ __forceinline__ void reset_role(const Dev& d, int list_mode, const int* list, const int* count,
+                                           const uint8_t* mask, int* err_out, int wg, int nwg, void* obs_out) {
+    extern __shared__ __align__(16) uint8_t smem[];
+    const int n = list_mode ? *count : d.N;
+    if (wg >= n) return;
+    const ResetLds L = reset_lds_carve(d, smem);
     for (int idx = wg; idx < n; idx += nwg) {
         int e = list_mode ? list[idx] : idx;
         if (!list_mode && mask && !mask[e]) continue;
@@ -281,6 +293,77 @@ __device__ __forceinline__ void reset_role(const Dev& d, int list_mode, const in
 __global__ void __launch_bounds__(64, ZS_STEP_WAVES) k_reset(Dev d, int list_mode, const int* list, const int* count,
                                               const uint8_t* mask, int* err_out, void* obs_out) {
     reset_role(d, list_mode, list, count, mask, err_out, blockIdx.x, gridDim.x, obs_out);
+}
+
+// ---------------------------------------------------------------------------
+// k_respawn: Game.spawn_zombies_to_maintain_minimum (game.py:196-201) for the envs whose tick
+// deferred it (d.defer_respawn: long candidate lists, e.g. city128's 439 zombie spawns or every
+// cell of city_for_safehouse).  One wave per env continues the env's stream where the tick left
+// it: randint(50, 100) per new Zombie (things.py:61-68), then World.spawn_in_random's shuffle
+// (core.py:40-66) as wave work (wave_spawn), new zombies appended to the dict order.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void respawn_env_wave(const Dev& d, const ResetLds& L, int e) {
+    const int lane = threadIdx.x, N = d.N, E = d.E, Z0 = d.A + d.P;
+    for (int w = lane; w < d.DW; w += 64) L.bm[w] = d.occ_bits[(size_t)e * d.DW + w];
+    for (int s = lane; s < E; s += 64) {
+        L.lpos[s] = d.pos[(size_t)s * N + e];
+        L.llife[s] = d.life[(size_t)s * N + e];
+        L.lweap[s] = d.weapon[(size_t)s * N + e];
+        L.lpres[s] = d.present[(size_t)s * N + e];
+        L.lorder[s] = d.order[(size_t)s * N + e];
+    }
+    WaveRng r;
+    r.ring = d.ring + (size_t)e * ZS_RING_WORDS;
+    r.lr = L.tw;
+    const uint32_t st_in = d.rngst[e];
+    wave_rng_stage(r, st_in);
+    rng_block_load(r, st_in);
+    // Game.spawn_zombies(count): the deficit's Zombie()s go into the free zombie slots, lowest first
+    int nz = 0;
+    for (int b = Z0; b < E; b += 64) nz += __popcll(__ballot(b + lane < E && L.lpres[b + lane]));
+    const int k = max(d.minimum_zombies - nz, 0);
+    int taken = 0;
+    for (int b = Z0; b < E && taken < k; b += 64) {
+        const int s = b + lane;
+        const bool fr = s < E && !L.lpres[s];
+        const unsigned long long m = __ballot(fr);
+        const int rk = taken + __popcll(m & ((1ull << lane) - 1ull));
+        if (fr && rk < k) L.lslots[rk] = (uint8_t)s;
+        taken += __popcll(m);
+    }
+    wave_sync();
+    wave_draws(r, 51, 0, k, k, [&](int t, uint32_t v) {
+        const int s = L.lslots[t];
+        L.llife[s] = 50 + (int)v;
+        L.lweap[s] = ZS_WEAPON_CLAWS;
+    });
+    const int n0 = d.scal[S_NORDER * N + e];
+    int n_order = n0, serial = d.scal[S_SERIAL * N + e];
+    const int placed = wave_spawn(d, L, r, e, k, 1, d.nzs, n_order, serial);
+    const uint32_t stf = wave_rng_finish(r);
+    for (int m = lane; m < k; m += 64) {  // the new zombies (dropped ones keep their drawn life)
+        const int s = L.lslots[m];
+        d.pos[(size_t)s * N + e] = L.lpos[s];
+        d.life[(size_t)s * N + e] = L.llife[s];
+        d.weapon[(size_t)s * N + e] = L.lweap[s];
+        d.present[(size_t)s * N + e] = L.lpres[s];
+    }
+    for (int m = n0 + lane; m < n0 + placed; m += 64) d.order[(size_t)m * N + e] = L.lorder[m];
+    for (int w = lane; w < d.DW; w += 64) d.occ_bits[(size_t)e * d.DW + w] = L.bm[w];
+    if (lane == 0) {
+        d.scal[S_NORDER * N + e] = n_order;
+        d.scal[S_SERIAL * N + e] = serial;
+        d.rngst[e] = stf;
+    }
+    wave_sync();
+}
+
+__global__ void __launch_bounds__(64, ZS_STEP_WAVES) k_respawn(Dev d) {
+    extern __shared__ __align__(16) uint8_t smem[];
+    const int n = *d.resp_count;
+    if ((int)blockIdx.x >= n) return;
+    const ResetLds L = reset_lds_carve(d, smem);
+    for (int idx = blockIdx.x; idx < n; idx += gridDim.x) respawn_env_wave(d, L, d.resp_list[idx]);
 }
 
 // Drop the envs a mask-mode reset just rebuilt from the pending list (src -> dst, dst count

@@ -156,6 +156,7 @@ struct Grp {
     uint32_t st0;  // ring state at the start of the LDS window
     int wpos, wlen;
     int n_order, t, deaths, zd, epsteps, prevzd, serial, odirty;
+    int respawn;  // the zombie respawn of this step is deferred to k_respawn
 };
 
 #define IX(c, k) ((k) * (c).ne + (c).g)
@@ -370,6 +371,22 @@ __device__ __forceinline__ void spawn_zombies(const Dev& d, Grp& c, int count) {
         LW(c, s) = ZS_WEAPON_CLAWS;
     }
     spawn_in_random(d, c, k, 1, d.nzs, 0);
+}
+
+// a free cell among the zombie spawn candidates (every cell when the map lists none)
+__device__ __forceinline__ int any_free_spawn(const Dev& d, const Grp& c) {
+    const int total = d.nzs ? d.nzs : d.W * d.H;
+    for (int i = 0; i < total; i++) {
+        int cell;
+        if (d.nzs) {
+            int32_t p = spawn_at(d, c, 1, i);
+            cell = unpack_y(p) * d.W + unpack_x(p);
+        } else {
+            cell = i;
+        }
+        if (!bm_test(c, cell)) return 1;
+    }
+    return 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -589,11 +606,12 @@ __device__ __forceinline__ void decide(const Dev& d, Grp& c, int s, const int32_
 // ---------------------------------------------------------------------------
 // rules (rules/{extermination,survival,safehouse,evacuation}.py)
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void rules_check(const Dev& d, const Grp& c, int& ended, int& won) {
+// za0: a zombie is alive beyond the entity table (one a deferred respawn will place)
+__device__ __forceinline__ void rules_check(const Dev& d, const Grp& c, int& ended, int& won, int za0 = 0) {
     int pa = 0;  // Rules.players_alive (rules.py:6-11)
     for (int s = 0; s < d.A + d.P; s++) pa |= LL(c, s) > 0;
     if (d.rules == ZS_RULES_EXTERMINATION) {
-        int za = 0;
+        int za = za0;
         for (int s = d.A + d.P; s < d.E; s++) za |= LPR(c, s) && LL(c, s) > 0;
         ended = !pa || !za;
         won = pa;
@@ -777,15 +795,26 @@ __device__ __forceinline__ void env_step_leader(const Dev& d, Grp& c, const int3
     }
     for (int a = 0; a < A; a++) MISC(c, MISC_N + a) = LL(c, a);
     c.prevzd = c.zd;
-    // spawn_zombies_to_maintain_minimum (game.py:196-201)
+    // spawn_zombies_to_maintain_minimum (game.py:196-201).  Deferred: the respawn is the step's
+    // last RNG consumer and nothing below reads the new zombies except Extermination's "any zombie
+    // alive", which only needs to know whether one more zombie gets placed (a free spawn cell).
+    int za0 = 0;
+    c.respawn = 0;
     {
         int nz = 0;
         for (int s = A + d.P; s < E; s++) nz += LPR(c, s);
-        if (nz < d.minimum_zombies) spawn_zombies(d, c, d.minimum_zombies - nz);
+        if (nz < d.minimum_zombies) {
+            if (d.defer_respawn) {
+                c.respawn = 1;
+                if (nz == 0 && d.rules == ZS_RULES_EXTERMINATION) za0 = any_free_spawn(d, c);
+            } else {
+                spawn_zombies(d, c, d.minimum_zombies - nz);
+            }
+        }
     }
     // rules and end-of-game reward (gym_env.py:130-141, gym/multiagent_env.py:143-162)
     int ended, won, tr = 0;
-    rules_check(d, c, ended, won);
+    rules_check(d, c, ended, won, za0);
     double end_reward = 0.0;
     if (ended) {
         end_reward = won ? 10.0 : -10.0;
@@ -1019,6 +1048,7 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
             needs_reset = 1;
             reset_list[atomicAdd(reset_count, 1)] = e;  // rebuilt by the next call's reset work
         }
+        if (c.respawn) d.resp_list[atomicAdd(d.resp_count, 1)] = e;  // k_respawn, after this launch
         if (reset_out) reset_out[e] = 0;
         MISC(c, MISC_T) = c.t;
         MISC(c, MISC_DEATHS) = c.deaths;

@@ -174,13 +174,13 @@ class Engine(object):
         self.L.zs_profile(self.h, 1 if enable else 0)
 
     def profile_read(self):
-        """Per-kernel totals: tick_ms/tick_n, obs_ms/obs_n, reset_ms/reset_n."""
-        out = (C.c_double * 6)()
+        """Per-kernel totals: tick_ms/tick_n, obs_ms/obs_n, reset_ms/reset_n, respawn_ms/respawn_n."""
+        out = (C.c_double * 8)()
         rc = self.L.zs_profile_read(self.h, out)
         if rc:
             _raise(self.L, rc, "zs_profile_read")
         return {"tick_ms": out[0], "tick_n": int(out[1]), "obs_ms": out[2], "obs_n": int(out[3]),
-                "reset_ms": out[4], "reset_n": int(out[5])}
+                "reset_ms": out[4], "reset_n": int(out[5]), "respawn_ms": out[6], "respawn_n": int(out[7])}
 
     def debug_stamps(self, n=5):
         """Per-phase k_tick cycle sums / maxima (diagnostic -DZS_STAMPS build only)."""

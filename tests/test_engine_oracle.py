@@ -142,3 +142,32 @@ def test_kernel_paths(path, monkeypatch):
                                                 observation_scope="world", observation_position_encoding="channels",
                                                 max_episode_steps=50),
                16, 60, check_state_every=30)
+
+
+# Zombie respawn in the tick's leader or deferred to k_respawn (wave per env): both bit-exact, on a
+# long candidate list (city128, 439 spawns), on every-cell candidates (city_for_safehouse) and on a
+# short list under Extermination, where a respawn decides whether the game ends (boxed: 1 zombie,
+# minimum 1).
+RESPAWN = {
+    "leader": {"ZS_DEFER_RESPAWN": "0"},
+    "deferred": {"ZS_DEFER_RESPAWN": "1"},
+    "deferred_fused": {"ZS_DEFER_RESPAWN": "1", "ZS_FUSED": "1"},
+    "deferred_unfused_serial_reset": {"ZS_DEFER_RESPAWN": "1", "ZS_FUSED": "0", "ZS_RESET_STREAM": "0"},
+}
+
+
+@pytest.mark.parametrize("path", sorted(RESPAWN))
+def test_respawn_paths(path, monkeypatch):
+    for k, v in RESPAWN[path].items():
+        monkeypatch.setenv(k, v)
+    run_parity(lambda n: _abi.single_env_config(n, "extermination", ["terminator"], "boxed", "0",
+                                                initial_zombies=1, minimum_zombies=1,
+                                                observation_scope="world", observation_position_encoding="channels",
+                                                agent_weapon="shotgun", max_episode_steps=60),
+               64, 100, stream="rich", check_state_every=20)
+    run_parity(lambda n: _abi.multi_env_config(n, "safehouse", [], "city128", ["0", "1", "2", "3"],
+                                               initial_zombies=50, minimum_zombies=50),
+               24, 40, check_state_every=20)
+    run_parity(lambda n: _abi.multi_env_config(n, "extermination", [], "city_for_safehouse", ["0", "1"],
+                                               initial_zombies=3, minimum_zombies=2, max_episode_steps=40),
+               32, 60, stream="rich", check_state_every=20)
