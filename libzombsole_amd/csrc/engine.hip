@@ -242,6 +242,8 @@ struct zs_handle {
     ObsLayout obs_l;  // k_obs per-wave LDS image
     int obs_wpg;      // k_obs waves (envs) per workgroup
     int obs_pipe = 0;      // k_obs_pipe<NOBS> usable (NOBS = 1, 2, 4), else 0
+    int obs_gather = 0;    // else k_obs_gather<NOBS> usable (NOBS = 1, 2, 4), else 0 (k_obs)
+    ObsLayout obs_gl;      // its per-wave image
     // step pipeline: the tick in `chunks` env ranges on the caller's stream, each range's observations
     // on s_obs as soon as its tick is done
     int chunks = 1;
@@ -624,6 +626,16 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
             h->obs_pipe_wgs = std::max(1, std::min(2, 160 * 1024 / (d.obs_stat * 4 + 4 * L.bytes)));
             if (getenv("ZS_OBS_WGS")) h->obs_pipe_wgs = std::max(1, std::min(32, atoi(getenv("ZS_OBS_WGS"))));
         }
+        // k_obs_gather when the store-stream kernel does not apply (e.g. city128's 3689 obstacles):
+        // window-only static words and HP instead of per-env staging.  ZS_OBS_GATHER=0 disables.
+        if (!h->obs_pipe && !world && d.obs_w == 21 && (nobs == 1 || nobs == 2 || nobs == 4) &&
+            !getenv_off("ZS_OBS_GATHER")) {
+            ObsLayout G = obs_layout(nobs, plane, d.E, d.DW, d.OW, d.O, true, false);
+            if (4 * G.bytes <= 64 * 1024) {
+                h->obs_gather = nobs;
+                h->obs_gl = G;
+            }
+        }
         // with the store-stream kernel available the observations are its job (measured faster than
         // writing them from the tick workgroups at both 8192 and 65536 envs); ZS_FOBS=1 forces them
         // into the step launch
@@ -689,9 +701,9 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
     }
     if (getenv("ZS_VERBOSE"))
         fprintf(stderr, "zs_create: N=%d E=%d G=%d step_lds=%zu resident=%d reset_lds=%zu rw_cap=%d cand_cap=%d "
-                        "lists_cap=%d fused=%d fobs=%d obs_img=%d k_obs_img=%d x%d pipe=%d pipe_wgs=%d chunks=%d reset_side=%d defer_respawn=%d\n",
+                        "lists_cap=%d fused=%d fobs=%d obs_img=%d k_obs_img=%d x%d pipe=%d gather=%d pipe_wgs=%d chunks=%d reset_side=%d defer_respawn=%d\n",
                 d.N, d.E, h->G, h->lds, h->resident, h->reset_lds, d.rw_cap, d.cand_cap, d.lists_cap, h->fused,
-                d.fobs, d.obsl.bytes, h->obs_l.bytes, h->obs_wpg, h->obs_pipe, h->obs_pipe_wgs, h->chunks,
+                d.fobs, d.obsl.bytes, h->obs_l.bytes, h->obs_wpg, h->obs_pipe, h->obs_gather, h->obs_pipe_wgs, h->chunks,
                 h->reset_side, d.defer_respawn);
     if (d.O > 0) {
         size_t n = N * d.O;
@@ -774,6 +786,31 @@ static int launch_obs(zs_handle* h, void* obs, const uint8_t* mask, hipStream_t 
         }
 #undef ZS_PIPE_T
 #undef ZS_PIPE
+        HIPCHK(hipGetLastError());
+        if (h->prof) {
+            HIPCHK(hipEventRecord(prof_event(h, &i1), s));
+            h->ev_obs.push_back({i0, i1});
+        }
+        return ZS_OK;
+    }
+    if (h->obs_gather) {  // one env per wave, four per workgroup, window-only fetches
+        const unsigned g = (unsigned)((d.N + 3) / 4);
+        const size_t lds = 4 * (size_t)h->obs_gl.bytes;
+#define ZS_GATH(TT, NB) \
+    hipLaunchKernelGGL((k_obs_gather<TT, NB>), dim3(g), dim3(256), lds, s, d, (TT*)obs, mask, h->obs_gl)
+#define ZS_GATH_T(TT)                         \
+    if (h->obs_gather == 1) ZS_GATH(TT, 1);     \
+    else if (h->obs_gather == 2) ZS_GATH(TT, 2); \
+    else ZS_GATH(TT, 4)
+        if (d.obs_dtype == ZS_DTYPE_I64) {
+            ZS_GATH_T(int64_t);
+        } else if (d.obs_dtype == ZS_DTYPE_I32) {
+            ZS_GATH_T(int32_t);
+        } else {
+            ZS_GATH_T(int16_t);
+        }
+#undef ZS_GATH_T
+#undef ZS_GATH
         HIPCHK(hipGetLastError());
         if (h->prof) {
             HIPCHK(hipEventRecord(prof_event(h, &i1), s));

@@ -439,3 +439,92 @@ __global__ void __launch_bounds__(256, ZS_OBS_PIPE_WAVES) k_obs_pipe(Dev d, T* o
         wave_sync();
     }
 }
+
+// ---------------------------------------------------------------------------
+// k_obs_gather: the registered shape (surroundings, width 21, NOBS observations per env) on maps
+// whose obstacle HP row is too large to stage per env (city128: 3689 obstacles, 14.7 KB, which
+// left k_obs one wave per CU slot).  Only the observed cells' data is fetched: per lane, the
+// static per-cell words of its NOBS x 7 window cells, then the HP of those cells' obstacles, each
+// batch issued as one group of loads before any store (one wait per batch, no global load inside
+// the store loop).  The wave image holds the window maps, entities, dead-body and obstacle-present
+// bits only (~5 KB at city128), so four waves per workgroup and many workgroups per CU hide the two
+// load round trips.
+// ---------------------------------------------------------------------------
+template <typename T, int NOBS>
+__global__ void __launch_bounds__(256) k_obs_gather(Dev d, T* out, const uint8_t* mask, ObsLayout L) {
+    extern __shared__ __align__(16) uint8_t smem[];
+    constexpr int WW = 21, PLANE = WW * WW, PER = (PLANE + 63) / 64;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int e = xcd_remap(blockIdx.x, gridDim.x) * 4 + wave;
+    if (e >= d.N) return;
+    if (mask && !mask[e]) return;
+    lu8* img = (lu8*)(smem + wave * L.bytes);
+    const int N = d.N, W = d.W, H = d.H;
+    obs_build(d, L, img, e, [&](int s, int& p, int& lf, int& wp, int& pr) {
+        p = d.pos[(size_t)s * N + e];
+        lf = d.life[(size_t)s * N + e];
+        wp = d.weapon[(size_t)s * N + e];
+        pr = d.present[(size_t)s * N + e];
+    });
+    const li32* pos = (const li32*)(img + L.off_pos);
+    const li32* life = (const li32*)(img + L.off_life);
+    const li32* cw = (const li32*)(img + L.off_cw);
+    const lu32* dead = (const lu32*)(img + L.off_dead);
+    const lu32* opres = (const lu32*)(img + L.off_opres);
+    const bool ch = d.obs_enc == ZS_ENC_CHANNELS;
+    const int C = ch ? 3 : 1;
+    const int32_t* hrow = d.obst_hp + (size_t)e * d.O;
+    uint32_t sc[NOBS][PER];
+    int32_t hv[NOBS][PER];
+    // static words of the window cells (out-of-bounds cells read cell 0, discarded below)
+#pragma unroll
+    for (int a = 0; a < NOBS; a++) {
+        const int32_t ap = pos[a];
+        const int ox = unpack_x(ap) - WW / 2, oy = unpack_y(ap) - WW / 2;
+#pragma unroll
+        for (int i = 0; i < PER; i++) {
+            const int cc = min(lane + 64 * i, PLANE - 1), r = cc / WW, q = cc - r * WW;
+            const int x = ox + q, y = oy + r;
+            const bool inb = (unsigned)x < (unsigned)W && (unsigned)y < (unsigned)H;
+            sc[a][i] = (uint32_t)d.scell[inb ? y * W + x : 0];
+        }
+    }
+    // HP of the window cells' obstacles (cells without one read obstacle 0, discarded below)
+#pragma unroll
+    for (int a = 0; a < NOBS; a++)
+#pragma unroll
+        for (int i = 0; i < PER; i++) {
+            const int oi = (int)(sc[a][i] & SC_OBST_MASK) - 1;
+            hv[a][i] = hrow[oi > 0 ? oi : 0];
+        }
+    // the store stream: LDS and registers only
+#pragma unroll 1
+    for (int a = 0; a < NOBS; a++) {
+        const int32_t ap = pos[a];
+        const int ox = unpack_x(ap) - WW / 2, oy = unpack_y(ap) - WW / 2;
+        const lu8* wm = img + a * PLANE;
+        T* o = out + ((size_t)e * NOBS + a) * C * PLANE;
+#pragma unroll
+        for (int i = 0; i < PER; i++) {
+            const int cell = lane + 64 * i;
+            const int cc = cell < PLANE ? cell : PLANE - 1, r = cc / WW, q = cc - r * WW;
+            const int x = ox + q, y = oy + r;
+            const bool inb = (unsigned)x < (unsigned)W && (unsigned)y < (unsigned)H;
+            const int c = inb ? y * W + x : 0;
+            const uint32_t bit = 1u << (c & 31);
+            const int sb = wm[cc];
+            const int v = cw[sb ? sb - 1 : 0], elife = life[sb ? sb - 1 : 0];
+            const uint32_t s = sc[a][i];
+            const int oi = (int)(s & SC_OBST_MASK) - 1;
+            const bool obp = oi >= 0 && ((opres[(oi > 0 ? oi : 0) >> 5] >> (oi & 31)) & 1u);
+            int code = (dead[c >> 5] & bit) ? ZS_THING_DEADBODY : (s & SC_OBJ_BIT) ? ZS_THING_OBJECTIVE : ZS_THING_NONE;
+            code = obp ? (int)((s >> SC_KIND_SHIFT) & 7u) : code;
+            code = sb ? (v & 255) : code;
+            code = inb ? code : ZS_THING_WALL;
+            int lf = sb ? elife : (obp ? hv[a][i] : 0);
+            lf = inb ? lf : 200;
+            const int weapon = (inb && sb) ? ((v >> 8) & 255) : 0;
+            if (cell < PLANE) obs_store(o, PLANE, cell, ch, code, lf, weapon);
+        }
+    }
+}

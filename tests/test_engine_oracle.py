@@ -122,7 +122,8 @@ PATHS = {
     "fused": {"ZS_FUSED": "1"},                    # reset work inside the step launch
     "obs_in_step": {"ZS_FOBS": "1"},               # observations written by the step / reset launches
     "obs_in_step_unfused": {"ZS_FOBS": "1", "ZS_FUSED": "0"},
-    "obs_k_obs": {"ZS_FOBS": "0", "ZS_OBS_PIPE": "0"},  # one-env-per-wave k_obs instead of k_obs_pipe
+    "obs_k_obs": {"ZS_FOBS": "0", "ZS_OBS_PIPE": "0", "ZS_OBS_GATHER": "0"},  # one-env-per-wave k_obs
+    "obs_gather": {"ZS_FOBS": "0", "ZS_OBS_PIPE": "0"},  # window-only fetches (k_obs_gather)
     "obs_scan": {"ZS_OBS_WIN": "0"},                # per-cell entity scan instead of the window map
     "obs_scan_in_step": {"ZS_OBS_WIN": "0", "ZS_FOBS": "1"},
     "obs_scell": {"ZS_OBS_STAT": "0"},              # per-cell static words instead of LDS bitmaps
