@@ -389,17 +389,26 @@ static bool getenv_off(const char* name) {
 static int choose_layout(zs_handle* h, int want_g, bool fused, int obs_bytes) {
     Dev& d = h->d;
     const int kMax = 64 * 1024;
-    int g0 = want_g > 0 ? want_g : 16;  // measured: G=16 and 32 beat 8 and 64 at C3 (tools/sweep_lanes.sh)
+    // measured: G=16 and 32 beat 8 and 64 at C3 (E=12, tools/sweep_lanes.sh); G=32 beats 16 and 64
+    // at C4 (E=54: the decisions spread over more lanes)
+    int g0 = want_g > 0 ? want_g : (d.E > 32 ? 32 : 16);
     int cand_full = (d.W * d.H <= 65535) ? d.ncand : 0;
+    // RNG window: a plain step draws about 1.5 words per actor (shuffle) plus one per attack or heal
+    // in range (C4, 54 actors: median 82 words); a window that runs dry sends the leader to HBM
+    int rw_need = 64;
+    while (rw_need < 512 && rw_need < 2 * d.E) rw_need *= 2;
+    if (getenv("ZS_RW_NEED")) rw_need = std::max(64, std::min(512, atoi(getenv("ZS_RW_NEED"))));
     int lists = (d.nps + d.nzs <= 4096) ? d.nps + d.nzs : 0;
     for (int G = g0; G <= 64; G *= 2) {
         int ne = 64 / G;
         int wgs = (d.N + ne - 1) / ne + (fused ? std::min(d.N, kResetWGs) : 0);
         int want = getenv_off("ZS_LDS_BUDGET") ? 1 : std::min(32, std::max(1, (wgs + 255) / 256));
         int best_res = -1;
+        for (int pass = 0; pass < 2 && best_res < 0; pass++)  // windows below the need only if nothing else fits
         for (int cand : {cand_full, 0})
             for (int lst : {lists, 0})
                 for (int rw : {512, 256, 128, 64}) {
+                    if (pass == 0 && rw < rw_need) continue;
                     int bytes = tick_layout(ne, d.E, d.DW, rw, cand, lst, d.A, obs_bytes).bytes;
                     if (fused) bytes = std::max(bytes, reset_lds_bytes(d.E, d.DW, d.ncand, lst, obs_bytes));
                     if (bytes > kMax) continue;
@@ -409,7 +418,7 @@ static int choose_layout(zs_handle* h, int want_g, bool fused, int obs_bytes) {
                         best_res = res;
                         h->G = G;
                         d.rw_cap = rw;
-                        d.rw_step = std::min(rw, 64);
+                        d.rw_step = std::min(rw, rw_need);
                         d.cand_cap = cand;
                         d.lists_cap = lst;
                         h->lds = bytes;

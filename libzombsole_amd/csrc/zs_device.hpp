@@ -18,9 +18,12 @@
 
 #include "../../include/zombsole_mi355x.h"
 
-// minimum waves per SIMD the one-wave step / tick / reset kernels are compiled for (register budget)
+// minimum waves per SIMD the one-wave step / tick / reset kernels are compiled for (register budget):
+// 6 caps k_tick at 80 VGPRs (88 unbounded: 5 waves) for a few dwords of scratch on cold paths;
+// measured C3 125 -> 127, C5 109 -> 114 M env-steps/s, C4 unchanged; 8 (64 VGPRs) spills more and
+// loses at C4
 #ifndef ZS_STEP_WAVES
-#define ZS_STEP_WAVES 1
+#define ZS_STEP_WAVES 6
 #endif
 
 #define ZS_MT_N 624

@@ -191,10 +191,15 @@ __device__ __forceinline__ void rng_reload(const Dev& d, Grp& c) {
         mt_twist_serial(ring + (slot ^ 1u) * ZS_MT_N, ring + slot * ZS_MT_N);
         ready = 1;
     }
-    for (int i = 0; i < n; i++) {
-        uint32_t q = off + i;
-        uint32_t w = q < ZS_MT_N ? ring[slot * ZS_MT_N + q] : ring[(slot ^ 1u) * ZS_MT_N + q - ZS_MT_N];
-        c.rw[IX(c, i)] = mt_temper(w);
+    for (int i0 = 0; i0 < n; i0 += 4) {  // 4 loads in flight (n is a multiple of 64)
+        uint32_t v[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            uint32_t q = off + i0 + u;
+            v[u] = q < ZS_MT_N ? ring[slot * ZS_MT_N + q] : ring[(slot ^ 1u) * ZS_MT_N + q - ZS_MT_N];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) c.rw[IX(c, i0 + u)] = mt_temper(v[u]);
     }
     c.st0 = st_pack(off, slot, ready);
     c.wpos = 0;
