@@ -65,6 +65,8 @@ def parse():
     p.add_argument("--obs-dtype", default=None, choices=["int64", "int32", "int16"])
     p.add_argument("--lanes-per-env", type=int, default=0, help="k_tick lanes per env (0 = engine default)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-graph", action="store_true",
+                   help="launch every step's kernels from the host instead of replaying the step as a hipGraph")
     p.add_argument("--cpu-steps", type=int, default=2000)
     a = p.parse_args()
     for k, v in PRESETS[a.config].items():
@@ -143,6 +145,8 @@ def main():
         env0 = rank * total_envs // world
         n_local = (rank + 1) * total_envs // world - env0
     eng = Engine(builder(n_local), device=dev)
+    launch = eng.describe()
+    launch["step_graph"] = not args.no_graph
     eng.seed([env0 + i for i in range(n_local)])
     eng.reset()
     torch.cuda.synchronize()
@@ -164,30 +168,49 @@ def main():
             dist.all_gather_into_tensor(g_pack, pack)
 
     step = 0
-    for _ in range(args.warmup):
+    use_graph = not args.no_graph
+
+    def one_step():
+        # the bench loop's step: the on-device policy's actions for step t, then zs_step; with graphs
+        # both are one replayed hipGraph whose step counter advances on the device
+        nonlocal step
         step += 1
-        eng.gen_actions(step, 7)
-        eng.step()
+        if use_graph:
+            eng.step_graph(step, 7)
+        else:
+            eng.gen_actions(step, 7)
+            eng.step()
         if gather:
             gather()
+
+    for _ in range(args.warmup):
+        one_step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    eng.profile(True)
+    if not use_graph:
+        eng.profile(True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step += 1
-        eng.gen_actions(step, 7)
-        eng.step()
-        if gather:
-            gather()
+        one_step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    prof_steps = args.steps
+    if use_graph:
+        # per-kernel HIP-event durations: the same steps launched one kernel at a time right after
+        # the timed replays (events cannot bracket the kernels inside a graph)
+        prof_steps = min(args.steps, 50)
+        eng.profile(True)
+        for _ in range(prof_steps):
+            step += 1
+            eng.gen_actions(step, 7)
+            eng.step()
+        torch.cuda.synchronize()
     prof = eng.profile_read()
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
@@ -203,9 +226,9 @@ def main():
     tick_b, obs_b = algorithmic_bytes(E, args.agents, (m.size[0] * m.size[1] + 7) // 8, obs_per_env, mt_words)
     # per-step kernel time (a step may run its tick and observation kernels in several env chunks
     # on two streams: sum the launches of each kind per step)
-    tick_ms = prof["tick_ms"] / args.steps
-    obs_ms = prof["obs_ms"] / args.steps
-    reset_ms = prof["reset_ms"] / args.steps
+    tick_ms = prof["tick_ms"] / prof_steps
+    obs_ms = prof["obs_ms"] / prof_steps
+    reset_ms = prof["reset_ms"] / prof_steps
     fused = prof["reset_n"] == 0  # reset work runs inside the step launch (k_step)
     fobs = prof["obs_n"] == 0      # the step launch writes the observations itself
     step_name = "k_step" if fused else "k_tick"
@@ -213,14 +236,17 @@ def main():
     if fobs or tick_ms >= obs_ms:
         dom, dom_ms, dom_b = step_name, tick_ms, step_b
     else:
-        dom, dom_ms, dom_b = "k_obs_pipe", obs_ms, obs_b
+        dom, dom_ms, dom_b = launch["obs_kernel"], obs_ms, obs_b
     achieved = dom_b * n_local / (dom_ms * 1e-3) / 1e9
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc):
         try:
             with open(pmc) as f:
-                traffic = json.load(f).get(dom, {}).get("hbm_bytes_per_launch")
+                wl = json.load(f).get("workloads", {}).get(args.config)
+            # profiled bytes per launch, scaled to this run's envs per GPU (per-env work is fixed)
+            t = wl["kernels"].get(dom, {}).get("hbm_bytes_per_launch") if wl else None
+            traffic = t * n_local / wl["envs_per_gpu"] if t is not None else None
         except Exception:
             traffic = None
     out = {
@@ -240,15 +266,16 @@ def main():
                    "minimum_zombies": args.min_zombies, "obs_dtype": args.obs_dtype,
                    "parallelism": "env-sharded x%d (%s)" % (
                        world, "RCCL all-gather of obs + rewards/done per step" if gather
-                       else "no data-path collective")},
+                       else "no data-path collective"), "launch": launch},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
                      "algorithmic_bytes_per_step": dom_b * n_local,
                      "kernel_ms_per_step": dom_ms, "launches_per_step": {
-                         "tick": prof["tick_n"] / args.steps, "obs": prof["obs_n"] / args.steps,
-                         "reset": prof["reset_n"] / args.steps},
+                         "tick": prof["tick_n"] / prof_steps, "obs": prof["obs_n"] / prof_steps,
+                         "reset": prof["reset_n"] / prof_steps, "respawn": prof["respawn_n"] / prof_steps},
                      "step_launch_ms": tick_ms, "k_obs_ms": obs_ms,
-                     "k_reset_ms": reset_ms, "step_launch_writes_obs": bool(fobs),
+                     "k_reset_ms": reset_ms, "k_respawn_ms": prof["respawn_ms"] / prof_steps,
+                     "step_launch_writes_obs": bool(fobs),
                      "step_launch_resets": bool(fused)},
         "cpu_baseline": None,
     }

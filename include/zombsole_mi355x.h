@@ -187,6 +187,14 @@ int zs_step(zs_handle* h, const int32_t* actions_dev, void* obs_dev, double* rew
 int zs_gen_actions(zs_handle* h, uint64_t step, int32_t n_discrete, int32_t* actions_dev,
                    void* stream);
 
+/* The bench loop's step as one replayed hipGraph: zs_gen_actions for step number t, then
+ * zs_step (same outputs), where t = step0 on the first call after a (re)capture and advances by
+ * one per call on the device.  The launches are captured once per pending-reset-list parity and
+ * recaptured when any buffer argument changes; results equal zs_gen_actions + zs_step. */
+int zs_step_graph(zs_handle* h, uint64_t step0, int32_t n_discrete, int32_t* actions_dev, void* obs_dev,
+                  double* rewards_dev, uint8_t* done_dev, uint8_t* trunc_dev, uint8_t* listed_dev,
+                  uint8_t* reset_dev, void* stream);
+
 /* Host view of one env's state as a flat int32 record (layout below). */
 int zs_state_size(const zs_handle* h, int32_t* n_words);
 int zs_get_state(zs_handle* h, int32_t env, int32_t* buf_host, void* stream);
@@ -209,6 +217,10 @@ int zs_set_rng(zs_handle* h, int32_t env, const uint32_t* state_host, void* stre
  * respawns), then clears the record. */
 int zs_profile(zs_handle* h, int32_t enable);
 int zs_profile_read(zs_handle* h, double out[8]);
+/* Diagnostics: the launch configuration the handle chose (lanes per env, LDS images, which
+ * observation kernel, fused / side-stream reset work, deferred respawn) as a one-line JSON
+ * object, NUL-terminated and truncated to len bytes.  Returns ZS_OK. */
+int zs_describe(zs_handle* h, char* buf, int32_t len);
 /* Diagnostic builds compiled with -DZS_STAMPS only (the product .so returns ZS_ESTATE):
  * per-phase k_tick cycle sums / maxima over all workgroup launches since the last call. */
 int zs_debug_stamps(zs_handle* h, uint64_t* sum_out, uint64_t* max_out, int32_t n);

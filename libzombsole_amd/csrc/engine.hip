@@ -100,6 +100,37 @@ __global__ void k_gen_actions(Dev d, uint64_t step, int n_discrete, int32_t* act
     act[(size_t)i * 3 + 2] = c_discrete[id][2];
 }
 
+__global__ void k_zero2(int* a, int* b) {
+    if (threadIdx.x == 0) *a = 0;
+    if (threadIdx.x == 1 && b) *b = 0;
+}
+
+// The same policy with the step read from device memory (zs_step_graph): every workgroup reads
+// ctr[0], then takes a ticket; the workgroup holding the last ticket knows every read is done and
+// advances the step for the next replay.
+__global__ void __launch_bounds__(256) k_gen_actions_dev(Dev d, uint64_t* ctr, int n_discrete, int32_t* act) {
+    __shared__ uint64_t s_step;
+    if (threadIdx.x == 0) s_step = __hip_atomic_load(&ctr[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const uint64_t step = s_step;
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < d.N * d.A) {
+        int e = i / d.A, a = i - e * d.A;
+        uint64_t h = splitmix64(splitmix64(splitmix64(d.seeds[e]) ^ step) ^ (uint64_t)a);
+        int id = (int)(h % (uint64_t)n_discrete);
+        act[(size_t)i * 3 + 0] = c_discrete[id][0];
+        act[(size_t)i * 3 + 1] = c_discrete[id][1];
+        act[(size_t)i * 3 + 2] = c_discrete[id][2];
+    }
+    if (threadIdx.x == 0) {
+        uint64_t t = __hip_atomic_fetch_add(&ctr[1], 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (t == gridDim.x - 1) {
+            __hip_atomic_store(&ctr[1], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&ctr[0], step + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // state views (one env, one thread; test pokes)
 // ---------------------------------------------------------------------------
@@ -244,6 +275,11 @@ struct zs_handle {
     int obs_pipe = 0;      // k_obs_pipe<NOBS> usable (NOBS = 1, 2, 4), else 0
     int obs_gather = 0;    // else k_obs_gather<NOBS> usable (NOBS = 1, 2, 4), else 0 (k_obs)
     ObsLayout obs_gl;      // its per-wave image
+    // zs_step_graph: one captured hipGraph per autoreset-list parity (the step alternates the two
+    // pending-reset lists), replayed on the caller's stream; keyed by the caller's buffers
+    hipGraphExec_t gexec[2] = {nullptr, nullptr};
+    const void* gkey[8] = {};
+    uint64_t* d_gstep = nullptr;  // [0] policy step counter, [1] workgroup ticket (k_gen_actions_dev)
     // step pipeline: the tick in `chunks` env ranges on the caller's stream, each range's observations
     // on s_obs as soon as its tick is done
     int chunks = 1;
@@ -324,6 +360,11 @@ static void free_all(zs_handle* h) {
     h->ev_rfork = h->ev_rjoin = nullptr;
     if (h->s_reset) (void)hipStreamDestroy(h->s_reset);
     h->s_reset = nullptr;
+    for (hipGraphExec_t& g : h->gexec)
+        if (g) {
+            (void)hipGraphExecDestroy(g);
+            g = nullptr;
+        }
     for (hipEvent_t ev : h->ev_pool) (void)hipEventDestroy(ev);
     h->ev_pool.clear();
 }
@@ -978,8 +1019,10 @@ extern "C" int zs_step(zs_handle* h, const int32_t* actions_dev, void* obs_dev, 
         if (side) HIPCHK(hipEventRecord(h->ev_rjoin, h->s_reset));
     }
     // 2) tick every other env; envs that end now are queued on list[q] for the next call
-    HIPCHK(hipMemsetAsync(h->d_rcount + q, 0, sizeof(int), s));
-    if (h->d.defer_respawn) HIPCHK(hipMemsetAsync(h->d.resp_count, 0, sizeof(int), s));
+    // the work-list counters this call appends to: one tiny kernel instead of one memset each (a
+    // 4-byte hipMemsetAsync captured into zs_step_graph's graph faulted on replay, ROCm 7.2)
+    hipLaunchKernelGGL(k_zero2, dim3(1), dim3(64), 0, s, h->d_rcount + q, h->d.defer_respawn ? h->d.resp_count : nullptr);
+    HIPCHK(hipGetLastError());
     const int K = (!h->fused && !h->d.fobs && obs_dev) ? h->chunks : 1;
     if (K > 1) {
         if (side) HIPCHK(hipStreamWaitEvent(s, h->ev_rjoin, 0));
@@ -1024,6 +1067,77 @@ extern "C" int zs_gen_actions(zs_handle* h, uint64_t step, int32_t n_discrete, i
     int n = h->d.N * h->d.A;
     hipLaunchKernelGGL(k_gen_actions, dim3((n + 255) / 256), dim3(256), 0, s, h->d, step, n_discrete, actions_dev);
     HIPCHK(hipGetLastError());
+    return ZS_OK;
+}
+
+// One step of the on-device policy loop (zs_gen_actions for the next step number, then zs_step) as a
+// replayed hipGraph: the launches of a step are captured once per pending-list parity and then
+// cost one graph launch per step instead of one dispatch each.  step0 is the step number of the
+// first call after (re)capture; later calls continue from the device counter.
+extern "C" int zs_step_graph(zs_handle* h, uint64_t step0, int32_t n_discrete, int32_t* actions_dev, void* obs_dev,
+                             double* rewards_dev, uint8_t* done_dev, uint8_t* trunc_dev, uint8_t* listed_dev,
+                             uint8_t* reset_dev, void* stream) {
+    if (!h || !actions_dev || !rewards_dev || !done_dev || !trunc_dev) return fail(ZS_EINVAL, "null argument");
+    if (n_discrete < 1 || n_discrete > 7) return fail(ZS_EINVAL, "n_discrete must be in 1..7");
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(hipSetDevice(h->device));
+    const void* key[8] = {actions_dev, obs_dev, rewards_dev, done_dev, trunc_dev, listed_dev, reset_dev,
+                          (const void*)(intptr_t)n_discrete};
+    bool same = h->gexec[0] && h->gexec[1];
+    for (int k = 0; k < 8 && same; k++) same = key[k] == h->gkey[k];
+    if (!same) {
+        for (hipGraphExec_t& g : h->gexec)
+            if (g) {
+                HIPCHK(hipGraphExecDestroy(g));
+                g = nullptr;
+            }
+        if (!h->d_gstep) {
+            int rc = dalloc(h, &h->d_gstep, 2);
+            if (rc) return rc;
+        }
+        uint64_t init[2] = {step0, 0};
+        HIPCHK(hipMemcpyAsync(h->d_gstep, init, sizeof(init), hipMemcpyHostToDevice, s));
+        HIPCHK(hipStreamSynchronize(s));
+        hipStream_t cs;
+        HIPCHK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+        const int prof = h->prof;
+        h->prof = 0;  // no timing events inside a graph
+        const int p0 = h->rpar;
+        int rc = ZS_OK;
+        for (int g = 0; g < 2 && rc == ZS_OK; g++) {  // parity p0, then 1 - p0 (zs_step flips rpar)
+            hipGraph_t graph = nullptr;
+            if (hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+                rc = fail(ZS_EHIP, "hipStreamBeginCapture failed");
+                break;
+            }
+            const int n = h->d.N * h->d.A;
+            hipLaunchKernelGGL(k_gen_actions_dev, dim3((n + 255) / 256), dim3(256), 0, cs, h->d, h->d_gstep, n_discrete,
+                               actions_dev);
+            rc = zs_step(h, actions_dev, obs_dev, rewards_dev, done_dev, trunc_dev, listed_dev, reset_dev, cs);
+            hipError_t ce = hipStreamEndCapture(cs, &graph);
+            if (rc == ZS_OK && ce != hipSuccess) rc = fail(ZS_EHIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(ce));
+            if (rc == ZS_OK) {
+                hipError_t ie = hipGraphInstantiate(&h->gexec[(p0 + g) & 1], graph, nullptr, nullptr, 0);
+                if (ie != hipSuccess) rc = fail(ZS_EHIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(ie));
+            }
+            if (graph) (void)hipGraphDestroy(graph);
+        }
+        h->rpar = p0;  // capturing ran no work: the lists are where they were
+        h->prof = prof;
+        (void)hipStreamDestroy(cs);
+        if (rc != ZS_OK) {
+            for (hipGraphExec_t& g : h->gexec)
+                if (g) {
+                    (void)hipGraphExecDestroy(g);
+                    g = nullptr;
+                }
+            return rc;
+        }
+        for (int k = 0; k < 8; k++) h->gkey[k] = key[k];
+    }
+    // gexec[p] drains list p (the parity of this step) and fills list 1 - p
+    HIPCHK(hipGraphLaunch(h->gexec[h->rpar], s));
+    h->rpar = 1 - h->rpar;
     return ZS_OK;
 }
 
@@ -1142,6 +1256,19 @@ extern "C" int zs_profile_read(zs_handle* h, double* out) {
     h->ev_reset.clear();
     h->ev_respawn.clear();
     h->ev_next = 0;
+    return ZS_OK;
+}
+
+extern "C" int zs_describe(zs_handle* h, char* buf, int32_t len) {
+    if (!h || !buf || len <= 0) return fail(ZS_EINVAL, "null argument");
+    const Dev& d = h->d;
+    const char* obs_kernel = d.fobs ? "step launch" : h->obs_pipe ? "k_obs_pipe" : h->obs_gather ? "k_obs_gather" : "k_obs";
+    snprintf(buf, (size_t)len,
+             "{\"envs\": %d, \"entities\": %d, \"lanes_per_env\": %d, \"step_kernel\": \"%s\", \"step_lds\": %zu, "
+             "\"step_wgs_per_cu\": %d, \"rng_window\": %d, \"obs_kernel\": \"%s\", \"reset_side_stream\": %d, "
+             "\"reset_lds\": %zu, \"respawn\": \"%s\", \"chunks\": %d}",
+             d.N, d.E, h->G, h->fused ? "k_step" : "k_tick", h->lds, h->resident, d.rw_cap, obs_kernel, h->reset_side,
+             h->reset_lds, d.defer_respawn ? "k_respawn" : "tick", h->chunks);
     return ZS_OK;
 }
 

@@ -13,7 +13,7 @@ from . import _abi
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_build", "libzombsole_mi355x.so")
 SYMBOLS = ["zs_last_error", "zs_create", "zs_destroy", "zs_obs_shape", "zs_seed", "zs_reset", "zs_step", "zs_observe",
-           "zs_gen_actions", "zs_state_size", "zs_get_state", "zs_set_state", "zs_get_rng", "zs_set_rng", "zs_profile", "zs_profile_read",
+           "zs_gen_actions", "zs_step_graph", "zs_state_size", "zs_get_state", "zs_set_state", "zs_get_rng", "zs_set_rng", "zs_profile", "zs_profile_read", "zs_describe",
            "zs_debug_stamps"]
 
 _lib = None
@@ -47,6 +47,7 @@ def load_library(path=None):
     L.zs_step.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.zs_observe.argtypes = [vp, vp, vp, vp]
     L.zs_gen_actions.argtypes = [vp, u64, i32, vp, vp]
+    L.zs_step_graph.argtypes = [vp, u64, i32, vp, vp, vp, vp, vp, vp, vp, vp]
     L.zs_state_size.argtypes = [vp, C.POINTER(i32)]
     L.zs_get_state.argtypes = [vp, i32, vp, vp]
     L.zs_set_state.argtypes = [vp, i32, vp, vp]
@@ -55,6 +56,7 @@ def load_library(path=None):
     L.zs_profile.argtypes = [vp, i32]
     L.zs_profile_read.argtypes = [vp, C.POINTER(C.c_double)]
     L.zs_debug_stamps.argtypes = [vp, vp, vp, i32]
+    L.zs_describe.argtypes = [vp, C.c_char_p, i32]
     for s in SYMBOLS:
         if s != "zs_last_error":
             getattr(L, s).restype = C.c_int
@@ -155,6 +157,16 @@ class Engine(object):
             _raise(self.L, rc, "zs_step")
         return self.obs, self.rewards, self.done, self.trunc
 
+    def step_graph(self, step0, n_discrete):
+        """gen_actions(t, n_discrete) + step() as one replayed hipGraph (t = step0 on the first call,
+        then advancing by one per call on the device)."""
+        rc = self.L.zs_step_graph(self.h, int(step0), int(n_discrete), _ptr(self.actions), _ptr(self.obs),
+                                  _ptr(self.rewards), _ptr(self.done), _ptr(self.trunc), _ptr(self.listed),
+                                  _ptr(self.was_reset), self._stream())
+        if rc:
+            _raise(self.L, rc, "zs_step_graph")
+        return self.obs, self.rewards, self.done, self.trunc
+
     def observe(self, mask=None):
         """Re-encode observations from the current state (after pokes)."""
         rc = self.L.zs_observe(self.h, _ptr(mask), _ptr(self.obs), self._stream())
@@ -181,6 +193,15 @@ class Engine(object):
             _raise(self.L, rc, "zs_profile_read")
         return {"tick_ms": out[0], "tick_n": int(out[1]), "obs_ms": out[2], "obs_n": int(out[3]),
                 "reset_ms": out[4], "reset_n": int(out[5]), "respawn_ms": out[6], "respawn_n": int(out[7])}
+
+    def describe(self):
+        """The launch configuration the engine chose (zs_describe), as a dict."""
+        import json
+        buf = C.create_string_buffer(1024)
+        rc = self.L.zs_describe(self.h, buf, len(buf))
+        if rc:
+            _raise(self.L, rc, "zs_describe")
+        return json.loads(buf.value.decode())
 
     def debug_stamps(self, n=5):
         """Per-phase k_tick cycle sums / maxima (diagnostic -DZS_STAMPS build only)."""

@@ -18,7 +18,8 @@ def _rich_triples(seed, step, n_agents):
     return np.array([A.encode_action(A.rich_action(seed, step, a)) for a in range(n_agents)], dtype=np.int32)
 
 
-def run_parity(make_builder, n_envs, steps, stream="discrete", seed0=1000, n_discrete=7, check_state_every=25):
+def run_parity(make_builder, n_envs, steps, stream="discrete", seed0=1000, n_discrete=7, check_state_every=25,
+               graph=False):
     import torch
     from libzombsole_amd.engine import Engine
     from oracle.oracle import OracleEnv
@@ -37,13 +38,18 @@ def run_parity(make_builder, n_envs, steps, stream="discrete", seed0=1000, n_dis
         refs.append(o)
     need = [False] * n_envs
     for t in range(1, steps + 1):
-        if stream == "discrete":
+        if graph:  # actions generated inside the replayed step graph
+            assert stream == "discrete"
+            eng.step_graph(t, n_discrete)
+            acts = eng.actions.cpu().numpy()
+        elif stream == "discrete":
             eng.gen_actions(t, n_discrete)
             acts = eng.actions.cpu().numpy()
+            eng.step()
         else:
             acts = np.stack([_rich_triples(s, t, eng.A) for s in seeds])
             eng.actions.copy_(torch.from_numpy(acts))
-        eng.step()
+            eng.step()
         torch.cuda.synchronize()
         obs = eng.obs.cpu().numpy()
         rew = eng.rewards.cpu().numpy()
@@ -172,3 +178,23 @@ def test_respawn_paths(path, monkeypatch):
     run_parity(lambda n: _abi.multi_env_config(n, "extermination", [], "city_for_safehouse", ["0", "1"],
                                                initial_zombies=3, minimum_zombies=2, max_episode_steps=40),
                32, 60, stream="rich", check_state_every=20)
+
+
+# The bench loop as a replayed hipGraph (zs_step_graph): same trajectories, for both pending-list
+# parities and every launch layout the graph may capture (fused step launch, separate reset launch on
+# the side stream, deferred respawn).
+GRAPH = {
+    "default": {},
+    "unfused_side_stream": {"ZS_FUSED": "0"},
+    "unfused_serial": {"ZS_FUSED": "0", "ZS_RESET_STREAM": "0"},
+}
+
+
+@pytest.mark.parametrize("path", sorted(GRAPH))
+def test_step_graph(path, monkeypatch):
+    for k, v in GRAPH[path].items():
+        monkeypatch.setenv(k, v)
+    run_parity(c2, 128, 80, check_state_every=40, graph=True)
+    run_parity(lambda n: _abi.multi_env_config(n, "safehouse", [], "city128", ["0", "1", "2", "3"],
+                                               initial_zombies=50, minimum_zombies=50),
+               16, 30, check_state_every=15, graph=True)

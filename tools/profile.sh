@@ -17,4 +17,4 @@ for c in FETCH_SIZE WRITE_SIZE; do
     echo "pmc $c ok"
 done
 # profiles/ written on the box is not merged back: run tools/pmc_summary.py locally on gpurun_out/prof
-python3 tools/pmc_summary.py "$OUT" ${TAG:-r01}
+python3 tools/pmc_summary.py "$OUT" ${TAG:-r01} ${PRESET:-c3} ${ENVS:-65536}
