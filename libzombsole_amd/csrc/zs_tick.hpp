@@ -80,7 +80,7 @@ struct TickLayout {
     int off_lst;
     int off_pos, off_life, off_weap, off_pres;
     int off_region;                          // = off_bm
-    int off_bm, off_rw, off_cand, off_tgt, off_ohp, off_ox, off_mod, off_order, off_rank, off_kind, off_perm, off_moved;
+    int off_bm, off_rw, off_cand, off_tgt, off_order, off_rank, off_kind, off_perm, off_moved;
     int bytes;
 };
 
@@ -114,12 +114,6 @@ __host__ __device__ inline TickLayout tick_layout(int ne, int E, int DW, int rw_
     o += rw_cap * ne * 4;
     L.off_tgt = o;
     o += E * ne * 4;
-    L.off_ohp = o;
-    o += E * ne * 4;
-    L.off_ox = o;
-    o += E * ne * 4;
-    L.off_mod = o;
-    o += 2 * E * ne * 4;
     L.off_cand = o;
     o += ((cand_cap * ne * 2 + 3) / 4) * 4;
     L.off_order = o;
@@ -158,16 +152,11 @@ struct Grp {
     lu8* lkind;
     lu8* lperm;
     lu8* lmoved;
-    li32* lohp;  // HP of the obstacle an actor's decision targets, fetched at decision time
-    li32* lox;   // its position
-    li32* lmod;  // obstacles whose HP this tick changed: (index, HP) pairs, first touch first
     // leader registers
     uint32_t st0;  // ring state at the start of the LDS window
     int wpos, wlen;
     int n_order, t, deaths, zd, epsteps, prevzd, serial, odirty;
     int respawn;  // the zombie respawn of this step is deferred to k_respawn
-    int nmod;     // entries of lmod
-    int fin;      // this step ended the episode (done or truncated)
 };
 
 #define IX(c, k) ((k) * (c).ne + (c).g)
@@ -182,10 +171,6 @@ struct Grp {
 #define LPE(c, s) (c).lperm[IX(c, s)]
 #define LM(c, s) (c).lmoved[IX(c, s)]
 #define MISC(c, f) (c).misc[IX(c, f)]
-#define LOH(c, s) (c).lohp[IX(c, s)]
-#define LOX(c, s) (c).lox[IX(c, s)]
-#define MOI(c, k) (c).lmod[IX(c, 2 * (k))]
-#define MHP(c, k) (c).lmod[IX(c, 2 * (k) + 1)]
 
 // ---------------------------------------------------------------------------
 // RNG: the leader draws pre-tempered words from the LDS window; when it runs dry it reloads
@@ -263,45 +248,28 @@ __device__ __forceinline__ int thing_at(const Dev& d, const Grp& c, int x, int y
     return -((int)d.cellmap[y * d.W + x] + 1);
 }
 
-// The obstacle a decision targets: its HP and position are fetched into LDS by the deciding lane,
-// so the leader's chain reads no global memory (a load behind the leader's own stores would wait
-// for all of them).  HP changes of the tick live in lmod; the global HP row is only written.
-__device__ __forceinline__ void obst_fetch(const Dev& d, Grp& c, int s, int kind, int tgt) {
-    if (tgt < 0 && (kind == K_ATTACK || kind == K_HEAL)) {
-        const int oi = -tgt - 1;
-        LOH(c, s) = d.obst_hp[(size_t)c.e * d.O + oi];
-        LOX(c, s) = d.obst_xy[oi];
-    }
+__device__ __forceinline__ int32_t target_pos(const Dev& d, const Grp& c, int tgt) {
+    return tgt >= 0 ? LP(c, tgt) : d.obst_xy[-tgt - 1];
 }
-__device__ __forceinline__ int obst_mod(const Grp& c, int oi) {
-    for (int k = 0; k < c.nmod; k++)
-        if (MOI(c, k) == oi) return k;
-    return -1;
-}
-// s: the acting slot (whose decision fetched an obstacle target)
-__device__ __forceinline__ int32_t target_pos(const Grp& c, int s, int tgt) { return tgt >= 0 ? LP(c, tgt) : LOX(c, s); }
 __device__ __forceinline__ int target_maxlife(const Dev& d, int tgt) {
     if (tgt >= 0) return 100;  // Zombie / Player / Agent MAX_LIFE (things.py:62,109)
     return d.obst_kind[-tgt - 1] == ZS_THING_BOX ? 10 : 200;
 }
-__device__ __forceinline__ int target_life(const Grp& c, int s, int tgt) {
+__device__ __forceinline__ int target_life(const Dev& d, const Grp& c, int tgt) {
     if (tgt >= 0) return LL(c, tgt);
-    const int k = obst_mod(c, -tgt - 1);
-    return k >= 0 ? MHP(c, k) : LOH(c, s);
+    return d.obst_hp[(size_t)c.e * d.O + (-tgt - 1)];
 }
 __device__ __forceinline__ void set_target_life(const Dev& d, Grp& c, int tgt, int v) {
     if (tgt >= 0) {
         LL(c, tgt) = v;
         return;
     }
-    const int oi = -tgt - 1;
-    int k = obst_mod(c, oi);
-    if (k < 0) {
-        k = c.nmod++;
-        MOI(c, k) = oi;
-    }
-    MHP(c, k) = v;
-    d.obst_hp[(size_t)c.e * d.O + oi] = v;  // store only: this launch reads the HP from lmod
+    int oi = -tgt - 1;
+    d.obst_hp[(size_t)c.e * d.O + oi] = v;
+    uint32_t* w = &d.obst_nonpos[(size_t)c.e * d.OW + (oi >> 5)];
+    uint32_t bit = 1u << (oi & 31);
+    *w = v <= 0 ? (*w | bit) : (*w & ~bit);
+    c.odirty = 1;
 }
 
 // closest(...) over present slots [s0, s1) \ {excl}: the first minimum in dict order
@@ -725,7 +693,6 @@ __device__ __forceinline__ void env_step_leader(const Dev& d, Grp& c, const int3
             decide(d, c, s, actions, true, kind, tgt);
             LK(c, s) = (uint8_t)kind;
             LT(c, s) = tgt;
-            obst_fetch(d, c, s, kind, tgt);
         }
         if (LK(c, s) != K_NONE) LPE(c, nact++) = (uint8_t)s;
     }
@@ -752,18 +719,18 @@ __device__ __forceinline__ void env_step_leader(const Dev& d, Grp& c, const int3
                 LR(c, s) = 255;  // re-inserted at the end of the dict
             }
         } else if (kind == K_ATTACK) {  // thing_attack (core.py:168-184)
-            int tp = target_pos(c, s, tgt);
+            int tp = target_pos(d, c, tgt);
             int w = LW(c, s);
             if (d2(x, y, unpack_x(tp), unpack_y(tp)) <= weapon_r2(w)) {
                 int dmg = rng_int(d, c, weapon_lo(w), weapon_hi(w));
-                set_target_life(d, c, tgt, target_life(c, s, tgt) - dmg);
+                set_target_life(d, c, tgt, target_life(d, c, tgt) - dmg);
             }
         } else {  // thing_heal (core.py:186-202), HEALING_RANGE = 3
-            int tp = target_pos(c, s, tgt);
+            int tp = target_pos(d, c, tgt);
             if (d2(x, y, unpack_x(tp), unpack_y(tp)) <= 9) {
                 int ml = target_maxlife(d, tgt);
                 int hl = rng_int(d, c, ml / 10, ml / 4);
-                set_target_life(d, c, tgt, min(ml, target_life(c, s, tgt) + hl));
+                set_target_life(d, c, tgt, min(ml, target_life(d, c, tgt) + hl));
             }
         }
     }
@@ -776,24 +743,7 @@ __device__ __forceinline__ void env_step_leader(const Dev& d, Grp& c, const int3
         }
         for (int j = 0; j < nmoved; j++) LO(c, m++) = LM(c, j);
     }
-    // clean_dead_things (core.py:121-138).  Obstacles whose HP this tick changed: the sign of the
-    // HP (carried over to later episodes) and the removal of the dead ones; every one of them is
-    // present (it was a target of this tick).
-    for (int k = 0; k < c.nmod; k++) {
-        const int oi = MOI(c, k), v = MHP(c, k);
-        const size_t wi = (size_t)c.e * d.OW + (oi >> 5);
-        const uint32_t bit = 1u << (oi & 31);
-        const uint32_t np = d.obst_nonpos[wi];
-        d.obst_nonpos[wi] = v <= 0 ? (np | bit) : (np & ~bit);
-        if (v <= 0) {
-            d.obst_present[wi] &= ~bit;
-            c.deaths++;
-            const int32_t op = d.obst_xy[oi];
-            bm_clr(c, unpack_y(op) * d.W + unpack_x(op));
-        }
-    }
-    c.nmod = 0;
-    // obstacles an episode starts with at HP <= 0 (carried over; k_reset sets odirty)
+    // clean_dead_things (core.py:121-138)
     if (c.odirty) {
         for (int w = 0; w < d.OW; w++) {
             uint32_t* pw = &d.obst_present[(size_t)c.e * d.OW + w];
@@ -841,10 +791,15 @@ __device__ __forceinline__ void env_step_leader(const Dev& d, Grp& c, const int3
         double prev = (double)c.prevzd + (double)sp / 100.0;
         double cur = (double)c.zd + (double)sc / 100.0;
         rs = cur - prev;
+    } else {
+        for (int a = 0; a < A; a++) {
+            double prev = (double)c.prevzd + (double)MISC(c, MISC_N + a) / 100.0;
+            double cur = (double)c.zd + (double)LL(c, a) / 100.0;
+            rew[(size_t)c.e * A + a] = cur - prev;
+        }
     }
-    // the multi-agent deltas are formed where they are written, after the rules (respawn and rules
-    // change no agent's life and no death count): reading back a stored delta would wait for every
-    // store the wave has in flight
+    for (int a = 0; a < A; a++) MISC(c, MISC_N + a) = LL(c, a);
+    c.prevzd = c.zd;
     // spawn_zombies_to_maintain_minimum (game.py:196-201).  Deferred: the respawn is the step's
     // last RNG consumer and nothing below reads the new zombies except Extermination's "any zombie
     // alive", which only needs to know whether one more zombie gets placed (a free spawn cell).
@@ -885,22 +840,17 @@ __device__ __forceinline__ void env_step_leader(const Dev& d, Grp& c, const int3
         for (int a = 0; a < A; a++) {
             uint8_t was = (uint8_t)MISC(c, MISC_N + A + a);
             if (listed_out) listed_out[(size_t)c.e * A + a] = was;
-            const double prev = (double)c.prevzd + (double)MISC(c, MISC_N + a) / 100.0;
-            const double cur = (double)c.zd + (double)LL(c, a) / 100.0;
-            double r = cur - prev;
+            double r = rew[(size_t)c.e * A + a];
             if (!was) r = 0.0;
             else if (LL(c, a) > 0) r = r + end_reward;
             rew[(size_t)c.e * A + a] = r;
             MISC(c, MISC_N + A + a) = LL(c, a) > 0;
         }
     }
-    for (int a = 0; a < A; a++) MISC(c, MISC_N + a) = LL(c, a);
-    c.prevzd = c.zd;
     c.epsteps++;
     if (d.max_steps > 0 && c.epsteps >= d.max_steps) tr = 1;
     done_out[c.e] = (uint8_t)ended;
     trunc_out[c.e] = (uint8_t)tr;
-    c.fin = ended || tr;
     SUB(4);
 }
 
@@ -970,9 +920,6 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
     c.lkind = (lu8*)(smem + L.off_kind);
     c.lperm = (lu8*)(smem + L.off_perm);
     c.lmoved = (lu8*)(smem + L.off_moved);
-    c.lohp = (li32*)(smem + L.off_ohp);
-    c.lox = (li32*)(smem + L.off_ox);
-    c.lmod = (li32*)(smem + L.off_mod);
     c.lists = (li32*)(smem + L.off_lists);
     if (d.lists_cap)  // the static spawn lists, staged once per workgroup
         for (int i = lane; i < d.nps + d.nzs; i += 64) c.lists[i] = i < d.nps ? d.pspawn[i] : d.zspawn[i - d.nps];
@@ -1074,7 +1021,6 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
             decide(d, c, s, actions, false, kind, tgt);
             LK(c, s) = (uint8_t)kind;
             LT(c, s) = tgt;
-            obst_fetch(d, c, s, kind, tgt);
         }
     }
     wave_sync();
@@ -1102,9 +1048,8 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
         c.prevzd = MISC(c, MISC_PREVZD);
         c.serial = MISC(c, MISC_SERIAL);
         c.odirty = MISC(c, MISC_ODIRTY);
-        c.nmod = 0;
         env_step_leader(d, c, actions, rew, done_out, trunc_out, listed_out);
-        if (c.fin && (d.flags & ZS_FLAG_AUTORESET)) {
+        if ((done_out[e] || trunc_out[e]) && (d.flags & ZS_FLAG_AUTORESET)) {
             needs_reset = 1;
             reset_list[atomicAdd(reset_count, 1)] = e;  // rebuilt by the next call's reset work
         }
