@@ -273,6 +273,8 @@ struct zs_handle {
     ObsLayout obs_l;  // k_obs per-wave LDS image
     int obs_wpg;      // k_obs waves (envs) per workgroup
     int obs_pipe = 0;      // k_obs_pipe<NOBS> usable (NOBS = 1, 2, 4), else 0
+    int obs_lds = 0;       // k_obs_pipe's walk with LDS-staged 16-B stores (k_obs_lds), channels encoding
+    size_t obs_lds_bytes = 0;
     int obs_gather = 0;    // else k_obs_gather<NOBS> usable (NOBS = 1, 2, 4), else 0 (k_obs)
     ObsLayout obs_gl;      // its per-wave image
     // zs_step_graph: one captured hipGraph per autoreset-list parity (the step alternates the two
@@ -676,6 +678,24 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
             h->obs_pipe_wgs = std::max(1, std::min(2, 160 * 1024 / (d.obs_stat * 4 + 4 * L.bytes)));
             if (getenv("ZS_OBS_WGS")) h->obs_pipe_wgs = std::max(1, std::min(32, atoi(getenv("ZS_OBS_WGS"))));
         }
+        // k_obs_lds: the same walk with each observation block staged in LDS and streamed out as 16-B
+        // stores (channels encoding).  Measured on one MI355X: int16 blocks (C5) 341 -> 264 us per
+        // launch at 4 workgroups per CU (2: 334, 3: 278, 5: 307); int64 blocks at 2 per CU win only
+        // when every wave walks many envs (C3 65536 envs: 351 -> 335 us; 32768: even; 8192, one env
+        // per wave: 33 vs 36 us for k_obs_pipe).  ZS_OBS_LDS=0/1 forces either.
+        if (h->obs_pipe && d.obs_enc == ZS_ENC_CHANNELS && !getenv_off("ZS_OBS_LDS")) {
+            const int ts = d.obs_dtype == ZS_DTYPE_I64 ? 8 : d.obs_dtype == ZS_DTYPE_I32 ? 4 : 2;
+            const size_t lb = (size_t)d.obs_stat * 4 + 4 * ((size_t)L.bytes + (size_t)obs_lds_slot_bytes(ts));
+            int wgs = std::max(1, std::min(ts == 8 ? 2 : 4, (int)(160 * 1024 / lb)));
+            if (getenv("ZS_OBS_WGS")) wgs = std::max(1, std::min(32, atoi(getenv("ZS_OBS_WGS"))));
+            const bool forced = getenv("ZS_OBS_LDS") != nullptr;
+            const bool pays = ts < 8 || (long)d.N >= 24L * 256 * wgs * 4;
+            if (lb <= 64 * 1024 && (pays || forced)) {
+                h->obs_lds = 1;
+                h->obs_lds_bytes = lb;
+                h->obs_pipe_wgs = wgs;
+            }
+        }
         // k_obs_gather when the store-stream kernel does not apply (e.g. city128's 3689 obstacles):
         // window-only static words and HP instead of per-env staging.  ZS_OBS_GATHER=0 disables.
         if (!h->obs_pipe && !world && d.obs_w == 21 && (nobs == 1 || nobs == 2 || nobs == 4) &&
@@ -820,9 +840,14 @@ static int launch_obs(zs_handle* h, void* obs, const uint8_t* mask, hipStream_t 
     if (env1 < 0) env1 = d.N;
     if (!mask && h->obs_pipe) {  // every env of [env0, env1), registered shape: the prefetching store stream
         const unsigned g = (unsigned)std::min((env1 - env0 + 3) / 4, 256 * h->obs_pipe_wgs);
-        const size_t lds = (size_t)d.obs_stat * 4 + 4 * (size_t)h->obs_l.bytes;
-#define ZS_PIPE(TT, NB) \
-    hipLaunchKernelGGL((k_obs_pipe<TT, NB>), dim3(g), dim3(256), lds, s, d, (TT*)obs, h->obs_l, env0, env1)
+        const size_t lds = h->obs_lds ? h->obs_lds_bytes : (size_t)d.obs_stat * 4 + 4 * (size_t)h->obs_l.bytes;
+#define ZS_PIPE(TT, NB)                                                                                                 \
+    do {                                                                                                                \
+        if (h->obs_lds)                                                                                                 \
+            hipLaunchKernelGGL((k_obs_lds<TT, NB>), dim3(g), dim3(256), lds, s, d, (TT*)obs, h->obs_l, env0, env1);    \
+        else                                                                                                            \
+            hipLaunchKernelGGL((k_obs_pipe<TT, NB>), dim3(g), dim3(256), lds, s, d, (TT*)obs, h->obs_l, env0, env1);   \
+    } while (0)
 #define ZS_PIPE_T(TT)                   \
     if (h->obs_pipe == 1) ZS_PIPE(TT, 1); \
     else if (h->obs_pipe == 2) ZS_PIPE(TT, 2); \
@@ -1262,7 +1287,9 @@ extern "C" int zs_profile_read(zs_handle* h, double* out) {
 extern "C" int zs_describe(zs_handle* h, char* buf, int32_t len) {
     if (!h || !buf || len <= 0) return fail(ZS_EINVAL, "null argument");
     const Dev& d = h->d;
-    const char* obs_kernel = d.fobs ? "step launch" : h->obs_pipe ? "k_obs_pipe" : h->obs_gather ? "k_obs_gather" : "k_obs";
+    const char* obs_kernel = d.fobs ? "step launch"
+                             : h->obs_pipe ? (h->obs_lds ? "k_obs_lds" : "k_obs_pipe")
+                             : h->obs_gather ? "k_obs_gather" : "k_obs";
     snprintf(buf, (size_t)len,
              "{\"envs\": %d, \"entities\": %d, \"lanes_per_env\": %d, \"step_kernel\": \"%s\", \"step_lds\": %zu, "
              "\"step_wgs_per_cu\": %d, \"rng_window\": %d, \"obs_kernel\": \"%s\", \"reset_side_stream\": %d, "

@@ -528,3 +528,106 @@ __global__ void __launch_bounds__(256) k_obs_gather(Dev d, T* out, const uint8_t
         }
     }
 }
+
+// ---------------------------------------------------------------------------
+// k_obs_lds: k_obs_pipe's persistent walk and register prefetch, but each observation block
+// (3 x 441 values, channels encoding) is first computed into a wave-private LDS slot, laid out at
+// the destination's 16-B phase, and then streamed out as 16-B stores: every full 16-B chunk of the
+// block is one aligned global_store_dwordx4 (half the store instructions of per-cell int64 stores,
+// an eighth of int16 ones) and the stream carries no lookups between its stores; the partial chunks
+// at the block's two ends are element stores.  tools/probe/storebw.hip: this store shape 5.2 TB/s.
+// ---------------------------------------------------------------------------
+typedef unsigned int zs_v4u __attribute__((ext_vector_type(4)));
+
+// staging bytes per wave: one channels block at any 16-B phase of its destination
+__host__ __device__ constexpr int obs_lds_slot_bytes(int tsize) { return ((3 * 441 * tsize + 31) / 16) * 16; }
+
+template <typename T, int NOBS>
+__global__ void __launch_bounds__(256, ZS_OBS_PIPE_WAVES) k_obs_lds(Dev d, T* out, ObsLayout L, int env0, int env1) {
+    extern __shared__ __align__(16) uint8_t smem[];
+    constexpr int WW = 21, PLANE = WW * WW, PER = (PLANE + 63) / 64, TS = (int)sizeof(T);
+    constexpr int ABYTES = 3 * PLANE * TS, SLOT = obs_lds_slot_bytes(TS), NCH = SLOT / 16;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int stat_words = 4 * d.DW;
+    lu32* st = (lu32*)smem;
+    obs_stage_static(d, st, threadIdx.x, blockDim.x);
+    __syncthreads();
+    const int waves = gridDim.x * 4;
+    int e = env0 + xcd_remap(blockIdx.x, gridDim.x) * 4 + wave;
+    if (e >= env1) return;
+    lu8* img = (lu8*)(smem + stat_words * 4 + wave * (L.bytes + SLOT));
+    lu8* slot = img + L.bytes;  // 16-B aligned: the static tables, L.bytes and SLOT are multiples of 16
+    li32* pos = (li32*)(img + L.off_pos);
+    li32* life = (li32*)(img + L.off_life);
+    li32* cw = (li32*)(img + L.off_cw);
+    lu32* dead = (lu32*)(img + L.off_dead);
+    lu32* opres = (lu32*)(img + L.off_opres);
+    li32* hp = (li32*)(img + L.off_hp);
+    const int code_s = lane < d.A ? d.agent_codes[lane < d.A ? lane : 0] : (lane < d.A + d.P ? ZS_THING_PLAYER : ZS_THING_ZOMBIE);
+    ObsPrefetch f;
+    obs_prefetch(d, e, f);
+    for (; e < env1; e += waves) {
+        // the image of env e from the registers
+        for (int w = lane; w < L.win / 4; w += 64) ((lu32*)img)[w] = 0u;
+        if (lane < d.E) {
+            pos[lane] = f.pos;
+            life[lane] = f.life;
+            cw[lane] = code_s | (f.wp << 8) | (f.pr << 16);
+        }
+#pragma unroll
+        for (int i = 0; i < OBS_PF_D; i++)
+            if (lane + 64 * i < d.DW) dead[lane + 64 * i] = f.dead[i];
+        if (lane < d.OW) opres[lane] = f.opres;
+#pragma unroll
+        for (int i = 0; i < OBS_PF_H; i++)
+            if (lane + 64 * i < d.O) hp[lane + 64 * i] = f.hp[i];
+        obs_prefetch(d, min(e + waves, env1 - 1), f);  // the next env (the last wave re-reads its own)
+        wave_sync();
+        // window map
+        if (lane < d.E && ((cw[lane] >> 16) & 1)) {
+            const int32_t p = pos[lane];
+            const int x = unpack_x(p), y = unpack_y(p);
+#pragma unroll
+            for (int a = 0; a < NOBS; a++) {
+                const int32_t ap = pos[a];
+                const int dx = x - (unpack_x(ap) - WW / 2), dy = y - (unpack_y(ap) - WW / 2);
+                if (dx >= 0 && dy >= 0 && dx < WW && dy < WW) img[a * PLANE + dy * WW + dx] = (uint8_t)(lane + 1);
+            }
+        }
+        wave_sync();
+#pragma unroll 1
+        for (int a = 0; a < NOBS; a++) {
+            const int32_t ap = pos[a];
+            const int ox = unpack_x(ap) - WW / 2, oy = unpack_y(ap) - WW / 2;
+            const lu8* wm = img + a * PLANE;
+            T* o = out + ((size_t)e * NOBS + a) * 3 * PLANE;
+            const int mis = (int)((uintptr_t)o & 15);
+            ZS_LDS T* ot = (ZS_LDS T*)(slot + mis);
+#pragma unroll
+            for (int i = 0; i < PER; i++) {
+                const int cell = lane + 64 * i;
+                const int cc = cell < PLANE ? cell : PLANE - 1, r = cc / WW, q = cc - r * WW;
+                int code, lf, weapon;
+                obs_cell_fast(d, L, st, img, wm, cc, ox + q, oy + r, code, lf, weapon);
+                if (cell < PLANE) {
+                    ot[cell] = (T)code;
+                    ot[PLANE + cell] = (T)lf;
+                    ot[2 * PLANE + cell] = (T)weapon;
+                }
+            }
+            wave_sync();
+            // chunk k = bytes [16k, 16k + 16) from the 16-B boundary at or below the block start
+            uint8_t* g0 = (uint8_t*)o - mis;
+            const int nb = mis + ABYTES, kend = nb >> 4, k0 = mis ? 1 : 0;
+#pragma unroll
+            for (int i = 0; i < (NCH + 63) / 64; i++) {
+                const int k = lane + 64 * i;
+                if (k >= k0 && k < kend) *(zs_v4u*)(g0 + 16 * k) = *(const ZS_LDS zs_v4u*)(slot + 16 * k);
+            }
+            const int nhead = mis ? (16 - mis) / TS : 0, tail0 = (16 * kend - mis) / TS, ntail = (nb - 16 * kend) / TS;
+            if (lane < nhead) o[lane] = ot[lane];
+            else if (lane >= 32 && lane - 32 < ntail) o[tail0 + lane - 32] = ot[tail0 + lane - 32];
+            wave_sync();
+        }
+    }
+}

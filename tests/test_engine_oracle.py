@@ -130,6 +130,8 @@ PATHS = {
     "obs_in_step_unfused": {"ZS_FOBS": "1", "ZS_FUSED": "0"},
     "obs_k_obs": {"ZS_FOBS": "0", "ZS_OBS_PIPE": "0", "ZS_OBS_GATHER": "0"},  # one-env-per-wave k_obs
     "obs_gather": {"ZS_FOBS": "0", "ZS_OBS_PIPE": "0"},  # window-only fetches (k_obs_gather)
+    "obs_pipe_cells": {"ZS_OBS_LDS": "0"},          # k_obs_pipe's per-cell stores instead of k_obs_lds
+    "obs_lds": {"ZS_OBS_LDS": "1"},                 # k_obs_lds at any env count
     "obs_scan": {"ZS_OBS_WIN": "0"},                # per-cell entity scan instead of the window map
     "obs_scan_in_step": {"ZS_OBS_WIN": "0", "ZS_FOBS": "1"},
     "obs_scell": {"ZS_OBS_STAT": "0"},              # per-cell static words instead of LDS bitmaps
@@ -198,3 +200,16 @@ def test_step_graph(path, monkeypatch):
     run_parity(lambda n: _abi.multi_env_config(n, "safehouse", [], "city128", ["0", "1", "2", "3"],
                                                initial_zombies=50, minimum_zombies=50),
                16, 30, check_state_every=15, graph=True)
+
+
+def test_store_stream_every_phase(monkeypatch):
+    """k_obs_lds writes each observation block from an LDS slot kept at the destination's 16-B
+    phase: int16 blocks of 4 agents (2646 B: every even phase), int32 single-agent blocks (5292 B)."""
+    monkeypatch.setenv("ZS_OBS_LDS", "1")
+    run_parity(lambda n: _abi.multi_env_config(n, "extermination", [], "bridge64", ["0", "1", "2", "3"],
+                                               initial_zombies=20, obs_dtype=_abi.DTYPE_I16, max_episode_steps=200),
+               64, 60, check_state_every=30)
+    run_parity(lambda n: _abi.single_env_config(n, "extermination", [], "bridge64", 0, initial_zombies=10,
+                                                observation_scope="surroundings:21",
+                                                observation_position_encoding="channels", max_episode_steps=200),
+               64, 60, n_discrete=6, check_state_every=30)
