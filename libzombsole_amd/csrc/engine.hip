@@ -100,19 +100,17 @@ __global__ void k_gen_actions(Dev d, uint64_t step, int n_discrete, int32_t* act
     act[(size_t)i * 3 + 2] = c_discrete[id][2];
 }
 
-__global__ void k_zero2(int* a, int* b) {
+// The work-list counters a step appends to; inside zs_step_graph's graph also the policy's step
+// counter, advanced here, after k_gen_actions_dev (earlier in the same stream) has read it.
+__global__ void k_zero2(int* a, int* b, uint64_t* step) {
     if (threadIdx.x == 0) *a = 0;
     if (threadIdx.x == 1 && b) *b = 0;
+    if (threadIdx.x == 2 && step) *step += 1;
 }
 
-// The same policy with the step read from device memory (zs_step_graph): every workgroup reads
-// ctr[0], then takes a ticket; the workgroup holding the last ticket knows every read is done and
-// advances the step for the next replay.
-__global__ void __launch_bounds__(256) k_gen_actions_dev(Dev d, uint64_t* ctr, int n_discrete, int32_t* act) {
-    __shared__ uint64_t s_step;
-    if (threadIdx.x == 0) s_step = __hip_atomic_load(&ctr[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    const uint64_t step = s_step;
+// The same policy with the step read from device memory (zs_step_graph); k_zero2 advances it.
+__global__ void __launch_bounds__(256) k_gen_actions_dev(Dev d, const uint64_t* ctr, int n_discrete, int32_t* act) {
+    const uint64_t step = ctr[0];
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < d.N * d.A) {
         int e = i / d.A, a = i - e * d.A;
@@ -121,13 +119,6 @@ __global__ void __launch_bounds__(256) k_gen_actions_dev(Dev d, uint64_t* ctr, i
         act[(size_t)i * 3 + 0] = c_discrete[id][0];
         act[(size_t)i * 3 + 1] = c_discrete[id][1];
         act[(size_t)i * 3 + 2] = c_discrete[id][2];
-    }
-    if (threadIdx.x == 0) {
-        uint64_t t = __hip_atomic_fetch_add(&ctr[1], 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        if (t == gridDim.x - 1) {
-            __hip_atomic_store(&ctr[1], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&ctr[0], step + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        }
     }
 }
 
@@ -281,7 +272,8 @@ struct zs_handle {
     // pending-reset lists), replayed on the caller's stream; keyed by the caller's buffers
     hipGraphExec_t gexec[2] = {nullptr, nullptr};
     const void* gkey[8] = {};
-    uint64_t* d_gstep = nullptr;  // [0] policy step counter, [1] workgroup ticket (k_gen_actions_dev)
+    uint64_t* d_gstep = nullptr;  // [0] policy step counter (k_gen_actions_dev reads, k_zero2 advances)
+    int capturing = 0;            // zs_step is being captured by zs_step_graph
     // step pipeline: the tick in `chunks` env ranges on the caller's stream, each range's observations
     // on s_obs as soon as its tick is done
     int chunks = 1;
@@ -1046,7 +1038,8 @@ extern "C" int zs_step(zs_handle* h, const int32_t* actions_dev, void* obs_dev, 
     // 2) tick every other env; envs that end now are queued on list[q] for the next call
     // the work-list counters this call appends to: one tiny kernel instead of one memset each (a
     // 4-byte hipMemsetAsync captured into zs_step_graph's graph faulted on replay, ROCm 7.2)
-    hipLaunchKernelGGL(k_zero2, dim3(1), dim3(64), 0, s, h->d_rcount + q, h->d.defer_respawn ? h->d.resp_count : nullptr);
+    hipLaunchKernelGGL(k_zero2, dim3(1), dim3(64), 0, s, h->d_rcount + q, h->d.defer_respawn ? h->d.resp_count : nullptr,
+                       h->capturing ? h->d_gstep : nullptr);
     HIPCHK(hipGetLastError());
     const int K = (!h->fused && !h->d.fobs && obs_dev) ? h->chunks : 1;
     if (K > 1) {
@@ -1127,6 +1120,7 @@ extern "C" int zs_step_graph(zs_handle* h, uint64_t step0, int32_t n_discrete, i
         HIPCHK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
         const int prof = h->prof;
         h->prof = 0;  // no timing events inside a graph
+        h->capturing = 1;
         const int p0 = h->rpar;
         int rc = ZS_OK;
         for (int g = 0; g < 2 && rc == ZS_OK; g++) {  // parity p0, then 1 - p0 (zs_step flips rpar)
@@ -1149,6 +1143,7 @@ extern "C" int zs_step_graph(zs_handle* h, uint64_t step0, int32_t n_discrete, i
         }
         h->rpar = p0;  // capturing ran no work: the lists are where they were
         h->prof = prof;
+        h->capturing = 0;
         (void)hipStreamDestroy(cs);
         if (rc != ZS_OK) {
             for (hipGraphExec_t& g : h->gexec)
