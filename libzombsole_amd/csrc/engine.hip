@@ -267,6 +267,7 @@ struct zs_handle {
     int obs_lds = 0;       // k_obs_pipe's walk with LDS-staged 16-B stores (k_obs_lds), channels encoding
     size_t obs_lds_bytes = 0;
     int obs_gather = 0;    // else k_obs_gather<NOBS> usable (NOBS = 1, 2, 4), else 0 (k_obs)
+    int obs_gather_staged = 0;  // k_obs_gather through LDS-staged 16-B stores
     ObsLayout obs_gl;      // its per-wave image
     // zs_step_graph: one captured hipGraph per autoreset-list parity (the step alternates the two
     // pending-reset lists), replayed on the caller's stream; keyed by the caller's buffers
@@ -696,6 +697,12 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
             if (4 * G.bytes <= 64 * 1024) {
                 h->obs_gather = nobs;
                 h->obs_gl = G;
+                // channels blocks through LDS and out as 16-B stores: off by default, measured even at
+                // C4 (217 vs 218 us: this kernel waits on its two load rounds, not on store issue)
+                const int ts = d.obs_dtype == ZS_DTYPE_I64 ? 8 : d.obs_dtype == ZS_DTYPE_I32 ? 4 : 2;
+                const char* gl = getenv("ZS_OBS_GATHER_LDS");
+                h->obs_gather_staged = d.obs_enc == ZS_ENC_CHANNELS && (gl ? atoi(gl) != 0 : false) &&
+                                       4 * (G.bytes + obs_lds_slot_bytes(ts)) <= 64 * 1024;
             }
         }
         // with the store-stream kernel available the observations are its job (measured faster than
@@ -862,9 +869,15 @@ static int launch_obs(zs_handle* h, void* obs, const uint8_t* mask, hipStream_t 
     }
     if (h->obs_gather) {  // one env per wave, four per workgroup, window-only fetches
         const unsigned g = (unsigned)((d.N + 3) / 4);
-        const size_t lds = 4 * (size_t)h->obs_gl.bytes;
-#define ZS_GATH(TT, NB) \
-    hipLaunchKernelGGL((k_obs_gather<TT, NB>), dim3(g), dim3(256), lds, s, d, (TT*)obs, mask, h->obs_gl)
+        const int ts = d.obs_dtype == ZS_DTYPE_I64 ? 8 : d.obs_dtype == ZS_DTYPE_I32 ? 4 : 2;
+        const size_t lds = 4 * ((size_t)h->obs_gl.bytes + (h->obs_gather_staged ? obs_lds_slot_bytes(ts) : 0));
+#define ZS_GATH(TT, NB)                                                                                              \
+    do {                                                                                                             \
+        if (h->obs_gather_staged)                                                                                    \
+            hipLaunchKernelGGL((k_obs_gather<TT, NB, true>), dim3(g), dim3(256), lds, s, d, (TT*)obs, mask, h->obs_gl); \
+        else                                                                                                         \
+            hipLaunchKernelGGL((k_obs_gather<TT, NB, false>), dim3(g), dim3(256), lds, s, d, (TT*)obs, mask, h->obs_gl); \
+    } while (0)
 #define ZS_GATH_T(TT)                         \
     if (h->obs_gather == 1) ZS_GATH(TT, 1);     \
     else if (h->obs_gather == 2) ZS_GATH(TT, 2); \

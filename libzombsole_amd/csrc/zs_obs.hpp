@@ -440,6 +440,32 @@ __global__ void __launch_bounds__(256, ZS_OBS_PIPE_WAVES) k_obs_pipe(Dev d, T* o
     }
 }
 
+// 16-B store stream of one staged observation block (k_obs_lds, k_obs_gather<..., true>)
+typedef unsigned int zs_v4u __attribute__((ext_vector_type(4)));
+
+// staging bytes per wave: one channels block at any 16-B phase of its destination
+__host__ __device__ constexpr int obs_lds_slot_bytes(int tsize) { return ((3 * 441 * tsize + 31) / 16) * 16; }
+
+// Stream one staged channels block (3 x 441 values of T, written at slot + (o & 15)) to o: every
+// full 16-B chunk one aligned 16-B store, the partial chunks at the two ends element stores.
+template <typename T>
+__device__ __forceinline__ void obs_block_flush(const lu8* slot, T* o, int lane) {
+    constexpr int TS = (int)sizeof(T), ABYTES = 3 * 441 * TS, NCH = obs_lds_slot_bytes(TS) / 16;
+    const int mis = (int)((uintptr_t)o & 15);
+    const ZS_LDS T* ot = (const ZS_LDS T*)(slot + mis);
+    // chunk k = bytes [16k, 16k + 16) from the 16-B boundary at or below the block start
+    uint8_t* g0 = (uint8_t*)o - mis;
+    const int nb = mis + ABYTES, kend = nb >> 4, k0 = mis ? 1 : 0;
+#pragma unroll
+    for (int i = 0; i < (NCH + 63) / 64; i++) {
+        const int k = lane + 64 * i;
+        if (k >= k0 && k < kend) *(zs_v4u*)(g0 + 16 * k) = *(const ZS_LDS zs_v4u*)(slot + 16 * k);
+    }
+    const int nhead = mis ? (16 - mis) / TS : 0, tail0 = (16 * kend - mis) / TS, ntail = (nb - 16 * kend) / TS;
+    if (lane < nhead) o[lane] = ot[lane];
+    else if (lane >= 32 && lane - 32 < ntail) o[tail0 + lane - 32] = ot[tail0 + lane - 32];
+}
+
 // ---------------------------------------------------------------------------
 // k_obs_gather: the registered shape (surroundings, width 21, NOBS observations per env) on maps
 // whose obstacle HP row is too large to stage per env (city128: 3689 obstacles, 14.7 KB, which
@@ -450,15 +476,18 @@ __global__ void __launch_bounds__(256, ZS_OBS_PIPE_WAVES) k_obs_pipe(Dev d, T* o
 // bits only (~5 KB at city128), so four waves per workgroup and many workgroups per CU hide the two
 // load round trips.
 // ---------------------------------------------------------------------------
-template <typename T, int NOBS>
+// STAGED: channels blocks go through an LDS slot per wave and out as 16-B stores (obs_block_flush).
+template <typename T, int NOBS, bool STAGED>
 __global__ void __launch_bounds__(256) k_obs_gather(Dev d, T* out, const uint8_t* mask, ObsLayout L) {
     extern __shared__ __align__(16) uint8_t smem[];
     constexpr int WW = 21, PLANE = WW * WW, PER = (PLANE + 63) / 64;
+    constexpr int SLOT = STAGED ? obs_lds_slot_bytes((int)sizeof(T)) : 0;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int e = xcd_remap(blockIdx.x, gridDim.x) * 4 + wave;
     if (e >= d.N) return;
     if (mask && !mask[e]) return;
-    lu8* img = (lu8*)(smem + wave * L.bytes);
+    lu8* img = (lu8*)(smem + wave * (L.bytes + SLOT));
+    lu8* slot = img + L.bytes;
     const int N = d.N, W = d.W, H = d.H;
     obs_build(d, L, img, e, [&](int s, int& p, int& lf, int& wp, int& pr) {
         p = d.pos[(size_t)s * N + e];
@@ -524,7 +553,21 @@ __global__ void __launch_bounds__(256) k_obs_gather(Dev d, T* out, const uint8_t
             int lf = sb ? elife : (obp ? hv[a][i] : 0);
             lf = inb ? lf : 200;
             const int weapon = (inb && sb) ? ((v >> 8) & 255) : 0;
-            if (cell < PLANE) obs_store(o, PLANE, cell, ch, code, lf, weapon);
+            if (STAGED) {
+                ZS_LDS T* ot = (ZS_LDS T*)(slot + ((uintptr_t)o & 15));
+                if (cell < PLANE) {
+                    ot[cell] = (T)code;
+                    ot[PLANE + cell] = (T)lf;
+                    ot[2 * PLANE + cell] = (T)weapon;
+                }
+            } else if (cell < PLANE) {
+                obs_store(o, PLANE, cell, ch, code, lf, weapon);
+            }
+        }
+        if (STAGED) {
+            wave_sync();
+            obs_block_flush(slot, o, lane);
+            wave_sync();
         }
     }
 }
@@ -537,16 +580,11 @@ __global__ void __launch_bounds__(256) k_obs_gather(Dev d, T* out, const uint8_t
 // an eighth of int16 ones) and the stream carries no lookups between its stores; the partial chunks
 // at the block's two ends are element stores.  tools/probe/storebw.hip: this store shape 5.2 TB/s.
 // ---------------------------------------------------------------------------
-typedef unsigned int zs_v4u __attribute__((ext_vector_type(4)));
-
-// staging bytes per wave: one channels block at any 16-B phase of its destination
-__host__ __device__ constexpr int obs_lds_slot_bytes(int tsize) { return ((3 * 441 * tsize + 31) / 16) * 16; }
-
 template <typename T, int NOBS>
 __global__ void __launch_bounds__(256, ZS_OBS_PIPE_WAVES) k_obs_lds(Dev d, T* out, ObsLayout L, int env0, int env1) {
     extern __shared__ __align__(16) uint8_t smem[];
     constexpr int WW = 21, PLANE = WW * WW, PER = (PLANE + 63) / 64, TS = (int)sizeof(T);
-    constexpr int ABYTES = 3 * PLANE * TS, SLOT = obs_lds_slot_bytes(TS), NCH = SLOT / 16;
+    constexpr int SLOT = obs_lds_slot_bytes(TS);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int stat_words = 4 * d.DW;
     lu32* st = (lu32*)smem;
@@ -616,17 +654,7 @@ __global__ void __launch_bounds__(256, ZS_OBS_PIPE_WAVES) k_obs_lds(Dev d, T* ou
                 }
             }
             wave_sync();
-            // chunk k = bytes [16k, 16k + 16) from the 16-B boundary at or below the block start
-            uint8_t* g0 = (uint8_t*)o - mis;
-            const int nb = mis + ABYTES, kend = nb >> 4, k0 = mis ? 1 : 0;
-#pragma unroll
-            for (int i = 0; i < (NCH + 63) / 64; i++) {
-                const int k = lane + 64 * i;
-                if (k >= k0 && k < kend) *(zs_v4u*)(g0 + 16 * k) = *(const ZS_LDS zs_v4u*)(slot + 16 * k);
-            }
-            const int nhead = mis ? (16 - mis) / TS : 0, tail0 = (16 * kend - mis) / TS, ntail = (nb - 16 * kend) / TS;
-            if (lane < nhead) o[lane] = ot[lane];
-            else if (lane >= 32 && lane - 32 < ntail) o[tail0 + lane - 32] = ot[tail0 + lane - 32];
+            obs_block_flush(slot, o, lane);
             wave_sync();
         }
     }
