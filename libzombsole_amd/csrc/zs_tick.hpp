@@ -157,6 +157,7 @@ struct Grp {
     int wpos, wlen;
     int n_order, t, deaths, zd, epsteps, prevzd, serial, odirty;
     int respawn;  // the zombie respawn of this step is deferred to k_respawn
+    int fin;      // this step ended the episode (done or truncated)
 };
 
 #define IX(c, k) ((k) * (c).ne + (c).g)
@@ -791,15 +792,10 @@ __device__ __forceinline__ void env_step_leader(const Dev& d, Grp& c, const int3
         double prev = (double)c.prevzd + (double)sp / 100.0;
         double cur = (double)c.zd + (double)sc / 100.0;
         rs = cur - prev;
-    } else {
-        for (int a = 0; a < A; a++) {
-            double prev = (double)c.prevzd + (double)MISC(c, MISC_N + a) / 100.0;
-            double cur = (double)c.zd + (double)LL(c, a) / 100.0;
-            rew[(size_t)c.e * A + a] = cur - prev;
-        }
     }
-    for (int a = 0; a < A; a++) MISC(c, MISC_N + a) = LL(c, a);
-    c.prevzd = c.zd;
+    // the multi-agent deltas are formed where they are written, after the rules (respawn and rules
+    // change no agent's life and no death count): reading back a stored delta would wait for every
+    // store the wave has in flight
     // spawn_zombies_to_maintain_minimum (game.py:196-201).  Deferred: the respawn is the step's
     // last RNG consumer and nothing below reads the new zombies except Extermination's "any zombie
     // alive", which only needs to know whether one more zombie gets placed (a free spawn cell).
@@ -840,17 +836,22 @@ __device__ __forceinline__ void env_step_leader(const Dev& d, Grp& c, const int3
         for (int a = 0; a < A; a++) {
             uint8_t was = (uint8_t)MISC(c, MISC_N + A + a);
             if (listed_out) listed_out[(size_t)c.e * A + a] = was;
-            double r = rew[(size_t)c.e * A + a];
+            const double prev = (double)c.prevzd + (double)MISC(c, MISC_N + a) / 100.0;
+            const double cur = (double)c.zd + (double)LL(c, a) / 100.0;
+            double r = cur - prev;
             if (!was) r = 0.0;
             else if (LL(c, a) > 0) r = r + end_reward;
             rew[(size_t)c.e * A + a] = r;
             MISC(c, MISC_N + A + a) = LL(c, a) > 0;
         }
     }
+    for (int a = 0; a < A; a++) MISC(c, MISC_N + a) = LL(c, a);
+    c.prevzd = c.zd;
     c.epsteps++;
     if (d.max_steps > 0 && c.epsteps >= d.max_steps) tr = 1;
     done_out[c.e] = (uint8_t)ended;
     trunc_out[c.e] = (uint8_t)tr;
+    c.fin = ended || tr;
     SUB(4);
 }
 
@@ -1049,7 +1050,7 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
         c.serial = MISC(c, MISC_SERIAL);
         c.odirty = MISC(c, MISC_ODIRTY);
         env_step_leader(d, c, actions, rew, done_out, trunc_out, listed_out);
-        if ((done_out[e] || trunc_out[e]) && (d.flags & ZS_FLAG_AUTORESET)) {
+        if (c.fin && (d.flags & ZS_FLAG_AUTORESET)) {
             needs_reset = 1;
             reset_list[atomicAdd(reset_count, 1)] = e;  // rebuilt by the next call's reset work
         }
