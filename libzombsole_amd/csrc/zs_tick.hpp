@@ -931,18 +931,67 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
     // this call's reset work, possibly concurrently: its state is neither read nor written here,
     // only this call's outputs (as after env.reset()) and the flag.
     int needs_reset = 0, stepping = 0, n_order = 0;
-    uint32_t st0 = 0;
+    uint32_t st0 = 0, st = 0;
     int wlen = 0;
-    if (active) needs_reset = d.scal[S_NEEDRESET * N + e];
+    // One round of loads for the flag, the stream state and the first batch of the entity table,
+    // scalar rows and bitmap, issued for every active env (a pending env's values go unused), then
+    // the LDS stores: one memory wait instead of one per kind of row.
+    int32_t vp[4], vl[4];
+    uint8_t vw[4], vr[4], vo[4];
+    int mval = 0;
+    uint32_t bmv[8];
+    const int nmisc = MISC_N + 2 * A;
+    if (active) {
+        needs_reset = d.scal[S_NEEDRESET * N + e];
+        n_order = d.scal[S_NORDER * N + e];
+        st = d.rngst[e];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int s = min(j + u * G, E - 1);
+            vp[u] = d.pos[(size_t)s * N + e];
+            vl[u] = d.life[(size_t)s * N + e];
+            vw[u] = d.weapon[(size_t)s * N + e];
+            vr[u] = d.present[(size_t)s * N + e];
+            vo[u] = d.order[(size_t)s * N + e];
+        }
+        const int f = min(j, nmisc - 1);
+        if (f == MISC_T) mval = d.scal[S_T * N + e];
+        else if (f == MISC_DEATHS) mval = d.scal[S_DEATHS * N + e];
+        else if (f == MISC_ZD) mval = d.scal[S_ZD * N + e];
+        else if (f == MISC_EPSTEPS) mval = d.scal[S_EPSTEPS * N + e];
+        else if (f == MISC_PREVZD) mval = d.scal[S_PREVZD * N + e];
+        else if (f == MISC_SERIAL) mval = d.scal[S_SERIAL * N + e];
+        else if (f == MISC_ODIRTY) mval = d.scal[S_ODIRTY * N + e];
+        else if (f == MISC_NONPOS) mval = 0;
+        else if (f < MISC_N + A) mval = d.prev_life[(size_t)(f - MISC_N) * N + e];
+        else mval = d.listed[(size_t)(f - MISC_N - A) * N + e];
+        const uint32_t* brow = d.occ_bits + (size_t)e * d.DW;
+#pragma unroll
+        for (int u = 0; u < 8; u++) bmv[u] = brow[min(j + u * G, d.DW - 1)];
+    }
     stepping = active && needs_reset == 0;
     if (stepping) {
-        n_order = d.scal[S_NORDER * N + e];
-        // stage the entity table (SoA [slot][N]: this env's column)
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int s = j + u * G;
+            if (s < E) {
+                c.lpos[IX(c, s)] = vp[u];
+                c.llife[IX(c, s)] = vl[u];
+                c.lweap[IX(c, s)] = vw[u];
+                c.lpres[IX(c, s)] = vr[u];
+                c.lorder[IX(c, s)] = vo[u];
+            }
+        }
+        if (j < nmisc) MISC(c, j) = mval;
+#pragma unroll
+        for (int u = 0; u < 8; u++)
+            if (j + u * G < d.DW) c.bm[IX(c, j + u * G)] = bmv[u];
+        // the rest of the entity table (E > 4G) (SoA [slot][N]: this env's column)
         {
             auto ix = [&](int s) { return IX(c, s); };
             const int32_t* pcol = d.pos + e;
             const int32_t* lcol = d.life + e;
-            for (int b = j; b < E; b += 4 * G) {
+            for (int b = j + 4 * G; b < E; b += 4 * G) {
                 int32_t vp[4], vl[4];
                 uint8_t vw[4], vr[4], vo[4];
 #pragma unroll
@@ -967,8 +1016,8 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
                 }
             }
         }
-        // per-env scalars and the reward tracker / env.agents rows
-        for (int f = j; f < MISC_N + 2 * A; f += G) {
+        // the rest of the per-env scalars and reward tracker / env.agents rows (more rows than lanes)
+        for (int f = j + G; f < nmisc; f += G) {
             int v;
             if (f == MISC_T) v = d.scal[S_T * N + e];
             else if (f == MISC_DEATHS) v = d.scal[S_DEATHS * N + e];
@@ -982,10 +1031,11 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
             else v = d.listed[(size_t)(f - MISC_N - A) * N + e];
             MISC(c, f) = v;
         }
-        // occupancy bitmap
-        stage_in(d.occ_bits + (size_t)e * d.DW, d.DW, j, G, c.bm, [&](int w) { return IX(c, w); });
+        // the rest of the occupancy bitmap
+        if (d.DW > 8 * G)
+            stage_in(d.occ_bits + (size_t)e * d.DW + 8 * G, d.DW - 8 * G, j, G, c.bm,
+                     [&](int w) { return IX(c, w + 8 * G); });
         // RNG window: the next words of this env's stream, tempered
-        uint32_t st = d.rngst[e];
         uint32_t off = st & 1023u, slot = (st >> 10) & 1u, ready = (st >> 11) & 1u;
         if (off >= ZS_MT_N && ready) {
             slot ^= 1u;
