@@ -1,8 +1,12 @@
 // engine.hip — MI355X-native batched zombsole step engine (gfx950) and its C ABI.
 //
-// k_tick (zs_tick.hpp) steps 64/G envs per wave with G lanes per env and the env's hot
-// state in LDS; k_obs (zs_obs.hpp) encodes the observations, one wave per env;
-// k_seed / k_gen_actions / k_get_state / k_set_state are the small helpers behind the ABI.
+// A step (zs_step) is: k_reset (zs_reset.hpp, one wave per env that ended at the previous step, on
+// a side stream concurrent with the tick, or fused with it into k_step), k_tick (zs_tick.hpp, 64/G
+// envs per wave with G lanes per env and the env's hot state in LDS), k_respawn (deferred zombie
+// respawns, one wave per env) and the observation kernel (zs_obs.hpp: k_obs_lds / k_obs_pipe
+// persistent store streams, k_obs_gather for large maps, k_obs in general).  zs_step_graph replays
+// a step as a hipGraph.  k_seed / k_gen_actions / k_get_state / k_set_state are the small helpers
+// behind the ABI.
 //
 // Semantics follow the reference exactly (parity: tests/); every sqrt range
 // test of the reference is replaced by its exact integer d^2 equivalent.
