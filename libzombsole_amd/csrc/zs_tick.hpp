@@ -80,7 +80,7 @@ struct TickLayout {
     int off_lst;
     int off_pos, off_life, off_weap, off_pres;
     int off_region;                          // = off_bm
-    int off_bm, off_rw, off_cand, off_tgt, off_order, off_rank, off_kind, off_perm, off_moved;
+    int off_bm, off_rw, off_cand, off_tgt, off_act, off_order, off_rank, off_kind, off_perm, off_moved;
     int bytes;
 };
 
@@ -114,6 +114,8 @@ __host__ __device__ inline TickLayout tick_layout(int ne, int E, int DW, int rw_
     o += rw_cap * ne * 4;
     L.off_tgt = o;
     o += E * ne * 4;
+    L.off_act = o;  // the agents' action triples, loaded with the stage-in round
+    o += 3 * A * ne * 4;
     L.off_cand = o;
     o += ((cand_cap * ne * 2 + 3) / 4) * 4;
     L.off_order = o;
@@ -152,6 +154,7 @@ struct Grp {
     lu8* lkind;
     lu8* lperm;
     lu8* lmoved;
+    li32* lact;  // agent a's action triple at 3a..3a+2
     // leader registers
     uint32_t st0;  // ring state at the start of the LDS window
     int wpos, wlen;
@@ -172,6 +175,7 @@ struct Grp {
 #define LPE(c, s) (c).lperm[IX(c, s)]
 #define LM(c, s) (c).lmoved[IX(c, s)]
 #define MISC(c, f) (c).misc[IX(c, f)]
+#define LACT(c, k) (c).lact[IX(c, k)]
 
 // ---------------------------------------------------------------------------
 // RNG: the leader draws pre-tempered words from the LDS window; when it runs dry it reloads
@@ -472,9 +476,9 @@ __device__ __forceinline__ void decide_zombie(const Dev& d, Grp& c, int s, bool 
 __device__ __forceinline__ int clamp16(int v) { return v < -16384 ? -16384 : (v > 16383 ? 16383 : v); }
 
 // Agent.next_step (players/agent.py:28-96) on the action triple
-__device__ __forceinline__ void decide_agent(const Dev& d, const Grp& c, int s, const int32_t* act, int& kind, int& tgt) {
+__device__ __forceinline__ void decide_agent(const Dev& d, const Grp& c, int s, int& kind, int& tgt) {
     int p = LP(c, s), x = unpack_x(p), y = unpack_y(p);
-    int ak = act[0], dx = clamp16(act[1]), dy = clamp16(act[2]);
+    int ak = LACT(c, 3 * s), dx = clamp16(LACT(c, 3 * s + 1)), dy = clamp16(LACT(c, 3 * s + 2));
     kind = K_NONE;
     if (ak == ZS_ACT_MOVE) {
         kind = K_MOVE;
@@ -604,7 +608,7 @@ __device__ __forceinline__ void decide(const Dev& d, Grp& c, int s, const int32_
                                        int& tgt) {
     kind = K_NONE;
     tgt = 0;
-    if (s < d.A) decide_agent(d, c, s, actions + ((size_t)c.e * d.A + s) * 3, kind, tgt);
+    if (s < d.A) decide_agent(d, c, s, kind, tgt);
     else if (s < d.A + d.P) decide_bot(d, c, s, rng, kind, tgt);
     else decide_zombie(d, c, s, rng, kind, tgt);
 }
@@ -921,6 +925,7 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
     c.lkind = (lu8*)(smem + L.off_kind);
     c.lperm = (lu8*)(smem + L.off_perm);
     c.lmoved = (lu8*)(smem + L.off_moved);
+    c.lact = (li32*)(smem + L.off_act);
     c.lists = (li32*)(smem + L.off_lists);
     if (d.lists_cap)  // the static spawn lists, staged once per workgroup
         for (int i = lane; i < d.nps + d.nzs; i += 64) c.lists[i] = i < d.nps ? d.pspawn[i] : d.zspawn[i - d.nps];
@@ -938,10 +943,11 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
     // the LDS stores: one memory wait instead of one per kind of row.
     int32_t vp[4], vl[4];
     uint8_t vw[4], vr[4], vo[4];
-    int mval = 0;
+    int mval = 0, av = 0;
     uint32_t bmv[8];
     const int nmisc = MISC_N + 2 * A;
     if (active) {
+        if (A) av = actions[(size_t)e * A * 3 + min(j, 3 * A - 1)];
         needs_reset = d.scal[S_NEEDRESET * N + e];
         n_order = d.scal[S_NORDER * N + e];
         st = d.rngst[e];
@@ -983,6 +989,8 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
             }
         }
         if (j < nmisc) MISC(c, j) = mval;
+        if (j < 3 * A) LACT(c, j) = av;
+        for (int k = j + G; k < 3 * A; k += G) LACT(c, k) = actions[(size_t)e * A * 3 + k];
 #pragma unroll
         for (int u = 0; u < 8; u++)
             if (j + u * G < d.DW) c.bm[IX(c, j + u * G)] = bmv[u];
