@@ -87,28 +87,77 @@ def algorithmic_bytes(E, A, occ_bytes, obs_bytes_per_env, mt_words):
     return tick, obs_bytes_per_env
 
 
-def cpu_baseline(args, builder_fn):
-    """The C oracle (bit-exact CPU restatement, "port") on this host, bounded sample."""
-    from oracle.oracle import run_batch
+def host_cpu():
+    """nproc, the affinity set, the cgroup CPU quota and the CPU model of this host."""
+    info = {"nproc": os.cpu_count()}
     try:
-        threads = len(os.sched_getaffinity(0))
+        info["affinity"] = len(os.sched_getaffinity(0))
     except AttributeError:
-        threads = os.cpu_count() or 1
-    threads = max(1, min(threads, int(os.environ.get("OMP_NUM_THREADS", "16") or 16), 16))
-    n_envs = 8192
+        info["affinity"] = info["nproc"]
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            info["cgroup_cpu_quota"] = None if q == "max" else float(q) / float(per)
+    except (OSError, ValueError):
+        info["cgroup_cpu_quota"] = None
+    model, sockets, cores = None, set(), None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name") and model is None:
+                    model = line.split(":", 1)[1].strip()
+                elif line.startswith("physical id"):
+                    sockets.add(line.split(":", 1)[1].strip())
+                elif line.startswith("cpu cores") and cores is None:
+                    cores = int(line.split(":", 1)[1])
+    except (OSError, ValueError):
+        pass
+    info["model"] = model
+    info["sockets"] = len(sockets) or None
+    info["physical_cores"] = cores * len(sockets) if cores and sockets else None
+    return info
+
+
+def cpu_baseline(args, builder_fn):
+    """The C oracle (bit-exact CPU restatement, "port") on this host, bounded sample, OpenMP over every
+    CPU of the affinity set, plus a 1-thread figure."""
+    from oracle.oracle import run_batch
+    host = host_cpu()
+    # every CPU of the affinity set, unless a cgroup CPU quota caps the process below that (the GPU
+    # box: 256 CPUs visible, a 16-CPU quota; oversubscribing the quota only adds preemption)
+    threads = host["affinity"] or 1
+    if host["cgroup_cpu_quota"]:
+        threads = max(1, min(threads, int(host["cgroup_cpu_quota"] + 0.5)))
     b = builder_fn(1)
-    steps = args.cpu_steps
-    if args.config != "c3":  # heavier configs: size the sample from a short probe (~2 s wall)
+
+    def timed(n_envs, steps, th):
         t0 = time.perf_counter()
-        run_batch(b, 0, n_envs, 20, 7, threads=threads)
-        steps = max(20, min(steps, int(20 * 2.0 / max(time.perf_counter() - t0, 1e-3))))
-    t0 = time.perf_counter()
-    n, _ = run_batch(b, 0, n_envs, steps, 7, threads=threads)
-    dt = time.perf_counter() - t0
+        n, _ = run_batch(b, 0, n_envs, steps, 7, threads=th)
+        return n, time.perf_counter() - t0
+
+    # size the samples from a short probe: ~1.5 s wall on one thread, ~3 s on all of them
+    n1, dt1 = timed(64, 20, 1)
+    rate1 = n1 / dt1
+    steps1 = max(20, min(args.cpu_steps, int(1.5 * rate1 / 64)))
+    n1, dt1 = timed(64, steps1, 1)
+    rate1 = n1 / dt1
+    steps = args.cpu_steps
+    eff = min(threads, host["cgroup_cpu_quota"] or threads)
+    n_envs = max(threads * 4, int(3.0 * rate1 * eff / steps))
+    n, dt = timed(n_envs, steps, threads)
+    cores = host["physical_cores"] or host["nproc"]
     return {"value": n / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "sample": "C oracle (oracle/zs_oracle.c, OpenMP over envs), %d envs x %d steps of the same "
-                      "workload (same map/agents/zombies/policy/obs, autoreset, TimeLimit), %.1f s wall x %d "
-                      "threads = %.0f thread-s" % (n_envs, steps, dt, threads, dt * threads)}
+            "host": host, "one_thread_value": rate1,
+            # not measured: the 1-thread rate times the host's physical cores (linear scaling, no SMT
+            # gain), the figure the whole host could reach without the quota
+            "all_cores_linear_estimate": rate1 * cores,
+            "sample": "C oracle (oracle/zs_oracle.c, OpenMP over envs, %d threads = the CPUs of the affinity set "
+                      "within the cgroup quota; "
+                      "host %s, %s socket(s), %s cores, nproc %s, cgroup CPU quota %s), %d envs x %d steps of the same "
+                      "workload (same map/agents/zombies/policy/obs, autoreset, TimeLimit), %.2f s wall; "
+                      "1 thread: %.0f env-steps/s over 64 envs x %d steps" % (
+                          threads, host["model"], host["sockets"], host["physical_cores"], host["nproc"], host["cgroup_cpu_quota"],
+                          n_envs, steps, dt, rate1, steps1)}
 
 
 def main():
@@ -120,9 +169,11 @@ def main():
     from libzombsole_amd.engine import Engine
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    # under torchrun (even --nproc-per-node 1) the ranks form an RCCL group: C5's gather then runs
+    distributed = world > 1 or "TORCHELASTIC_RUN_ID" in os.environ
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    if distributed:
         torch.cuda.set_device(local)
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -152,20 +203,11 @@ def main():
     torch.cuda.synchronize()
 
     gather = None
-    if args.gather and world > 1:
+    if args.gather and distributed:
         # C5: every step's observation shards + (rewards, done, truncated) packed per env, all-gathered
         # over RCCL into preallocated node-wide tensors (a centralised learner's input)
-        A = args.agents
-        pack = torch.empty((n_local, 8 * A + 2), dtype=torch.uint8, device="cuda")
-        g_obs = torch.empty((world * n_local,) + tuple(eng.obs.shape[1:]), dtype=eng.obs.dtype, device="cuda")
-        g_pack = torch.empty((world * n_local, 8 * A + 2), dtype=torch.uint8, device="cuda")
-
-        def gather():
-            pack[:, :8 * A].copy_(eng.rewards.view(torch.uint8).view(n_local, 8 * A))
-            pack[:, 8 * A] = eng.done.view(torch.uint8)
-            pack[:, 8 * A + 1] = eng.trunc.view(torch.uint8)
-            dist.all_gather_into_tensor(g_obs, eng.obs)
-            dist.all_gather_into_tensor(g_pack, pack)
+        from libzombsole_amd.vector import StepGather
+        gather = StepGather(eng)
 
     step = 0
     use_graph = not args.no_graph
@@ -186,18 +228,18 @@ def main():
     for _ in range(args.warmup):
         one_step()
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     if not use_graph:
         eng.profile(True)
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         one_step()
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     prof_steps = args.steps
@@ -212,7 +254,7 @@ def main():
             eng.step()
         torch.cuda.synchronize()
     prof = eng.profile_read()
-    if world > 1:
+    if distributed:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -284,7 +326,7 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     eng.close()
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
 
 

@@ -92,19 +92,105 @@ class BatchedZombsole(object):
         self.engine.close()
 
 
-def gather_observations(obs, group=None):
-    """All-gather every rank's observation shard into one [G*N, ...] tensor.
-
-    Over RCCL on MI355X this is one all_gather_into_tensor of the compact obs; with gloo
-    (CPU tests) the same call runs on host tensors."""
+def _gather_sizes(n_local, device, group):
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
-    out = torch.empty((world * obs.shape[0],) + tuple(obs.shape[1:]), dtype=obs.dtype, device=obs.device)
+    t = torch.tensor([int(n_local)], dtype=torch.int64, device=device)
+    parts = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(parts, t, group=group)
+    return [int(p.item()) for p in parts]
+
+
+def _all_gather_rows(out, x, group):
+    """out[r*m:(r+1)*m] = rank r's x (every rank's x has m rows).
+
+    RCCL has no int16 type (the compact C5 observations): such tensors travel as their bytes."""
+    import torch
+    import torch.distributed as dist
     if dist.get_backend(group) == "gloo":
-        parts = list(out.chunk(world, dim=0))
-        dist.all_gather(parts, obs.contiguous(), group=group)
-        out = torch.cat(parts, dim=0)
-    else:
-        dist.all_gather_into_tensor(out, obs.contiguous(), group=group)
-    return out
+        dist.all_gather(list(out.chunk(dist.get_world_size(group), dim=0)), x, group=group)
+        return
+    if x.dtype in (torch.int16, torch.uint16, torch.bool):
+        out, x = out.view(torch.uint8), x.view(torch.uint8)
+    dist.all_gather_into_tensor(out, x, group=group)
+
+
+def gather_observations(obs, group=None):
+    """All-gather every rank's observation shard into one [sum(N_r), ...] tensor in global env
+    order.
+
+    Shards from `shard_range` differ by at most one env: the per-rank sizes are exchanged first and
+    short shards padded to the longest, so every rank issues one equal-sized collective.  Over RCCL
+    on MI355X it is one all_gather_into_tensor; with gloo (CPU tests) the same call on host tensors."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    sizes = _gather_sizes(obs.shape[0], obs.device, group)
+    m = max(sizes)
+    x = obs.contiguous()
+    if x.shape[0] < m:
+        x = torch.cat([x, x.new_zeros((m - x.shape[0],) + tuple(x.shape[1:]))], dim=0)
+    out = torch.empty((world * m,) + tuple(obs.shape[1:]), dtype=obs.dtype, device=obs.device)
+    _all_gather_rows(out, x, group)
+    if all(n == m for n in sizes):
+        return out
+    return torch.cat([out[r * m:r * m + n] for r, n in enumerate(sizes)], dim=0)
+
+
+class StepGather(object):
+    """C5's per-step exchange for a centralised learner: every rank's observation
+    shard plus its rewards / done / truncated, all-gathered into preallocated node-wide tensors.
+
+    Rewards (float64 [N, A] as bytes), done and truncated are packed into one uint8 row per env so
+    the exchange is two collectives per step.  The shard sizes are exchanged once, at construction;
+    short shards (sizes differ by one when the total does not divide) are padded, and `obs()` /
+    `rewards()` / `done()` / `truncated()` return the node-wide tensors in global env order."""
+
+    def __init__(self, engine, group=None):
+        import torch
+        import torch.distributed as dist
+        self.torch = torch
+        self.eng = engine
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.n = engine.N
+        self.sizes = _gather_sizes(self.n, engine.device, group)
+        self.m = max(self.sizes)
+        self.R = engine.rewards.shape[1]
+        dev = engine.device
+        shape = tuple(engine.obs.shape[1:])
+        self.pad = None if self.n == self.m else torch.zeros((self.m,) + shape, dtype=engine.obs.dtype, device=dev)
+        self.pack = torch.zeros((self.m, 8 * self.R + 2), dtype=torch.uint8, device=dev)
+        self.g_obs = torch.empty((self.world * self.m,) + shape, dtype=engine.obs.dtype, device=dev)
+        self.g_pack = torch.empty((self.world * self.m, 8 * self.R + 2), dtype=torch.uint8, device=dev)
+
+    def __call__(self):
+        e, n, R = self.eng, self.n, self.R
+        self.pack[:n, :8 * R].copy_(e.rewards.view(self.torch.uint8).view(n, 8 * R))
+        self.pack[:n, 8 * R] = e.done
+        self.pack[:n, 8 * R + 1] = e.trunc
+        src = e.obs
+        if self.pad is not None:
+            self.pad[:n].copy_(e.obs)
+            src = self.pad
+        _all_gather_rows(self.g_obs, src, self.group)
+        _all_gather_rows(self.g_pack, self.pack, self.group)
+
+    def _rows(self, t):
+        if all(s == self.m for s in self.sizes):
+            return t
+        return self.torch.cat([t[r * self.m:r * self.m + s] for r, s in enumerate(self.sizes)], dim=0)
+
+    def obs(self):
+        return self._rows(self.g_obs)
+
+    def rewards(self):
+        R = self.R
+        return self._rows(self.g_pack[:, :8 * R]).contiguous().view(self.torch.float64).view(-1, R)
+
+    def done(self):
+        return self._rows(self.g_pack[:, 8 * self.R])
+
+    def truncated(self):
+        return self._rows(self.g_pack[:, 8 * self.R + 1])

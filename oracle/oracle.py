@@ -47,6 +47,11 @@ def load(path):
     L.zo_run_batch.restype = C.c_int64
     L.zo_run_batch.argtypes = [C.c_void_p, C.c_uint64, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                                C.POINTER(C.c_uint64)]
+    L.zo_hash_weight.restype = C.c_uint64
+    L.zo_hash_weight.argtypes = [C.c_uint64]
+    L.zo_run_hashes.restype = C.c_int64
+    L.zo_run_hashes.argtypes = [C.c_void_p, C.c_uint64, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+                                C.c_void_p]
     return L
 
 
@@ -134,3 +139,21 @@ def run_batch(builder, seed0, n_envs, steps, n_discrete, threads=1):
     n = lib().zo_run_batch(C.cast(builder.ptr(), C.c_void_p), seed0, n_envs, steps, n_discrete, threads,
                            C.byref(csum))
     return int(n), int(csum.value)
+
+
+def hash_weights(idx):
+    """zo_hash_weight(i) for every i of `idx` (uint64 array)."""
+    L = lib()
+    return np.array([L.zo_hash_weight(int(i)) for i in idx], dtype=np.uint64)
+
+
+HASH_R, HASH_D = 1 << 20, 1 << 21  # weight offsets of rewards / done, truncated, autoreset (zs_oracle.c)
+
+
+def run_hashes(builder, seed0, n_envs, steps, n_discrete, threads=0, reset_twice_mod=0):
+    """Per env and step output hashes of the bench workload: uint64 [n_envs, steps + 1]
+    (column 0 = the reset observation), see zo_run_hashes."""
+    out = np.zeros((n_envs, steps + 1), dtype=np.uint64)
+    lib().zo_run_hashes(C.cast(builder.ptr(), C.c_void_p), seed0, n_envs, steps, n_discrete, threads,
+                        reset_twice_mod, out.ctypes.data)
+    return out

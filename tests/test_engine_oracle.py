@@ -1,9 +1,10 @@
 """HIP engine vs the C oracle on many seeded envs (bit-exact), through the C ABI.
 
-Covers the configs of BASELINE.json at reduced env counts (the oracle finishes
-them in seconds) plus bots / rules / encodings the golden fixtures touch only
-briefly.  Full-size runs are checked by size-independent properties in
-test_engine_props.py.
+Covers the configs of BASELINE.json at reduced env counts, step by step with
+full observations and periodic state, plus bots / rules / encodings the golden
+fixtures touch only briefly.  The configs at the sizes bench.py times them
+(4 096 .. 65 536 envs) are checked every env and every step in
+test_fullsize_parity.py.
 """
 import numpy as np
 import pytest

@@ -1,0 +1,156 @@
+"""Parity of the timed path at the sizes it is timed (BASELINE.json configs C2..C5).
+
+`bench.py` replays the step as a hipGraph (`zs_step_graph`: on-device discrete policy +
+reset work + tick + observations) over 4 096 .. 65 536 envs.  At those sizes the persistent
+observation kernels walk many envs per wave (C3: 32 per wave, with the next env prefetched
+into registers), `k_reset` grid-strides over the pending list / mask, and the graph replays
+both pending-list parities.  Every env and every step is compared with the oracle
+(`oracle/zs_oracle.c`, the restatement of `zombsole/core.py:72-78` World.step and its env
+glue) through 64-bit per-env step hashes of obs, listed rewards, done/truncated and the
+autoreset flag (`tests/parity_hash.py`; the hash itself is pinned on the CPU by
+`tests/test_parity_hash.py`).  At the end, the full canonical state of envs at every
+wave-stride residue is compared with an oracle replay.
+"""
+import numpy as np
+import pytest
+
+from libzombsole_amd import _abi
+from libzombsole_amd.actions import DISCRETE_TRIPLES, discrete_action_id
+
+pytestmark = pytest.mark.gpu
+
+
+def c3(n, max_steps=1000):
+    return _abi.multi_env_config(n, "extermination", [], "bridge64", ["0", "1"], initial_zombies=10,
+                                 minimum_zombies=0, max_episode_steps=max_steps)
+
+
+def c4(n):
+    return _abi.multi_env_config(n, "safehouse", [], "city128", ["0", "1", "2", "3"], initial_zombies=50,
+                                 minimum_zombies=50, max_episode_steps=1000)
+
+
+def c5(n, max_steps=1000):
+    return _abi.multi_env_config(n, "extermination", [], "bridge64", ["0", "1", "2", "3"], initial_zombies=20,
+                                 minimum_zombies=0, max_episode_steps=max_steps, obs_dtype=_abi.DTYPE_I16)
+
+
+def spot_envs(n):
+    """Envs at every wave-stride position the persistent kernels use (256 CUs x 1..4 workgroups x
+    4 waves: strides 1024 .. 4096), plus both ends."""
+    s = {0, 1, 63, 64, n - 1, n - 2}
+    for stride in (1024, 2048, 4096):
+        for base in (0, 5, stride - 1):
+            for k in (1, 2, 7, 15):
+                e = base + k * stride
+                if e < n:
+                    s.add(e)
+    return sorted(e for e in s if 0 <= e < n)
+
+
+def oracle_state(make_builder, seed, steps, nd, twice):
+    from oracle.oracle import OracleEnv
+    o = OracleEnv(make_builder(1))
+    o.seed(seed)
+    o.reset()
+    if twice:
+        o.reset()
+    need = False
+    for t in range(1, steps + 1):
+        if need:
+            o.reset()
+            need = False
+            continue
+        acts = np.stack([DISCRETE_TRIPLES[discrete_action_id(seed, t, a, nd)] for a in range(o.A)])
+        _, _, d, tr, _ = o.step(acts)
+        need = d or tr
+    return o.state()
+
+
+def run_full(make_builder, n, steps, nd=7, seed0=0, graph=True, twice=0, min_resets=1):
+    import torch
+
+    from libzombsole_amd.engine import Engine
+    from oracle.oracle import run_hashes
+    from parity_hash import StepHasher
+
+    eng = Engine(make_builder(n))
+    eng.seed([seed0 + i for i in range(n)])
+    eng.reset()
+    if twice:  # a masked reset of every twice-th env (zs_reset mask mode over the whole grid)
+        mask = (torch.arange(n, device=eng.device) % twice == 1).to(torch.uint8)
+        eng.reset(mask)
+    hs = StepHasher(eng)
+    got = np.zeros((n, steps + 1), dtype=np.uint64)
+    got[:, 0] = hs.obs_hash().cpu().numpy().view(np.uint64)
+    resets = 0
+    for t in range(1, steps + 1):
+        if graph:
+            eng.step_graph(t, nd)
+        else:
+            eng.gen_actions(t, nd)
+            eng.step()
+        got[:, t] = hs.step_hash().cpu().numpy().view(np.uint64)
+        resets += int(eng.was_reset.sum().item())
+    exp = run_hashes(make_builder(1), seed0, n, steps, nd, threads=0, reset_twice_mod=twice)
+    bad = np.argwhere(got != exp)
+    assert bad.size == 0, "%d of %d env-steps differ; first (env, step): %s" % (
+        len(bad), got.size, bad[:12].tolist())
+    assert resets >= min_resets, ("too few autoresets to cover the reset path", resets)
+    kinds = [o[2] for o in eng.builder.map.obstacles]
+    for e in spot_envs(n):
+        exp_state = oracle_state(make_builder, seed0 + e, steps, nd, twice and e % twice == 1)
+        assert eng.get_state(e).canonical(kinds) == exp_state, ("state", e)
+    eng.close()
+    return resets
+
+
+def test_c3_65536_graph():
+    """The headline (BASELINE metric, C3 at N=1): 65 536 envs, k_obs_lds walking 32 envs per wave."""
+    run_full(c3, 65536, 40)
+
+
+def test_c3_65536_truncation_waves():
+    """TimeLimit 16: every env truncates at steps 16 and 33 -> 65 536-env autoreset waves (k_reset list
+    mode grid-striding far past 2 048 pending envs), plus a masked reset of 21 846 envs before step 1."""
+    r = run_full(lambda n: c3(n, max_steps=16), 65536, 40, twice=3, min_resets=2 * 65536)
+    assert r >= 2 * 65536
+
+
+def test_c2_4096_graph():
+    run_full(c3, 4096, 60, seed0=4242)
+
+
+def test_c2_4096_one_obs_workgroup_per_cu(monkeypatch):
+    """ZS_OBS_WGS=1: the persistent observation kernel at 1 workgroup per CU walks 4 envs per wave at 4 096."""
+    monkeypatch.setenv("ZS_OBS_WGS", "1")
+    monkeypatch.setenv("ZS_OBS_LDS", "1")
+    run_full(c3, 4096, 40, seed0=99)
+
+
+def test_c2_4096_one_obs_workgroup_per_cu_cells(monkeypatch):
+    """The same walk through k_obs_pipe's per-cell stores."""
+    monkeypatch.setenv("ZS_OBS_WGS", "1")
+    monkeypatch.setenv("ZS_OBS_LDS", "0")
+    run_full(c3, 4096, 40, seed0=7)
+
+
+def test_c5_65536_int16_graph():
+    """C5's engine side: 4 agents + 20 zombies, int16 observations (the gathered form)."""
+    run_full(c5, 65536, 32, min_resets=0)
+
+
+def test_c5_65536_int16_truncation_waves():
+    """C5 with TimeLimit 12: 65 536-env autoreset waves at steps 12 and 25 (int16 reset observations)
+    and a masked reset of every 4th env before step 1."""
+    run_full(lambda n: c5(n, max_steps=12), 65536, 30, twice=4, min_resets=2 * 65536)
+
+
+def test_c4_16384_graph():
+    """C4: city128 safehouse, 4 agents + 50 zombies (minimum 50): k_obs_gather and k_respawn."""
+    run_full(c4, 16384, 30, min_resets=0)
+
+
+def test_c3_8192_shard_eager():
+    """The N=8 shard size (8 192 envs per GPU) through per-kernel launches (zs_step), env range of rank 3."""
+    run_full(c3, 8192, 40, seed0=3 * 8192, graph=False)

@@ -4,7 +4,8 @@ Envs are independent and env i is seeded base+i, so a node's results must not de
 how envs are split over ranks: each rank runs its `shard_range` of the bench workload
 through the C oracle (test infrastructure) and the all-reduced checksum must equal the
 single-rank run.  The optional observation gather (`gather_observations`) is checked with
-rank-tagged tensors.
+rank-tagged tensors, on shards of unequal size (25 envs over 2 ranks: 13 + 12), and C5's
+per-step `StepGather` (rewards / done / truncated packed beside the observations) likewise.
 """
 import os
 import socket
@@ -30,7 +31,7 @@ def _builder():
                                  max_episode_steps=1000, obs_dtype=_abi.DTYPE_I64)
 
 
-TOTAL, STEPS = 24, 60
+TOTAL, STEPS = 25, 60
 
 
 def _worker(rank, world, port, q):
@@ -44,10 +45,22 @@ def _worker(rank, world, port, q):
         cnt, csum = run_batch(_builder(), e0, n, STEPS, 7, threads=1)
         parts = [None] * world
         dist.all_gather_object(parts, (cnt, csum))
+        from libzombsole_amd.vector import StepGather
         obs = torch.full((n, 2, 3, 5, 5), rank, dtype=torch.int32)
         g = gather_observations(obs)
+        # a stand-in engine (CPU tensors) for the per-step exchange
+        gl = torch.arange(e0, e0 + n)
+        fake = type("E", (), dict(N=n, device=torch.device("cpu"), obs=obs + 10 * gl.view(-1, 1, 1, 1, 1).int(),
+                                  rewards=(gl.double() / 4).view(-1, 1).repeat(1, 2),
+                                  done=(gl % 2).to(torch.uint8), trunc=(gl % 3 == 0).to(torch.uint8)))
+        sg = StepGather(fake)
+        sg()
+        ok = (torch.equal(sg.obs()[:, 0, 0, 0, 0], torch.arange(TOTAL).int() * 10 + (torch.arange(TOTAL) >= 13).int())
+              and torch.equal(sg.rewards()[:, 1], torch.arange(TOTAL).double() / 4)
+              and torch.equal(sg.done(), (torch.arange(TOTAL) % 2).to(torch.uint8))
+              and torch.equal(sg.truncated(), (torch.arange(TOTAL) % 3 == 0).to(torch.uint8)))
         if rank == 0:
-            q.put((sum(c for c, _ in parts), sum(s for _, s in parts) % (1 << 64), g[:, 0, 0, 0, 0].tolist()))
+            q.put((sum(c for c, _ in parts), sum(s for _, s in parts) % (1 << 64), g[:, 0, 0, 0, 0].tolist(), ok))
     finally:
         dist.destroy_process_group()
 
@@ -65,7 +78,8 @@ def test_two_rank_shards_match_single_rank():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    cnt2, csum2, tags = res
+    cnt2, csum2, tags, ok = res
     assert cnt2 == cnt1 == TOTAL * STEPS
     assert csum2 == csum1  # checksums add over envs (oracle/zs_oracle.c zo_run_batch)
-    assert tags == [0] * 12 + [1] * 12
+    assert tags == [0] * 13 + [1] * 12
+    assert ok

@@ -1,0 +1,93 @@
+"""Env sharding and the RCCL exchange on one MI355X.
+
+- Two engine handles owning global env ranges [0, N/2) and [N/2, N) (seeds = global index, as
+  bench.py's ranks do) produce exactly the observations, rewards and flags of one handle over
+  [0, N): trajectories do not depend on how the envs are split over GPUs.
+- A world_size-1 RCCL ("nccl") process group runs `gather_observations` and C5's per-step
+  `StepGather` (the bench's pack + all-gather) on the engine's device tensors; the gathered
+  tensors equal the local ones.
+"""
+import os
+import socket
+
+import pytest
+
+from libzombsole_amd import _abi
+
+pytestmark = pytest.mark.gpu
+
+
+def _c2(n):
+    return _abi.multi_env_config(n, "extermination", [], "bridge64", ["0", "1"], initial_zombies=10,
+                                 minimum_zombies=0, max_episode_steps=25)
+
+
+def _c5(n):
+    return _abi.multi_env_config(n, "extermination", [], "bridge64", ["0", "1", "2", "3"], initial_zombies=20,
+                                 minimum_zombies=0, max_episode_steps=1000, obs_dtype=_abi.DTYPE_I16)
+
+
+@pytest.mark.parametrize("total", [4096, 4097])
+def test_two_handles_equal_one(total):
+    import torch
+
+    from libzombsole_amd.engine import Engine
+    from libzombsole_amd.vector import shard_range
+
+    whole = Engine(_c2(total))
+    whole.seed(list(range(total)))
+    whole.reset()
+    parts = []
+    for r in range(2):
+        e0, n = shard_range(total, r, 2)
+        eng = Engine(_c2(n))
+        eng.seed([e0 + i for i in range(n)])
+        eng.reset()
+        parts.append(eng)
+    for t in range(1, 61):  # TimeLimit 25: two autoreset waves
+        for eng in [whole] + parts:
+            eng.step_graph(t, 7)
+        torch.cuda.synchronize()
+        for name in ("obs", "rewards", "done", "trunc", "listed", "was_reset"):
+            cat = torch.cat([getattr(p, name) for p in parts], dim=0)
+            assert torch.equal(cat, getattr(whole, name)), (name, t)
+    for eng in [whole] + parts:
+        eng.close()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_rccl_world1_gather():
+    import torch
+    import torch.distributed as dist
+
+    from libzombsole_amd.engine import Engine
+    from libzombsole_amd.vector import StepGather, gather_observations
+
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % _free_port(), rank=0, world_size=1,
+                            device_id=dev)
+    try:
+        assert dist.get_backend() == "nccl"
+        eng = Engine(_c5(2048))
+        eng.seed(list(range(2048)))
+        eng.reset()
+        g = StepGather(eng)
+        for t in range(1, 6):
+            eng.step_graph(t, 7)
+            g()
+            torch.cuda.synchronize()
+            assert torch.equal(g.obs(), eng.obs)
+            assert torch.equal(g.rewards(), eng.rewards)
+            assert torch.equal(g.done(), eng.done)
+            assert torch.equal(g.truncated(), eng.trunc)
+            assert torch.equal(gather_observations(eng.obs), eng.obs)
+        eng.close()
+    finally:
+        dist.destroy_process_group()
