@@ -91,6 +91,11 @@ extern "C" {
 #define ZS_ACT_HEAL 4
 #define ZS_ACT_HEAL_CLOSEST 5
 #define ZS_ACT_CONFUSED 6
+/* the agent's next_step raises (a debug=True env, core.py:96-99): World.step has advanced t and
+ * taken the decisions of the actors before this one in dict order (their RNG draws included), then
+ * stops; the env's state is otherwise unchanged and that step reports reward 0, not done, not
+ * truncated (the drop-ins re-raise the agent's exception) */
+#define ZS_ACT_RAISE 7
 
 /* ---- env surface / observation ------------------------------------------ */
 #define ZS_REWARD_SINGLE 0 /* AgentRewards, include_life_in_reward=True (gym/reward.py:19-47) */
@@ -221,6 +226,9 @@ int zs_profile_read(zs_handle* h, double out[8]);
  * observation kernel, fused / side-stream reset work, deferred respawn) as a one-line JSON
  * object, NUL-terminated and truncated to len bytes.  Returns ZS_OK. */
 int zs_describe(zs_handle* h, char* buf, int32_t len);
+/* Diagnostics: out[0], out[1] = the two pending-reset list counts, out[2] = the deferred-respawn
+ * count (after everything queued on stream), out[3] = the list parity the next step drains. */
+int zs_debug_lists(zs_handle* h, int32_t out[4], void* stream);
 /* Diagnostic builds compiled with -DZS_STAMPS only (the product .so returns ZS_ESTATE):
  * per-phase k_tick cycle sums / maxima over all workgroup launches since the last call. */
 int zs_debug_stamps(zs_handle* h, uint64_t* sum_out, uint64_t* max_out, int32_t n);
@@ -230,7 +238,9 @@ int zs_debug_stamps(zs_handle* h, uint64_t* sum_out, uint64_t* max_out, int32_t 
  *   [3]  episode_steps        [4] n_order (things with ask_for_actions + ... present, dict order)
  *   [5]  needs_reset          [6] n_entities (E)    [7] n_obstacles (O)
  *   [8]  width                [9] height            [10] reward prev zombie_deaths
- *   [11] n_zombies_present    [12..15] reserved
+ *   [11] n_zombies_present    [12] spawn serial counter [13..15] reserved
+ *   zs_set_state restores every field except [5] (pending resets stay the engine's) and the
+ *   read-only [6..9], [11]
  *   [16 .. 16+8E)  entity records: kind, present, x, y, life, weapon, extra, spawn_serial
  *                  (slots: agents [0,A), bots [A,A+P), zombies [A+P,E))
  *   [.. +E)        order: entity slot ids in dict order (first n_order valid)

@@ -14,7 +14,7 @@ import random
 import numpy as np
 
 from . import _abi
-from .actions import ActionError, encode_action
+from .actions import ACT_RAISE, ActionError, encode_action
 from .engine import Engine
 from .game import GameView
 
@@ -42,19 +42,35 @@ class EnvCore(object):
 
     def encode(self, action):
         """Agent.next_step's parse of one action dict; errors as World.get_actions treats them
-        (core.py:96-99): re-raised with debug, otherwise the agent idles."""
+        (core.py:96-99): with debug the agent's action becomes ZS_ACT_RAISE (the tick stops there
+        and `tick` re-raises the exception), otherwise the agent idles."""
         try:
             return encode_action(action)
         except ActionError as err:
             if self.debug:
-                raise err.args[0]
+                return err
             return (0, 0, 0)
 
     def tick(self, triples):
         """One World.step + env glue for the single engine env; returns host copies of
-        (obs[n_obs, C, H, W], rewards[A], done, truncated)."""
+        (obs[n_obs, C, H, W], rewards[A], done, truncated).
+
+        An entry of `triples` may be the ActionError `encode` returned for a debug env: the engine
+        then runs World.step up to the first such agent in dict order — t += 1 and the decisions
+        (RNG draws included) of the actors before it — and this re-raises that agent's exception,
+        as the reference's World.step does (core.py:72-78, 96-99).  Agents that are not in the
+        world are never asked for an action, so their errors do not raise."""
         eng = self.engine
-        self._host_actions[0, :len(triples)] = np.asarray(triples, dtype=np.int32).reshape(-1, 3)
+        errors = {i: t for i, t in enumerate(triples) if isinstance(t, ActionError)}
+        raising = None
+        if errors:
+            st = eng.get_state(0)
+            for slot in st.order[:st.n_order]:
+                if int(slot) in errors:
+                    raising = errors[int(slot)]
+                    break
+        rows = [(ACT_RAISE, 0, 0) if isinstance(t, ActionError) else t for t in triples]
+        self._host_actions[0, :len(rows)] = np.asarray(rows, dtype=np.int32).reshape(-1, 3)
         eng.actions.copy_(self.torch.from_numpy(self._host_actions))
         eng.load_python_random(0)
         try:
@@ -62,6 +78,8 @@ class EnvCore(object):
         finally:
             eng.store_python_random(0)
             self.game.invalidate()
+        if raising is not None:
+            raise raising.args[0]
         obs = eng.obs[0].cpu().numpy()
         rew = eng.rewards[0].cpu().numpy()
         return obs, rew, bool(eng.done[0].item()), bool(eng.trunc[0].item())

@@ -21,6 +21,7 @@ ACT_ATTACK_CLOSEST = 3  # closest zombie in dict order                  (agent.p
 ACT_HEAL = 4            # self if parameter falsy/(0,0) else Player/Box/Wall at pos+parameter (agent.py:59-75)
 ACT_HEAL_CLOSEST = 5    # closest other Player, else self               (agent.py:76-88)
 ACT_CONFUSED = 6        # unknown action_type -> None                   (agent.py:89-91)
+ACT_RAISE = 7           # next_step raises (debug=True): World.step stops at this actor (core.py:96-99)
 
 _KIND_BY_NAME = {
     "move": ACT_MOVE,
@@ -61,14 +62,26 @@ class ActionError(Exception):
     """An action the reference's Agent.next_step would raise on."""
 
 
+def _target_offset(param):
+    """The offset `Agent.next_step` adds to the position, evaluated as the reference does
+    (``self.position[0] + self.action_parameter[0]``, agent.py:36-37 / 51-52 / 67-68), so a bad
+    parameter raises the reference's own exception (None -> TypeError, short -> IndexError,
+    str -> TypeError)."""
+    try:
+        ox, oy = 0 + param[0], 0 + param[1]
+        return int(ox), int(oy)
+    except Exception as err:
+        raise ActionError(err)
+
+
 def encode_action(action):
     """Map one reference action dict to an engine triple.
 
-    Mirrors the branches of `Agent.next_step` (`zombsole/players/agent.py:28-96`).
-    Raises ActionError (carrying the exception the reference would raise) for
-    inputs on which the reference raises inside next_step; the caller decides,
-    like `World.get_actions` (`core.py:96-99`), whether to re-raise (debug) or
-    to treat the agent as idle.
+    Mirrors the branches of `Agent.next_step` (`zombsole/players/agent.py:28-96`), in its order
+    of evaluation.  Raises ActionError (carrying the exception the reference would raise) for
+    inputs on which the reference raises inside next_step; the caller decides, like
+    `World.get_actions` (`core.py:96-99`), whether to re-raise (debug) or to treat the agent as
+    idle.
     """
     atype = action.get("action_type", None)
     param = action.get("parameter", None)
@@ -76,24 +89,16 @@ def encode_action(action):
         return (ACT_IDLE, 0, 0)
     kind = _KIND_BY_NAME.get(atype, ACT_CONFUSED) if isinstance(atype, str) else ACT_CONFUSED
     if kind in (ACT_MOVE, ACT_ATTACK):
-        try:
-            dx, dy = int(param[0]), int(param[1])
-        except Exception as err:  # None, short sequence...
-            raise ActionError(err)
+        dx, dy = _target_offset(param)
         return (kind, dx, dy)
     if kind == ACT_HEAL:
-        try:
-            falsy = not param
-        except Exception as err:  # e.g. numpy array truth value (agent.py:61)
+        try:  # (not param) or (tuple(param) == (0, 0))  (agent.py:61)
+            self_heal = (not param) or (tuple(param) == (0, 0))
+        except Exception as err:  # numpy truth value, tuple(int)...
             raise ActionError(err)
-        if falsy:
+        if self_heal:
             return (ACT_HEAL, 0, 0)
-        try:
-            dx, dy = int(param[0]), int(param[1])
-        except Exception as err:
-            raise ActionError(err)
-        if tuple(param) == (0, 0):
-            return (ACT_HEAL, 0, 0)
+        dx, dy = _target_offset(param)
         return (ACT_HEAL, dx, dy)
     return (kind, 0, 0)
 
@@ -134,3 +139,17 @@ def rich_action(seed, step, agent):
     dx = int((h >> 8) % 5) - 2
     dy = int((h >> 16) % 5) - 2
     return {"action_type": atype, "parameter": [dx, dy]}
+
+
+BAD_PARAMETERS = [None, [1], 5, ["a", 1]]
+
+
+def bad_action(seed, step, agent):
+    """rich_action, with one in eight actions carrying a parameter on which Agent.next_step raises
+    for move / attack / heal (None, a short list, an int, a str coordinate: agent.py:36-68)."""
+    act = rich_action(seed, step, agent)
+    h = action_hash(seed ^ 0x5A5A, step, agent)
+    if h % 8 == 0:
+        act = {"action_type": ("move", "attack", "heal")[(h >> 3) % 3],
+               "parameter": BAD_PARAMETERS[(h >> 5) % len(BAD_PARAMETERS)]}
+    return act

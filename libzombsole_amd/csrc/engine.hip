@@ -107,7 +107,7 @@ __global__ void k_gen_actions(Dev d, uint64_t step, int n_discrete, int32_t* act
 // The work-list counters a step appends to; inside zs_step_graph's graph also the policy's step
 // counter, advanced here, after k_gen_actions_dev (earlier in the same stream) has read it.
 __global__ void k_zero2(int* a, int* b, uint64_t* step) {
-    if (threadIdx.x == 0) *a = 0;
+    if (threadIdx.x == 0 && a) *a = 0;
     if (threadIdx.x == 1 && b) *b = 0;
     if (threadIdx.x == 2 && step) *step += 1;
 }
@@ -151,7 +151,8 @@ __global__ void k_get_state(Dev d, int e, int32_t* buf) {
     int nz = 0;
     for (int s = d.A + d.P; s < E; s++) nz += d.present[(size_t)s * N + e];
     b[11] = nz;
-    b[12] = b[13] = b[14] = b[15] = 0;
+    b[12] = d.scal[S_SERIAL * N + e];
+    b[13] = b[14] = b[15] = 0;
     int32_t* r = b + ZS_STATE_HEADER;
     for (int s = 0; s < E; s++, r += ZS_STATE_ENTITY_WORDS) {
         int32_t p = d.pos[(size_t)s * N + e];
@@ -181,8 +182,11 @@ __global__ void k_set_state(Dev d, int e, const int32_t* buf) {
     d.scal[S_ZD * N + e] = b[2];
     d.scal[S_EPSTEPS * N + e] = b[3];
     d.scal[S_NORDER * N + e] = b[4];
-    d.scal[S_NEEDRESET * N + e] = b[5];
+    // b[5] (needs_reset) is not restored: pending resets are the engine's own work lists (an env on
+    // the list with the flag cleared would be reset and ticked by the same call, one off it with the
+    // flag set would report a reset without a rebuild)
     d.scal[S_PREVZD * N + e] = b[10];
+    d.scal[S_SERIAL * N + e] = b[12];
     const int32_t* r = b + ZS_STATE_HEADER;
     for (int s = 0; s < E; s++, r += ZS_STATE_ENTITY_WORDS) {
         d.present[(size_t)s * N + e] = (uint8_t)r[1];
@@ -208,21 +212,6 @@ __global__ void k_set_state(Dev d, int e, const int32_t* buf) {
     for (int a = 0; a < d.A; a++) d.prev_life[(size_t)a * N + e] = *r++;
     for (int a = 0; a < d.A; a++) d.listed[(size_t)a * N + e] = (uint8_t)*r++;
     for (int w = 0; w < d.DW; w++) d.dead[(size_t)e * d.DW + w] = (uint32_t)*r++;
-    // rebuild the occupancy bitmap: present obstacles and present entities
-    uint32_t* bm = d.occ_bits + (size_t)e * d.DW;
-    for (int w = 0; w < d.DW; w++) bm[w] = 0;
-    for (int o = 0; o < d.O; o++)
-        if ((d.obst_present[(size_t)e * d.OW + (o >> 5)] >> (o & 31)) & 1u) {
-            int32_t p = d.obst_xy[o];
-            int cell = unpack_y(p) * d.W + unpack_x(p);
-            bm[cell >> 5] |= 1u << (cell & 31);
-        }
-    for (int s = 0; s < E; s++)
-        if (d.present[(size_t)s * N + e]) {
-            int32_t p = d.pos[(size_t)s * N + e];
-            int cell = unpack_y(p) * d.W + unpack_x(p);
-            bm[cell >> 5] |= 1u << (cell & 31);
-        }
 }
 
 __global__ void k_init_pending(Dev d, int* list, int* count) {
@@ -279,6 +268,7 @@ struct zs_handle {
     const void* gkey[8] = {};
     uint64_t* d_gstep = nullptr;  // [0] policy step counter (k_gen_actions_dev reads, k_zero2 advances)
     int capturing = 0;            // zs_step is being captured by zs_step_graph
+    int memset_nodes = 0;         // ZS_GRAPH_MEMSET=1: list counters zeroed by hipMemsetAsync (diagnostic)
     // step pipeline: the tick in `chunks` env ranges on the caller's stream, each range's observations
     // on s_obs as soon as its tick is done
     int chunks = 1;
@@ -625,7 +615,6 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
     TRY(dalloc(h, &d.obst_hp, (size_t)d.O * N));
     TRY(dalloc(h, &d.obst_present, (size_t)d.OW * N));
     TRY(dalloc(h, &d.obst_nonpos, (size_t)d.OW * N));
-    TRY(dalloc(h, &d.occ_bits, (size_t)d.DW * N));
     TRY(dalloc(h, &d.dead, (size_t)d.DW * N));
     TRY(dalloc(h, &d.ring, (size_t)ZS_RING_WORDS * N));
     TRY(dalloc(h, &d.rngst, N));
@@ -677,16 +666,17 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
         }
         // k_obs_lds: the same walk with each observation block staged in LDS and streamed out as 16-B
         // stores (channels encoding).  Measured on one MI355X: int16 blocks (C5) 341 -> 264 us per
-        // launch at 4 workgroups per CU (2: 334, 3: 278, 5: 307); int64 blocks at 2 per CU win only
-        // when every wave walks many envs (C3 65536 envs: 351 -> 335 us; 32768: even; 8192, one env
-        // per wave: 33 vs 36 us for k_obs_pipe).  ZS_OBS_LDS=0/1 forces either.
+        // launch at 4 workgroups per CU (2: 334, 3: 278, 5: 307); int64 blocks (staged as int32) at
+        // up to 4 per CU.  It pays when every wave walks several envs (C3 65536 envs; at 8192, one env
+        // per wave, k_obs_pipe's per-cell stores measured 33 vs 36 us).  ZS_OBS_LDS=0/1 forces either,
+        // ZS_OBS_WGS sets the workgroups per CU.
         if (h->obs_pipe && d.obs_enc == ZS_ENC_CHANNELS && !getenv_off("ZS_OBS_LDS")) {
             const int ts = d.obs_dtype == ZS_DTYPE_I64 ? 8 : d.obs_dtype == ZS_DTYPE_I32 ? 4 : 2;
-            const size_t lb = (size_t)d.obs_stat * 4 + 4 * ((size_t)L.bytes + (size_t)obs_lds_slot_bytes(ts));
+            const size_t lb = (size_t)d.obs_stat * 4 + 4 * ((size_t)L.bytes + (size_t)obs_stage_slot_bytes(ts));
             int wgs = std::max(1, std::min(ts == 8 ? 2 : 4, (int)(160 * 1024 / lb)));
             if (getenv("ZS_OBS_WGS")) wgs = std::max(1, std::min(32, atoi(getenv("ZS_OBS_WGS"))));
             const bool forced = getenv("ZS_OBS_LDS") != nullptr;
-            const bool pays = ts < 8 || (long)d.N >= 24L * 256 * wgs * 4;
+            const bool pays = ts < 8 || (long)d.N >= 24L * 256 * 2 * 4;
             if (lb <= 64 * 1024 && (pays || forced)) {
                 h->obs_lds = 1;
                 h->obs_lds_bytes = lb;
@@ -757,6 +747,7 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
             if (h->chunks > 1 && hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) != hipSuccess) h->chunks = 1;
         }
     }
+    h->memset_nodes = getenv("ZS_GRAPH_MEMSET") && atoi(getenv("ZS_GRAPH_MEMSET")) != 0;
     // side-stream reset work (unfused steps; ZS_RESET_STREAM=0 keeps it on the caller's stream)
     if (!h->fused && !getenv_off("ZS_RESET_STREAM")) {
         h->reset_side = hipStreamCreateWithFlags(&h->s_reset, hipStreamNonBlocking) == hipSuccess &&
@@ -1009,7 +1000,7 @@ extern "C" int zs_reset(zs_handle* h, const uint8_t* env_mask_dev, void* obs_dev
             HIPCHK(hipMemsetAsync(h->d_rcount + q, 0, sizeof(int), s));
             hipLaunchKernelGGL(k_list_filter, dim3(std::min(64, (h->d.N + 255) / 256)), dim3(256), 0, s,
                                (const int*)h->d_rlist[p], (const int*)(h->d_rcount + p), h->d_rlist[q],
-                               h->d_rcount + q, env_mask_dev);
+                               h->d_rcount + q, env_mask_dev, h->d.N);
             HIPCHK(hipGetLastError());
             h->rpar = q;
         }
@@ -1055,10 +1046,21 @@ extern "C" int zs_step(zs_handle* h, const int32_t* actions_dev, void* obs_dev, 
         if (side) HIPCHK(hipEventRecord(h->ev_rjoin, h->s_reset));
     }
     // 2) tick every other env; envs that end now are queued on list[q] for the next call
-    // the work-list counters this call appends to: one tiny kernel instead of one memset each (a
-    // 4-byte hipMemsetAsync captured into zs_step_graph's graph faulted on replay, ROCm 7.2)
-    hipLaunchKernelGGL(k_zero2, dim3(1), dim3(64), 0, s, h->d_rcount + q, h->d.defer_respawn ? h->d.resp_count : nullptr,
-                       h->capturing ? h->d_gstep : nullptr);
+    // The work-list counters this call appends to are zeroed by k_zero2, which inside zs_step_graph's
+    // graph also advances the policy step.  Captured 4-byte hipMemsetAsync nodes (ZS_GRAPH_MEMSET=1,
+    // diagnostic) wrote byte patterns instead of zero into these counters, constant per instantiated
+    // graph (0x01010101 / 0x05050505 / 0xC0C0C0C0: profiles/r02_graph_memset_city128.log, from
+    // tools/debug/graph_memset.py); the pending-reset list indexed by such a count was the round-1
+    // replay fault.  Standalone graphs of the same node shapes zero correctly
+    // (profiles/r02_graphprobe_memset.log).  Every list index is bounds-checked in the kernels.
+    if (h->memset_nodes) {
+        HIPCHK(hipMemsetAsync(h->d_rcount + q, 0, sizeof(int), s));
+        if (h->d.defer_respawn) HIPCHK(hipMemsetAsync(h->d.resp_count, 0, sizeof(int), s));
+        if (h->capturing) hipLaunchKernelGGL(k_zero2, dim3(1), dim3(64), 0, s, nullptr, nullptr, h->d_gstep);
+    } else {
+        hipLaunchKernelGGL(k_zero2, dim3(1), dim3(64), 0, s, h->d_rcount + q, h->d.defer_respawn ? h->d.resp_count : nullptr,
+                           h->capturing ? h->d_gstep : nullptr);
+    }
     HIPCHK(hipGetLastError());
     const int K = (!h->fused && !h->d.fobs && obs_dev) ? h->chunks : 1;
     if (K > 1) {
@@ -1310,6 +1312,24 @@ extern "C" int zs_describe(zs_handle* h, char* buf, int32_t len) {
              "\"reset_lds\": %zu, \"respawn\": \"%s\", \"chunks\": %d}",
              d.N, d.E, h->G, h->fused ? "k_step" : "k_tick", h->lds, h->resident, d.rw_cap, obs_kernel, h->reset_side,
              h->reset_lds, d.defer_respawn ? "k_respawn" : "tick", h->chunks);
+    return ZS_OK;
+}
+
+// Diagnostics: the work-list counters as they stand after everything queued on `stream` (out[0..1]
+// the two pending-reset list counts, out[2] the deferred-respawn count, out[3] the parity the next
+// step drains).
+extern "C" int zs_debug_lists(zs_handle* h, int32_t* out, void* stream) {
+    if (!h || !out) return fail(ZS_EINVAL, "null argument");
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(hipSetDevice(h->device));
+    int v[3] = {0, 0, 0};
+    HIPCHK(hipMemcpyAsync(v, h->d_rcount, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(v + 2, h->d.resp_count, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    out[0] = v[0];
+    out[1] = v[1];
+    out[2] = v[2];
+    out[3] = h->rpar;
     return ZS_OK;
 }
 

@@ -6,10 +6,11 @@
 //       -> lanes touching the same slot of consecutive envs issue coalesced accesses.
 //   * per-env scalars [k][N] (World.t, deaths, zombie_deaths, ...), agent tracker [a][N].
 //   * env-major per-env blocks (a lane group walks its own env):
-//       occ_bits [N][DW] u32       occupancy bitmap: cell holds an entity or a present obstacle
 //       dead     [N][DW] u32       dead-body decoration bitmap
 //       obstacle hp [N][O] int32, present / nonpos bitmaps [N][OW] u32
 //       MT19937 ring [N][2][624] u32 (current block + precomputed next block)
+//   * no occupancy bitmap is stored: the step / respawn kernels rebuild it in LDS from the static
+//     obstacle bitmap, the env's obstacle-present bits and its things' positions.
 //   * static, shared by all envs: cellmap (cell -> obstacle index), obstacle occupancy bitmap,
 //     objective bitmap, obstacle xy/kind, spawn lists.
 #pragma once
@@ -116,7 +117,6 @@ struct Dev {
     int32_t* obst_hp;
     uint32_t* obst_present;
     uint32_t* obst_nonpos;
-    uint32_t* occ_bits;
     uint32_t* dead;
     uint32_t* ring;
     uint32_t* rngst;

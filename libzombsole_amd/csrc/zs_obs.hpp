@@ -352,15 +352,19 @@ struct ObsPrefetch {
 __device__ __forceinline__ void obs_prefetch(const Dev& d, int e, ObsPrefetch& f) {
     const int lane = threadIdx.x & 63, N = d.N;
     const int s = lane < d.E ? lane : d.E - 1;
-    f.pos = d.pos[(size_t)s * N + e];
-    f.life = d.life[(size_t)s * N + e];
-    f.wp = d.weapon[(size_t)s * N + e];
-    f.pr = d.present[(size_t)s * N + e];
-    const uint32_t* dr = d.dead + (size_t)e * d.DW;
+#ifndef ZS_OBS_DIAG
+#define ZS_OBS_DIAG 0
+#endif
+    const int ee = (ZS_OBS_DIAG & 4) ? 0 : e, ed = (ZS_OBS_DIAG & 2) ? 0 : e, eh = (ZS_OBS_DIAG & 1) ? 0 : e;
+    f.pos = d.pos[(size_t)s * N + ee];
+    f.life = d.life[(size_t)s * N + ee];
+    f.wp = d.weapon[(size_t)s * N + ee];
+    f.pr = d.present[(size_t)s * N + ee];
+    const uint32_t* dr = d.dead + (size_t)ed * d.DW;
 #pragma unroll
     for (int i = 0; i < OBS_PF_D; i++) f.dead[i] = dr[min(lane + 64 * i, d.DW - 1)];
-    f.opres = d.obst_present[(size_t)e * d.OW + min(lane, d.OW - 1)];
-    const int32_t* hr = d.obst_hp + (size_t)e * d.O;
+    f.opres = d.obst_present[(size_t)ed * d.OW + min(lane, d.OW - 1)];
+    const int32_t* hr = d.obst_hp + (size_t)eh * d.O;
 #pragma unroll
     for (int i = 0; i < OBS_PF_H; i++) f.hp[i] = hr[min(lane + 64 * i, d.O - 1)];
 }
@@ -442,6 +446,7 @@ __global__ void __launch_bounds__(256, ZS_OBS_PIPE_WAVES) k_obs_pipe(Dev d, T* o
 
 // 16-B store stream of one staged observation block (k_obs_lds, k_obs_gather<..., true>)
 typedef unsigned int zs_v4u __attribute__((ext_vector_type(4)));
+typedef unsigned int zs_v2u __attribute__((ext_vector_type(2)));
 
 // staging bytes per wave: one channels block at any 16-B phase of its destination
 __host__ __device__ constexpr int obs_lds_slot_bytes(int tsize) { return ((3 * 441 * tsize + 31) / 16) * 16; }
@@ -578,14 +583,83 @@ __global__ void __launch_bounds__(256) k_obs_gather(Dev d, T* out, const uint8_t
 // the destination's 16-B phase, and then streamed out as 16-B stores: every full 16-B chunk of the
 // block is one aligned global_store_dwordx4 (half the store instructions of per-cell int64 stores,
 // an eighth of int16 ones) and the stream carries no lookups between its stores; the partial chunks
-// at the block's two ends are element stores.  tools/probe/storebw.hip: this store shape 5.2 TB/s.
+// at the block's two ends are element stores.  tools/probe/storebw.hip: this store shape 6.0 TB/s.
+// The slot holds the values in the narrowest lossless type (obs_stage_t: int32 for int64 output —
+// every channel value is an int32: codes, lives, weapon codes), widened by the flush, so an int64
+// block stages in 5.3 KB instead of 10.6 KB and four workgroups (16 waves) fit a CU.
 // ---------------------------------------------------------------------------
+template <typename T> struct obs_stage { typedef T type; };
+template <> struct obs_stage<int64_t> { typedef int32_t type; };
+
+// staging bytes per wave: one channels block, shifted by the destination's 16-B phase in elements
+__host__ __device__ constexpr int obs_stage_slot_bytes(int tsize) {
+    return (((3 * 441 + 16 / tsize) * (tsize == 8 ? 4 : tsize) + 15) / 16) * 16;
+}
+
+// Stream one staged block to o: slot element k + mis / sizeof(T) holds output element k, so the
+// 16-B chunk q of the destination (counted from the 16-B boundary at or below o) reads the aligned
+// slot elements [q * VPC, (q + 1) * VPC).
+// Buffer-resource stores (raw buffer, gfx9 descriptor word 3): a lane whose offset is past the
+// resource's range is dropped by the hardware, so a masked store needs no branch.  Every flush is then
+// a fixed number of store instructions on every path, and the compiler's vmcnt waits for the next
+// env's prefetch loads (issued before these stores, completing in order) count them exactly instead
+// of assuming the shortest path and draining most of the stores still in flight.
+#define ZS_OOB 0x80000000u
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t zs_rsrc(void* base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(base, (short)0, (int)bytes, 0x00020000);
+}
+template <typename T>
+__device__ __forceinline__ void zs_buf_store(__amdgpu_buffer_rsrc_t r, uint32_t off, T v) {
+    if constexpr (sizeof(T) == 8) {
+        const uint64_t u = (uint64_t)v;
+        __builtin_amdgcn_raw_buffer_store_b64(zs_v2u{(uint32_t)u, (uint32_t)(u >> 32)}, r, (int)off, 0, 0);
+    } else if constexpr (sizeof(T) == 4) {
+        __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v, r, (int)off, 0, 0);
+    } else {
+        __builtin_amdgcn_raw_buffer_store_b16((unsigned short)v, r, (int)off, 0, 0);
+    }
+}
+
+// Stream one staged block to o: slot element k + mis / sizeof(T) holds output element k, so the
+// 16-B chunk q of the destination (counted from the 16-B boundary at or below o) reads the aligned
+// slot elements [q * VPC, (q + 1) * VPC).  The partial chunks at the two ends are element stores.
+template <typename T>
+__device__ __forceinline__ void obs_stage_flush(const lu8* slot, T* o, int lane) {
+    typedef typename obs_stage<T>::type S;
+    constexpr int TS = (int)sizeof(T), VPC = 16 / TS, NB = 3 * 441 * TS;
+    constexpr int NCH = (NB + 15 + 15) / 16;
+    const int mis = (int)((uintptr_t)o & 15), shift = mis / TS;
+    const ZS_LDS S* sv = (const ZS_LDS S*)slot;
+    const __amdgpu_buffer_rsrc_t r = zs_rsrc(o, NB);
+    const int nb = mis + NB, kend = nb >> 4, k0 = mis ? 1 : 0;
+#pragma unroll
+    for (int i = 0; i < (NCH + 63) / 64; i++) {
+        const int k = lane + 64 * i;
+        const int kr = k < kend ? k : kend - 1;
+        zs_v4u v;
+        if constexpr (TS == 8) {  // two int32 -> two int64
+            const zs_v2u w = *(const ZS_LDS zs_v2u*)(sv + kr * VPC);
+            v = zs_v4u{w.x, (uint32_t)((int32_t)w.x >> 31), w.y, (uint32_t)((int32_t)w.y >> 31)};
+        } else {
+            v = *(const ZS_LDS zs_v4u*)(sv + kr * VPC);
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)((k >= k0 && k < kend) ? (uint32_t)(16 * k - mis) : ZS_OOB), 0,
+                                               0);
+    }
+    const int nhead = mis ? (16 - mis) / TS : 0, tail0 = (16 * kend - mis) / TS, ntail = (nb - 16 * kend) / TS;
+    const int idx = lane < nhead ? lane : (lane >= 32 && lane - 32 < ntail) ? tail0 + lane - 32 : -1;
+    zs_buf_store<T>(r, idx >= 0 ? (uint32_t)(idx * TS) : ZS_OOB, (T)sv[(idx >= 0 ? idx : 0) + shift]);
+}
+
 template <typename T, int NOBS>
 __global__ void __launch_bounds__(256, ZS_OBS_PIPE_WAVES) k_obs_lds(Dev d, T* out, ObsLayout L, int env0, int env1) {
     extern __shared__ __align__(16) uint8_t smem[];
+    typedef typename obs_stage<T>::type S;
     constexpr int WW = 21, PLANE = WW * WW, PER = (PLANE + 63) / 64, TS = (int)sizeof(T);
-    constexpr int SLOT = obs_lds_slot_bytes(TS);
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    constexpr int SLOT = obs_stage_slot_bytes(TS);
+    // the wave index (hence the env and every block address) is wave-uniform: scalar registers, and
+    // the buffer resources of the flush need no waterfall loop
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int stat_words = 4 * d.DW;
     lu32* st = (lu32*)smem;
     obs_stage_static(d, st, threadIdx.x, blockDim.x);
@@ -602,10 +676,8 @@ __global__ void __launch_bounds__(256, ZS_OBS_PIPE_WAVES) k_obs_lds(Dev d, T* ou
     lu32* opres = (lu32*)(img + L.off_opres);
     li32* hp = (li32*)(img + L.off_hp);
     const int code_s = lane < d.A ? d.agent_codes[lane < d.A ? lane : 0] : (lane < d.A + d.P ? ZS_THING_PLAYER : ZS_THING_ZOMBIE);
-    ObsPrefetch f;
-    obs_prefetch(d, e, f);
-    for (; e < env1; e += waves) {
-        // the image of env e from the registers
+    // the image of an env from its prefetched registers
+    auto build = [&](const ObsPrefetch& f) {
         for (int w = lane; w < L.win / 4; w += 64) ((lu32*)img)[w] = 0u;
         if (lane < d.E) {
             pos[lane] = f.pos;
@@ -619,7 +691,12 @@ __global__ void __launch_bounds__(256, ZS_OBS_PIPE_WAVES) k_obs_lds(Dev d, T* ou
 #pragma unroll
         for (int i = 0; i < OBS_PF_H; i++)
             if (lane + 64 * i < d.O) hp[lane + 64 * i] = f.hp[i];
-        obs_prefetch(d, min(e + waves, env1 - 1), f);  // the next env (the last wave re-reads its own)
+    };
+    // Two envs of prefetch in flight: the loads of env e + 2 * waves are issued before the stores of
+    // env e and consumed after those of env e + waves, so a load has two envs' store streams to
+    // return in.  Between the loads and the wait for them everything is straight-line (agents
+    // unrolled, flush stores unconditional), so that wait leaves the stores in flight.
+    auto process = [&](int e) {
         wave_sync();
         // window map
         if (lane < d.E && ((cw[lane] >> 16) & 1)) {
@@ -633,14 +710,13 @@ __global__ void __launch_bounds__(256, ZS_OBS_PIPE_WAVES) k_obs_lds(Dev d, T* ou
             }
         }
         wave_sync();
-#pragma unroll 1
+#pragma unroll
         for (int a = 0; a < NOBS; a++) {
             const int32_t ap = pos[a];
             const int ox = unpack_x(ap) - WW / 2, oy = unpack_y(ap) - WW / 2;
             const lu8* wm = img + a * PLANE;
             T* o = out + ((size_t)e * NOBS + a) * 3 * PLANE;
-            const int mis = (int)((uintptr_t)o & 15);
-            ZS_LDS T* ot = (ZS_LDS T*)(slot + mis);
+            ZS_LDS S* ot = (ZS_LDS S*)slot + (int)((uintptr_t)o & 15) / TS;
 #pragma unroll
             for (int i = 0; i < PER; i++) {
                 const int cell = lane + 64 * i;
@@ -648,14 +724,30 @@ __global__ void __launch_bounds__(256, ZS_OBS_PIPE_WAVES) k_obs_lds(Dev d, T* ou
                 int code, lf, weapon;
                 obs_cell_fast(d, L, st, img, wm, cc, ox + q, oy + r, code, lf, weapon);
                 if (cell < PLANE) {
-                    ot[cell] = (T)code;
-                    ot[PLANE + cell] = (T)lf;
-                    ot[2 * PLANE + cell] = (T)weapon;
+                    ot[cell] = (S)code;
+                    ot[PLANE + cell] = (S)lf;
+                    ot[2 * PLANE + cell] = (S)weapon;
                 }
             }
             wave_sync();
-            obs_block_flush(slot, o, lane);
+            obs_stage_flush(slot, o, lane);
             wave_sync();
         }
+    };
+    ObsPrefetch fa, fb;
+    obs_prefetch(d, e, fa);
+    obs_prefetch(d, min(e + waves, env1 - 1), fb);
+    build(fa);
+    for (;;) {
+        obs_prefetch(d, min(e + 2 * waves, env1 - 1), fa);
+        process(e);
+        e += waves;
+        if (e >= env1) break;
+        build(fb);
+        obs_prefetch(d, min(e + 2 * waves, env1 - 1), fb);
+        process(e);
+        e += waves;
+        if (e >= env1) break;
+        build(fa);
     }
 }

@@ -205,7 +205,6 @@ __device__ __forceinline__ void reset_env_wave(const Dev& d, const ResetLds& L, 
         d.present[(size_t)s * N + e] = L.lpres[s];
         d.order[(size_t)s * N + e] = L.lorder[s];
     }
-    for (int w = lane; w < d.DW; w += 64) d.occ_bits[(size_t)e * d.DW + w] = L.bm[w];
     for (int a = lane; a < A; a += 64) {  // reward_tracker.reset / env.agents = possible_agents
         d.prev_life[(size_t)a * N + e] = L.llife[a];
         d.listed[(size_t)a * N + e] = 1;
@@ -266,7 +265,7 @@ __device__ __forceinline__ ResetLds reset_lds_carve(const Dev& d, uint8_t* smem)
 __device__ __forceinline__ void reset_role(const Dev& d, int list_mode, const int* list, const int* count,
                                            const uint8_t* mask, int* err_out, int wg, int nwg, void* obs_out) {
     extern __shared__ __align__(16) uint8_t smem[];
-    const int n = list_mode ? *count : d.N;
+    const int n = list_mode ? min(*count, d.N) : d.N;
     if (wg >= n) return;
     const ResetLds L = reset_lds_carve(d, smem);
     for (int idx = wg; idx < n; idx += nwg) {
@@ -304,7 +303,7 @@ __global__ void __launch_bounds__(64, ZS_STEP_WAVES) k_reset(Dev d, int list_mod
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void respawn_env_wave(const Dev& d, const ResetLds& L, int e) {
     const int lane = threadIdx.x, N = d.N, E = d.E, Z0 = d.A + d.P;
-    for (int w = lane; w < d.DW; w += 64) L.bm[w] = d.occ_bits[(size_t)e * d.DW + w];
+    for (int w = lane; w < d.DW; w += 64) L.bm[w] = d.obstbits[w];
     for (int s = lane; s < E; s += 64) {
         L.lpos[s] = d.pos[(size_t)s * N + e];
         L.llife[s] = d.life[(size_t)s * N + e];
@@ -312,6 +311,25 @@ __device__ __forceinline__ void respawn_env_wave(const Dev& d, const ResetLds& L
         L.lpres[s] = d.present[(size_t)s * N + e];
         L.lorder[s] = d.order[(size_t)s * N + e];
     }
+    // occupancy (as k_tick rebuilds it): the map's obstacle cells minus the lost obstacles, then the
+    // present things
+    wave_sync();
+    for (int w = lane; w < d.OW; w += 64) {
+        const int nb = min(32, d.O - 32 * w);
+        uint32_t gone = ~d.obst_present[(size_t)e * d.OW + w] & (nb == 32 ? 0xffffffffu : ((1u << nb) - 1u));
+        while (gone) {
+            const int32_t op = d.obst_xy[32 * w + __ffs(gone) - 1];
+            gone &= gone - 1;
+            const int cell = unpack_y(op) * d.W + unpack_x(op);
+            __hip_atomic_fetch_and(&L.bm[cell >> 5], ~(1u << (cell & 31)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
+    wave_sync();
+    for (int s = lane; s < E; s += 64)
+        if (L.lpres[s]) {
+            const int cell = unpack_y(L.lpos[s]) * d.W + unpack_x(L.lpos[s]);
+            __hip_atomic_fetch_or(&L.bm[cell >> 5], 1u << (cell & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
     WaveRng r;
     r.ring = d.ring + (size_t)e * ZS_RING_WORDS;
     r.lr = L.tw;
@@ -349,7 +367,6 @@ __device__ __forceinline__ void respawn_env_wave(const Dev& d, const ResetLds& L
         d.present[(size_t)s * N + e] = L.lpres[s];
     }
     for (int m = n0 + lane; m < n0 + placed; m += 64) d.order[(size_t)m * N + e] = L.lorder[m];
-    for (int w = lane; w < d.DW; w += 64) d.occ_bits[(size_t)e * d.DW + w] = L.bm[w];
     if (lane == 0) {
         d.scal[S_NORDER * N + e] = n_order;
         d.scal[S_SERIAL * N + e] = serial;
@@ -360,7 +377,7 @@ __device__ __forceinline__ void respawn_env_wave(const Dev& d, const ResetLds& L
 
 __global__ void __launch_bounds__(64, ZS_STEP_WAVES) k_respawn(Dev d) {
     extern __shared__ __align__(16) uint8_t smem[];
-    const int n = *d.resp_count;
+    const int n = min(*d.resp_count, d.N);
     if ((int)blockIdx.x >= n) return;
     const ResetLds L = reset_lds_carve(d, smem);
     for (int idx = blockIdx.x; idx < n; idx += gridDim.x) respawn_env_wave(d, L, d.resp_list[idx]);
@@ -369,9 +386,9 @@ __global__ void __launch_bounds__(64, ZS_STEP_WAVES) k_respawn(Dev d) {
 // Drop the envs a mask-mode reset just rebuilt from the pending list (src -> dst, dst count
 // zeroed by the host); mask == NULL drops all.  Keeps "list == pending envs" exact.
 __global__ void __launch_bounds__(256) k_list_filter(const int* src, const int* src_count, int* dst, int* dst_count,
-                                                     const uint8_t* mask) {
+                                                     const uint8_t* mask, int N) {
     if (!mask) return;
-    const int n = *src_count;
+    const int n = min(*src_count, N);
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         int e = src[i];
         if (!mask[e]) dst[atomicAdd(dst_count, 1)] = e;

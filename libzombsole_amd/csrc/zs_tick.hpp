@@ -4,7 +4,8 @@
 // in dict order -> random.shuffle -> execute one by one -> clean dead things), followed by the
 // env glue (rewards, zombie respawn, rules).  Mapping to CDNA4:
 //   * a 64-lane wave holds NE = 64/G envs; every env's hot state sits in LDS for the whole
-//     tick: occupancy bitmap (1 bit per cell), entity table, dict-order list, a window of
+//     tick: occupancy bitmap (1 bit per cell, rebuilt at stage-in from the static obstacle cells, the
+//     env's obstacle-present bits and its things: never stored), entity table, dict-order list, a window of
 //     pre-tempered MT19937 words and the spawn-candidate list, so the serial chain issues no
 //     dependent global loads;
 //   * the G lanes of an env stage state in/out and take the decisions in parallel (every
@@ -20,7 +21,7 @@
 
 #define NOTHING ((int)0x80000000)
 
-enum { K_NONE = 0, K_MOVE = 1, K_ATTACK = 2, K_HEAL = 3, K_DEFER = 4 };
+enum { K_NONE = 0, K_MOVE = 1, K_ATTACK = 2, K_HEAL = 3, K_DEFER = 4, K_RAISE = 5 };
 
 // Diagnostic build only (-DZS_STAMPS, never the product .so): lane 0 of every workgroup adds the
 // s_memtime ticks each k_tick phase took into its own slot g_stamp_wg[block][phase] (plain
@@ -510,6 +511,8 @@ __device__ __forceinline__ void decide_agent(const Dev& d, const Grp& c, int s, 
         int q = closest_in(d, c, x, y, 0, d.A + d.P, s);
         kind = K_HEAL;
         tgt = q >= 0 ? q : s;
+    } else if (ak == ZS_ACT_RAISE) {
+        kind = K_RAISE;
     }
 }
 
@@ -693,6 +696,19 @@ __device__ __forceinline__ void env_step_leader(const Dev& d, Grp& c, const int3
     int nact = 0;
     for (int k = 0; k < c.n_order; k++) {
         int s = LO(c, k);
+        if (LK(c, s) == K_RAISE) {
+            // this agent's next_step raised and the env re-raises (debug, core.py:96-99): the step
+            // stops here, after t += 1 and the earlier actors' decisions (and their draws)
+            const int nr = d.reward_mode == ZS_REWARD_SINGLE ? 1 : A;
+            for (int a = 0; a < nr; a++) rew[(size_t)c.e * nr + a] = 0.0;
+            if (listed_out)
+                for (int a = 0; a < A; a++) listed_out[(size_t)c.e * A + a] = (uint8_t)MISC(c, MISC_N + A + a);
+            done_out[c.e] = 0;
+            trunc_out[c.e] = 0;
+            c.fin = 0;
+            c.respawn = 0;
+            return;
+        }
         if (LK(c, s) == K_DEFER) {
             int kind, tgt;
             decide(d, c, s, actions, true, kind, tgt);
@@ -944,7 +960,7 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
     int32_t vp[4], vl[4];
     uint8_t vw[4], vr[4], vo[4];
     int mval = 0, av = 0;
-    uint32_t bmv[8];
+    uint32_t bmv[8], opw = 0u;
     const int nmisc = MISC_N + 2 * A;
     if (active) {
         if (A) av = actions[(size_t)e * A * 3 + min(j, 3 * A - 1)];
@@ -971,9 +987,11 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
         else if (f == MISC_NONPOS) mval = 0;
         else if (f < MISC_N + A) mval = d.prev_life[(size_t)(f - MISC_N) * N + e];
         else mval = d.listed[(size_t)(f - MISC_N - A) * N + e];
-        const uint32_t* brow = d.occ_bits + (size_t)e * d.DW;
+        // occupancy is rebuilt here, not kept in HBM: the map's obstacle cells (static, shared by every
+        // env, cache-resident), minus the obstacles this env has lost, plus its present things
 #pragma unroll
-        for (int u = 0; u < 8; u++) bmv[u] = brow[min(j + u * G, d.DW - 1)];
+        for (int u = 0; u < 8; u++) bmv[u] = d.obstbits[min(j + u * G, d.DW - 1)];
+        opw = d.obst_present[(size_t)e * d.OW + min(j, d.OW - 1)];
     }
     stepping = active && needs_reset == 0;
     if (stepping) {
@@ -1039,10 +1057,9 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
             else v = d.listed[(size_t)(f - MISC_N - A) * N + e];
             MISC(c, f) = v;
         }
-        // the rest of the occupancy bitmap
+        // the rest of the static obstacle bitmap
         if (d.DW > 8 * G)
-            stage_in(d.occ_bits + (size_t)e * d.DW + 8 * G, d.DW - 8 * G, j, G, c.bm,
-                     [&](int w) { return IX(c, w + 8 * G); });
+            stage_in(d.obstbits + 8 * G, d.DW - 8 * G, j, G, c.bm, [&](int w) { return IX(c, w + 8 * G); });
         // RNG window: the next words of this env's stream, tempered
         uint32_t off = st & 1023u, slot = (st >> 10) & 1u, ready = (st >> 11) & 1u;
         if (off >= ZS_MT_N && ready) {
@@ -1070,6 +1087,29 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
     if (stepping) {
         // dict-order ranks for closest() tie-breaks
         for (int k = j; k < n_order; k += G) LR(c, LO(c, k)) = (uint8_t)k;
+        // the cells of obstacles this env has lost (cleaned up, core.py:121-138) are free
+        for (int w = j; w < d.OW; w += G) {
+            const uint32_t pw = w == j ? opw : d.obst_present[(size_t)e * d.OW + w];
+            const int nb = min(32, d.O - 32 * w);
+            uint32_t gone = ~pw & (nb == 32 ? 0xffffffffu : ((1u << nb) - 1u));
+            while (gone) {
+                const int32_t op = d.obst_xy[32 * w + __ffs(gone) - 1];
+                gone &= gone - 1;
+                const int cell = unpack_y(op) * d.W + unpack_x(op);
+                __hip_atomic_fetch_and(&c.bm[IX(c, cell >> 5)], ~(1u << (cell & 31)), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        }
+    }
+    wave_sync();
+    if (stepping) {  // the present things' cells (one may stand where a lost obstacle was)
+        for (int s = j; s < E; s += G)
+            if (LPR(c, s)) {
+                const int32_t p = LP(c, s);
+                const int cell = unpack_y(p) * d.W + unpack_x(p);
+                __hip_atomic_fetch_or(&c.bm[IX(c, cell >> 5)], 1u << (cell & 31), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
     }
     wave_sync();
     STAMP(1);
@@ -1110,9 +1150,15 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
         env_step_leader(d, c, actions, rew, done_out, trunc_out, listed_out);
         if (c.fin && (d.flags & ZS_FLAG_AUTORESET)) {
             needs_reset = 1;
-            reset_list[atomicAdd(reset_count, 1)] = e;  // rebuilt by the next call's reset work
+            // rebuilt by the next call's reset work; a list holds each env at most once, so an index
+            // past N means the counter was not zeroed for this call: never written out of bounds
+            const int k = atomicAdd(reset_count, 1);
+            if ((unsigned)k < (unsigned)N) reset_list[k] = e;
         }
-        if (c.respawn) d.resp_list[atomicAdd(d.resp_count, 1)] = e;  // k_respawn, after this launch
+        if (c.respawn) {  // k_respawn, after this launch
+            const int k = atomicAdd(d.resp_count, 1);
+            if ((unsigned)k < (unsigned)N) d.resp_list[k] = e;
+        }
         if (reset_out) reset_out[e] = 0;
         MISC(c, MISC_T) = c.t;
         MISC(c, MISC_DEATHS) = c.deaths;
@@ -1150,7 +1196,6 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
             } else if (f < MISC_N + A) d.prev_life[(size_t)(f - MISC_N) * N + e] = v;
             else d.listed[(size_t)(f - MISC_N - A) * N + e] = (uint8_t)v;
         }
-        for (int w = j; w < d.DW; w += G) d.occ_bits[(size_t)e * d.DW + w] = c.bm[IX(c, w)];
     }
     wave_sync();
     STAMP(4);

@@ -14,7 +14,7 @@ from . import _abi
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_build", "libzombsole_mi355x.so")
 SYMBOLS = ["zs_last_error", "zs_create", "zs_destroy", "zs_obs_shape", "zs_seed", "zs_reset", "zs_step", "zs_observe",
            "zs_gen_actions", "zs_step_graph", "zs_state_size", "zs_get_state", "zs_set_state", "zs_get_rng", "zs_set_rng", "zs_profile", "zs_profile_read", "zs_describe",
-           "zs_debug_stamps"]
+           "zs_debug_stamps", "zs_debug_lists"]
 
 _lib = None
 
@@ -57,6 +57,7 @@ def load_library(path=None):
     L.zs_profile_read.argtypes = [vp, C.POINTER(C.c_double)]
     L.zs_debug_stamps.argtypes = [vp, vp, vp, i32]
     L.zs_describe.argtypes = [vp, C.c_char_p, i32]
+    L.zs_debug_lists.argtypes = [vp, C.POINTER(i32), vp]
     for s in SYMBOLS:
         if s != "zs_last_error":
             getattr(L, s).restype = C.c_int
@@ -211,6 +212,14 @@ class Engine(object):
         if rc:
             _raise(self.L, rc, "zs_debug_stamps")
         return ssum, smax
+
+    def debug_lists(self):
+        """(pending-reset count of list 0, of list 1, deferred-respawn count, parity drained next)."""
+        out = (C.c_int32 * 4)()
+        rc = self.L.zs_debug_lists(self.h, out, self._stream())
+        if rc:
+            _raise(self.L, rc, "zs_debug_lists")
+        return tuple(int(v) for v in out)
 
     def get_state(self, env):
         buf = np.zeros(self.state_words, dtype=np.int32)

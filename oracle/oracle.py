@@ -72,6 +72,13 @@ def parse_state(buf):
     return {"dyn": dyn, "obst": obst, "dead": dead, "ctr": ctr, "agents": agents, "players": players}
 
 
+ZO_RAISED = 100
+
+
+class OracleRaised(Exception):
+    """The step stopped at an agent whose action is ZS_ACT_RAISE (World.get_actions re-raising)."""
+
+
 class OracleEnv(object):
     """One reference env restated in C; `builder` is a libzombsole_amd._abi.ConfigBuilder."""
 
@@ -112,6 +119,8 @@ class OracleEnv(object):
         listed = np.zeros(max(self.A, 1), np.uint8)
         rc = self.L.zo_step(self.h, a.ctypes.data, rew.ctypes.data, done.ctypes.data, trunc.ctypes.data,
                             listed.ctypes.data)
+        if rc == ZO_RAISED:
+            raise OracleRaised()
         if rc:
             raise RuntimeError("zo_step failed: %d" % rc)
         return self.obs(), rew, bool(done[0]), bool(trunc[0]), listed[:self.A].astype(bool)

@@ -109,6 +109,16 @@ CONFIGS = [
      dict(rules_name="safehouse", player_names=[], map_name="to_the_closet",
           agent_ids=["0", "1"], initial_zombies=8, minimum_zombies=8,
           agent_weapons="shotgun"), [18], 120, 2, 0),
+    # debug=True with parameters Agent.next_step raises on (actions.bad_action): World.step re-raises
+    # after t += 1 and the earlier actors' decisions, incl. hamster / randoman RNG draws (core.py:72-99)
+    ("single_easyexit_debug_badactions", "single", "bad",
+     dict(rules_name="survival", player_names=["hamster", "randoman", "troll"], map_name="easy_exit",
+          agent_id=0, initial_zombies=6, minimum_zombies=4, observation_scope="surroundings:7",
+          observation_position_encoding="channels", agent_weapon="random", debug=True), [21, 22], 120, 2, 50),
+    ("multi_bridge_debug_badactions_a3", "multi", "bad",
+     dict(rules_name="extermination", player_names=["hamster", "randoman"], map_name="bridge",
+          agent_ids=["0", "1", "2"], initial_zombies=10, minimum_zombies=4,
+          observation_surroundings_width=11, debug=True), [23, 24], 120, 2, 60),
 ]
 
 

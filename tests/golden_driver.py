@@ -100,24 +100,36 @@ def run_config(cfg, K):
                 elapsed = 0
             else:
                 rec["kind"] = "step"
-                if surface == "single":
-                    if stream == "discrete":
-                        act = A.discrete_action_id(seed, call, 0, n_act)
-                        rec["act"] = int(act)
+                dict_act = A.bad_action if stream == "bad" else A.rich_action
+                try:
+                    if surface == "single":
+                        if stream == "discrete":
+                            act = A.discrete_action_id(seed, call, 0, n_act)
+                            rec["act"] = int(act)
+                        else:
+                            act = dict_act(seed, call, 0)
+                            rec["act"] = act
+                        obs, rew, done, trunc, _ = env.step(act)
+                        rec["rew"] = float(rew).hex()
                     else:
-                        act = A.rich_action(seed, call, 0)
-                        rec["act"] = act
-                    obs, rew, done, trunc, _ = env.step(act)
-                    rec["rew"] = float(rew).hex()
-                else:
-                    if stream == "discrete":
-                        act = {aid: int(A.discrete_action_id(seed, call, i, n_act))
-                               for i, aid in enumerate(agent_ids)}
-                    else:
-                        act = {aid: A.rich_action(seed, call, i) for i, aid in enumerate(agent_ids)}
-                    rec["act"] = [act[a] for a in agent_ids]
-                    before = list(base.agents)
-                    obs, rews, dones, truncs, _ = env.step(act)
+                        if stream == "discrete":
+                            act = {aid: int(A.discrete_action_id(seed, call, i, n_act))
+                                   for i, aid in enumerate(agent_ids)}
+                        else:
+                            act = {aid: dict_act(seed, call, i) for i, aid in enumerate(agent_ids)}
+                        rec["act"] = [act[a] for a in agent_ids]
+                        before = list(base.agents)
+                        obs, rews, dones, truncs, _ = env.step(act)
+                except Exception as err:
+                    if stream != "bad":
+                        raise
+                    # a debug env re-raises an agent's next_step error from inside World.step
+                    # (core.py:96-99): record it and the state it left, then go on stepping
+                    rec["raised"] = [type(err).__name__, str(err)]
+                    rec["state"] = canonical_state(game, obstacles, K)
+                    recs.append(rec)
+                    continue
+                if surface != "single":
                     rec["before"] = [agent_ids.index(a) for a in before]
                     rec["rew"] = [[agent_ids.index(a), float(r).hex()] for a, r in rews.items()]
                     done = bool(all(dones.values())) if dones else False

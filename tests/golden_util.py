@@ -57,11 +57,15 @@ def action_triples(fx, rec, n_agents):
     else:
         acts = rec["act"]
     out = np.zeros((max(n_agents, 1), 3), dtype=np.int32)
+    debug = bool(fx["kwargs"].get("debug", False))
     for i, a in enumerate(acts[:n_agents]):
         if fx["stream"] == "discrete":
             out[i] = A.DISCRETE_TRIPLES[int(a)]
         else:
-            out[i] = A.encode_action(a)
+            try:
+                out[i] = A.encode_action(a)
+            except A.ActionError:  # next_step raises: World.step re-raises (debug) or the agent idles
+                out[i] = (A.ACT_RAISE, 0, 0) if debug else (A.ACT_IDLE, 0, 0)
     return out
 
 
@@ -84,6 +88,14 @@ def compare_call(fx, rec, got, where):
     """Assert one call's outputs equal the fixture's.  `got` has keys obs_sha, state and,
     for steps, rew, done, trunc, listed (multi)."""
     assert got["kind"] == rec["kind"], where
+    if "raised" in rec:  # the step re-raised an agent's error: only the state it left is defined
+        assert got.get("raised"), (where, "expected the step to raise", rec["raised"])
+        if isinstance(got["raised"], list):
+            assert got["raised"] == rec["raised"], (where, "raised", got["raised"], rec["raised"])
+        for k in ("ctr", "agents", "players", "dyn", "obst", "dead"):
+            assert got["state"][k] == rec["state"][k], (where, k, got["state"][k], rec["state"][k])
+        return
+    assert not got.get("raised"), (where, "raised", got.get("raised"))
     if rec["kind"] == "step":
         assert got["done"] == rec["done"], (where, "done")
         assert got["trunc"] == rec["trunc"], (where, "trunc")

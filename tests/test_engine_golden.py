@@ -48,6 +48,10 @@ def replay_engine(fx):
             where = (fx["name"], r["seed"], i)
             kind = "reset" if (i == 0 or was_reset[k]) else "step"
             got = {"kind": kind}
+            if "raised" in rec:  # the step stopped at a ZS_ACT_RAISE agent: only the state is defined
+                got.update(raised=True, state=eng.get_state(k).canonical(kinds))
+                G.compare_call(fx, rec, got, where)
+                continue
             lst = listed[k].astype(bool) if kind == "step" else np.ones(eng.A, bool)
             if kind == "step":
                 got.update(done=bool(done[k]), trunc=bool(trunc[k]),

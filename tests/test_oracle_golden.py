@@ -6,7 +6,7 @@ failure here means the CPU restatement diverged from jvstinian/libzombsole.
 import pytest
 
 import golden_util as G
-from oracle.oracle import OracleEnv
+from oracle.oracle import OracleEnv, OracleRaised
 
 
 def replay_oracle(fx, run):
@@ -22,7 +22,12 @@ def replay_oracle(fx, run):
             listed = [True] * b.num_agents
         else:
             acts = G.action_triples(fx, rec, b.num_agents)
-            obs, rew, done, trunc, lb = env.step(acts)
+            try:
+                obs, rew, done, trunc, lb = env.step(acts)
+            except OracleRaised:
+                got.update(raised=True, state=env.state())
+                G.compare_call(fx, rec, got, where)
+                continue
             got.update(done=done, trunc=trunc, listed=[j for j in range(len(lb)) if lb[j]],
                        rew=G.rewards_record(fx, rew, lb))
             listed = lb

@@ -1,16 +1,12 @@
 #!/bin/bash
-# One GPU session: smoke -> gpu tests -> short bench.  Stops at the first crash /
-# timeout (exit >= 2 from pytest, or any nonzero from the others); plain test
-# failures (pytest exit 1) still let the bench run.
+# GPU regression pass: every -m gpu test (optionally -k filtered), then one bench line per config.
+# Each GPU step has its own time limit; the script stops at the first failure.
 cd "$(dirname "$0")/.." || exit 2
 mkdir -p gpurun_out
-export PYTHONUNBUFFERED=1
-timeout -k 10 300 python __graft_entry__.py smoke > gpurun_out/smoke.log 2>&1
-rc=$?; echo "smoke rc=$rc"; tail -3 gpurun_out/smoke.log
-[ $rc -ne 0 ] && exit $rc
-timeout -k 10 ${PYTEST_TIMEOUT:-900} python -m pytest tests -m gpu -q ${PYTEST_ARGS} > gpurun_out/pytest_gpu.log 2>&1
-rc=$?; echo "pytest rc=$rc"; tail -15 gpurun_out/pytest_gpu.log
-[ $rc -ge 2 ] && exit $rc
-timeout -k 10 300 python bench.py ${BENCH_ARGS:---steps 100 --warmup 10} > gpurun_out/bench.log 2>&1
-rc2=$?; echo "bench rc=$rc2"; tail -3 gpurun_out/bench.log
-exit $(( rc > rc2 ? rc : rc2 ))
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} \
+    > gpurun_out/pytest_gpu.log 2>&1 || { tail -40 gpurun_out/pytest_gpu.log; exit 1; }
+tail -2 gpurun_out/pytest_gpu.log
+for cfg in ${CFGS:-c3}; do
+    timeout -k 10 180 python bench.py --config $cfg --steps 100 --warmup 10 --no-cpu-baseline > gpurun_out/bench_$cfg.json 2> gpurun_out/bench_$cfg.err || { tail -5 gpurun_out/bench_$cfg.err; exit 1; }
+    python -c "import json,sys;d=json.load(open('gpurun_out/bench_$cfg.json'));r=d['roofline'];print('$cfg', round(d['value']/1e6,1), 'M/s ms', round(d['ms_per_step'],4), 'tick', round(r['step_launch_ms'],4), 'obs', round(r['k_obs_ms'],4), 'reset', round(r['k_reset_ms'],4), 'respawn', round(r['k_respawn_ms'],4))"
+done

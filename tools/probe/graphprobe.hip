@@ -101,6 +101,163 @@ int probe(hipStream_t s) {
     return 0;
 }
 
+// The engine's form: per pending-list parity q a graph zeroes counter cnt[q] with a captured 4-byte
+// hipMemsetAsync, then a kernel appends to it (atomicAdd from 64 lanes, the returned maximum recorded
+// per replay).  The two graphs are captured on one non-blocking stream and replayed alternately; a
+// correct replay leaves exactly 64 in cnt[q].  No address is ever derived from a counter value.
+__global__ void k_append(int* cnt, int* rec, int replay) {
+    const int v = atomicAdd(cnt, 1);
+    atomicMax(&rec[replay], v + 1);
+}
+
+int probe_chain(hipStream_t s, int replays, int lds) {
+    int *cnt, *rec;
+    CHK(hipMalloc(&cnt, 16));  // the engine's minimum allocation for d_rcount[2]
+    CHK(hipMemset(cnt, 0, 16));
+    CHK(hipMalloc(&rec, sizeof(int) * replays));
+    CHK(hipMemset(rec, 0, sizeof(int) * replays));
+    hipStream_t cs;
+    CHK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+    hipGraphExec_t x[2];
+    for (int q = 0; q < 2; q++) {
+        hipGraph_t g;
+        CHK(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
+        CHK(hipMemsetAsync(cnt + q, 0, sizeof(int), cs));
+        hipLaunchKernelGGL(k_lds, dim3(1), dim3(64), lds, cs, lds);  // a kernel with dynamic LDS between
+        hipLaunchKernelGGL(k_append, dim3(1), dim3(64), 0, cs, cnt + q, rec, 0);
+        CHK(hipStreamEndCapture(cs, &g));
+        CHK(hipGraphInstantiate(&x[q], g, nullptr, nullptr, 0));
+        CHK(hipGraphDestroy(g));
+    }
+    // replay: graph q each time, the recorded maximum per replay goes to rec[0]; read it back per replay
+    int bad = 0, first_bad = -1, worst = 0;
+    for (int i = 0; i < replays; i++) {
+        CHK(hipMemsetAsync(rec, 0, sizeof(int), s));
+        CHK(hipGraphLaunch(x[i & 1], s));
+        int got = 0;
+        CHK(hipMemcpyAsync(&got, rec, sizeof(int), hipMemcpyDeviceToHost, s));
+        CHK(hipStreamSynchronize(s));
+        if (got != 64) {
+            bad++;
+            if (first_bad < 0) first_bad = i;
+            worst = got > worst ? got : worst;
+        }
+    }
+    int host[4] = {0, 0, 0, 0};
+    CHK(hipMemcpy(host, cnt, 16, hipMemcpyDeviceToHost));
+    printf("memset+append chain, %d replays, %d B LDS between: %d bad (first %d, worst count %d), counters %d %d %d %d  %s\n",
+           replays, lds, bad, first_bad, worst, host[0], host[1], host[2], host[3], bad ? "MISMATCH" : "OK");
+    for (int q = 0; q < 2; q++) CHK(hipGraphExecDestroy(x[q]));
+    CHK(hipStreamDestroy(cs));
+    CHK(hipFree(cnt));
+    CHK(hipFree(rec));
+    return 0;
+}
+
+// The deferred-respawn form: two captured 4-byte memsets in a row (the parity's list counter, then a
+// second counter in its own allocation), then a kernel appending to both.
+__global__ void k_append2(int* c1, int* c2, int* rec) {
+    const int v = atomicAdd(c1, 1), w = atomicAdd(c2, 1);
+    atomicMax(&rec[0], v + 1);
+    atomicMax(&rec[1], w + 1);
+}
+
+// fills the host stack below the caller with a byte pattern (the frames the capture calls used)
+__attribute__((noinline)) void scribble_stack(unsigned char pat) {
+    volatile unsigned char buf[256 * 1024];
+    for (size_t i = 0; i < sizeof(buf); i++) buf[i] = pat;
+}
+
+// memset nodes followed by a kernel whose by-value argument block is large (the engine's Dev struct
+// is ~0.4 KB): are the kernel's arguments intact when the graph replays?
+template <int NW>
+int probe_memset_args(hipStream_t s, int n_memsets) {
+    Big<NW> b;
+    for (int i = 0; i < NW; i++) b.w[i] = 0x9e3779b9u * (i + 7);
+    const uint32_t zero[2] = {0, 0};
+    uint32_t direct[2], graph[2];
+    int* cnt;
+    CHK(hipMalloc(&cnt, 16));
+    CHK(hipMemcpyToSymbol(HIP_SYMBOL(g_out), zero, 8));
+    hipLaunchKernelGGL(k_sum<NW>, dim3(1), dim3(64), 0, s, b, 777);
+    CHK(hipStreamSynchronize(s));
+    CHK(hipMemcpyFromSymbol(direct, HIP_SYMBOL(g_out), 8));
+    hipStream_t cs;
+    CHK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+    hipGraph_t g;
+    hipGraphExec_t x;
+    CHK(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
+    for (int m = 0; m < n_memsets; m++) CHK(hipMemsetAsync(cnt + m, 0, sizeof(int), cs));
+    hipLaunchKernelGGL(k_sum<NW>, dim3(1), dim3(64), 0, cs, b, 777);
+    CHK(hipStreamEndCapture(cs, &g));
+    CHK(hipGraphInstantiate(&x, g, nullptr, nullptr, 0));
+    int bad = 0;
+    for (int rep = 0; rep < 20; rep++) {
+        CHK(hipMemcpyToSymbol(HIP_SYMBOL(g_out), zero, 8));
+        CHK(hipGraphLaunch(x, s));
+        CHK(hipStreamSynchronize(s));
+        CHK(hipMemcpyFromSymbol(graph, HIP_SYMBOL(g_out), 8));
+        bad += graph[0] != direct[0] || graph[1] != direct[1];
+    }
+    printf("%d memset node(s) then a kernel with %4d B of arguments: %d of 20 replays with other arguments  %s\n",
+           n_memsets, (int)sizeof(b) + 4, bad, bad ? "MISMATCH" : "OK");
+    CHK(hipGraphExecDestroy(x));
+    CHK(hipGraphDestroy(g));
+    CHK(hipStreamDestroy(cs));
+    CHK(hipFree(cnt));
+    return 0;
+}
+
+int probe_chain2(hipStream_t s, int replays, int kernel_between, int scribble = 0) {
+    int *cnt, *resp, *rec;
+    CHK(hipMalloc(&cnt, 16));
+    CHK(hipMalloc(&resp, 16));
+    CHK(hipMemset(cnt, 0, 16));
+    CHK(hipMemset(resp, 0, 16));
+    CHK(hipMalloc(&rec, 2 * sizeof(int)));
+    hipStream_t cs;
+    CHK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+    hipGraphExec_t x[2];
+    for (int q = 0; q < 2; q++) {
+        hipGraph_t g;
+        CHK(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
+        if (kernel_between) hipLaunchKernelGGL(k_lds, dim3(1), dim3(64), 1024, cs, 1024);
+        CHK(hipMemsetAsync(cnt + q, 0, sizeof(int), cs));
+        CHK(hipMemsetAsync(resp, 0, sizeof(int), cs));
+        if (scribble > 1) scribble_stack((unsigned char)(0x50 + q));  // dirty the stack before the rest of the capture
+        hipLaunchKernelGGL(k_append2, dim3(1), dim3(64), 0, cs, cnt + q, resp, rec);
+        CHK(hipStreamEndCapture(cs, &g));
+        if (scribble > 1) scribble_stack((unsigned char)(0x60 + q));  // ... and before instantiation
+        CHK(hipGraphInstantiate(&x[q], g, nullptr, nullptr, 0));
+        CHK(hipGraphDestroy(g));
+    }
+    int bad = 0, first_bad = -1, w1 = 0, w2 = 0;
+    for (int i = 0; i < replays; i++) {
+        if (scribble) scribble_stack((unsigned char)(0x40 + (i & 1)));
+        CHK(hipMemsetAsync(rec, 0, 2 * sizeof(int), s));
+        CHK(hipGraphLaunch(x[i & 1], s));
+        int got[2] = {0, 0};
+        CHK(hipMemcpyAsync(got, rec, sizeof(got), hipMemcpyDeviceToHost, s));
+        CHK(hipStreamSynchronize(s));
+        if (got[0] != 64 || got[1] != 64) {
+            bad++;
+            if (first_bad < 0) first_bad = i;
+            w1 = got[0] > w1 ? got[0] : w1;
+            w2 = got[1] > w2 ? got[1] : w2;
+        }
+    }
+    printf("two memsets + append, %d replays, kernel before: %d, host stack overwritten (1: between replays, "
+           "2: also during capture and before instantiation): %d: %d bad (first %d, worst counts 0x%08x 0x%08x)  %s\n",
+           replays, kernel_between, scribble, bad,
+           first_bad, w1, w2, bad ? "MISMATCH" : "OK");
+    for (int q = 0; q < 2; q++) CHK(hipGraphExecDestroy(x[q]));
+    CHK(hipStreamDestroy(cs));
+    CHK(hipFree(cnt));
+    CHK(hipFree(resp));
+    CHK(hipFree(rec));
+    return 0;
+}
+
 int main(int argc, char** argv) {
     hipStream_t s;
     CHK(hipStreamCreate(&s));
@@ -113,6 +270,12 @@ int main(int argc, char** argv) {
     if (probe_lds(s, 1024) || probe_lds(s, 7744) || probe_lds(s, 14304) || probe_lds(s, 32768) || probe_lds(s, 65536))
         return 1;
     if (argc < 2) return 0;  // "memset": also the captured memset (writes device memory from graph params)
+    if (probe_chain(s, 200, 1024) || probe_chain(s, 200, 14304)) return 1;
+    if (probe_chain2(s, 200, 0) || probe_chain2(s, 200, 1) || probe_chain2(s, 50, 1, 1) || probe_chain2(s, 50, 1, 2))
+        return 1;
+    if (probe_memset_args<16>(s, 1) || probe_memset_args<100>(s, 1) || probe_memset_args<100>(s, 2) ||
+        probe_memset_args<128>(s, 2) || probe_memset_args<200>(s, 2))
+        return 1;
     // captured 4-byte memset inside a 16-word sentinel buffer
     uint32_t host[16];
     for (int i = 0; i < 16; i++) host[i] = 0xabababab;
