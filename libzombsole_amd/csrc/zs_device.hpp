@@ -61,6 +61,7 @@ __host__ __device__ inline ObsLayout obs_layout(int nobs, int plane, int E, int 
     o += L.win;
     L.off_pos = o;
     o += E * 4;
+    o = ((o + 7) / 8) * 8;  // the store-stream kernels read {code word, life} pairs from off_life as 8 B
     L.off_life = o;
     o += E * 4;
     L.off_cw = o;

@@ -25,6 +25,10 @@
 #define SC_KIND_SHIFT 16
 #define SC_OBJ_BIT (1u << 20)
 
+typedef unsigned int zs_v4u __attribute__((ext_vector_type(4)));
+typedef unsigned int zs_v2u __attribute__((ext_vector_type(2)));
+typedef int zs_v2i __attribute__((ext_vector_type(2)));
+
 // observations per env
 __host__ __device__ inline int obs_count(int scope, int reward_mode, int A) {
     return scope == ZS_OBS_WORLD ? 1 : (reward_mode == ZS_REWARD_MULTI ? A : 1);
@@ -115,6 +119,50 @@ __device__ __forceinline__ void obs_stage_static(const Dev& d, lu32* st, int t0,
     stage_in(d.boxbits, d.DW, t0, nt, st + d.DW, [](int w) { return w; });
     stage_in(d.objbits, d.DW, t0, nt, st + 2 * d.DW, [](int w) { return w; });
     stage_in((const uint32_t*)d.oprefix, d.DW, t0, nt, st + 3 * d.DW, [](int w) { return w; });
+}
+
+// ---------------------------------------------------------------------------
+// Compact image of the store-stream kernels (k_obs_pipe, k_obs_lds), in the same ObsLayout regions:
+//   * the entity table is one 8-B pair per slot, {code | weapon << 8 | present << 16, life}, at
+//     off_life (the life and code-word regions are adjacent);
+//   * obstacle HP is stored with its presence folded in: HP of a present obstacle, ZS_HP_ABSENT for one
+//     cleaned up (its cell is then empty, core.py:121-138);
+//   * the static tables are interleaved per bitmap word: {obstacle, box, objective bits, obstacles in
+//     the cells below the word}, one 16-B read.
+// A cell is then five independent LDS reads (window-map byte, static word, dead-body word; then the
+// entity pair and the obstacle HP) in two dependency levels and no branch, instead of ten in four.
+// ---------------------------------------------------------------------------
+#define ZS_HP_ABSENT ((int)0x80000000)
+typedef ZS_LDS zs_v4u lv4u;
+typedef ZS_LDS zs_v2i lv2i;
+
+__device__ __forceinline__ void obs_stage_static4(const Dev& d, lv4u* st4, int t0, int nt) {
+    for (int w = t0; w < d.DW; w += nt)
+        st4[w] = zs_v4u{d.obstbits[w], d.boxbits[w], d.objbits[w], (uint32_t)d.oprefix[w]};
+}
+
+__device__ __forceinline__ void obs_cell_lds(const Dev& d, const ObsLayout& L, const lv4u* st4, const lu8* img,
+                                             const lu8* wm, int cell, int x, int y, int& code, int& lf, int& weapon) {
+    const lv2i* ent = (const lv2i*)(img + L.off_life);
+    const lu32* dead = (const lu32*)(img + L.off_dead);
+    const li32* hpx = (const li32*)(img + L.off_hp);
+    const bool inb = (unsigned)x < (unsigned)d.W && (unsigned)y < (unsigned)d.H;
+    const int c = inb ? y * d.W + x : 0, w = c >> 5;
+    const uint32_t bit = 1u << (c & 31);
+    const int sb = wm[cell];  // entity slot + 1, or 0
+    const zs_v4u sw = st4[w];
+    const uint32_t dw = dead[w];
+    const zs_v2i ev = ent[sb ? sb - 1 : 0];
+    const bool isob = (sw.x & bit) != 0u;
+    const int ohp = hpx[isob ? (int)sw.w + __popc(sw.x & (bit - 1u)) : 0];
+    const bool obp = isob && ohp != ZS_HP_ABSENT;
+    code = (dw & bit) ? ZS_THING_DEADBODY : (sw.z & bit) ? ZS_THING_OBJECTIVE : ZS_THING_NONE;
+    code = obp ? ((sw.y & bit) ? ZS_THING_BOX : ZS_THING_WALL) : code;
+    code = sb ? (ev.x & 255) : code;
+    code = inb ? code : ZS_THING_WALL;
+    lf = sb ? ev.y : (obp ? ohp : 0);
+    lf = inb ? lf : 200;
+    weapon = (inb && sb) ? ((ev.x >> 8) & 255) : 0;
 }
 
 // Stream env e's observations from its image: lane handles cells lane, lane + 64, ... of every
@@ -369,25 +417,60 @@ __device__ __forceinline__ void obs_prefetch(const Dev& d, int e, ObsPrefetch& f
     for (int i = 0; i < OBS_PF_H; i++) f.hp[i] = hr[min(lane + 64 * i, d.O - 1)];
 }
 
+// The compact image (obs_cell_lds) of one env from its prefetched registers.  Lane l holds the HP of
+// obstacles l, l + 64, ... and the present bits of obstacles 32l .. 32l + 31: obstacle o's bit comes
+// from lane o >> 5 by a cross-lane read.
+__device__ __forceinline__ void obs_build_compact(const Dev& d, const ObsLayout& L, lu8* img, const ObsPrefetch& f,
+                                                  int code_s, int lane) {
+    for (int w = lane; w < L.win / 4; w += 64) ((lu32*)img)[w] = 0u;
+    if (lane < d.E) {
+        ((li32*)(img + L.off_pos))[lane] = f.pos;
+        ((lv2i*)(img + L.off_life))[lane] = zs_v2i{code_s | (f.wp << 8) | (f.pr << 16), f.life};
+    }
+    lu32* dead = (lu32*)(img + L.off_dead);
+#pragma unroll
+    for (int i = 0; i < OBS_PF_D; i++)
+        if (lane + 64 * i < d.DW) dead[lane + 64 * i] = f.dead[i];
+    li32* hpx = (li32*)(img + L.off_hp);
+#pragma unroll
+    for (int i = 0; i < OBS_PF_H; i++) {
+        const uint32_t pw = (uint32_t)__shfl((int)f.opres, (lane >> 5) + 2 * i);
+        if (lane + 64 * i < d.O) hpx[lane + 64 * i] = ((pw >> (lane & 31)) & 1u) ? f.hp[i] : ZS_HP_ABSENT;
+    }
+}
+
+// window map of the compact image: every present entity's slot + 1 in each agent's window
+template <int NOBS>
+__device__ __forceinline__ void obs_window_compact(const Dev& d, const ObsLayout& L, lu8* img, int lane) {
+    constexpr int WW = 21, PLANE = WW * WW;
+    const li32* pos = (const li32*)(img + L.off_pos);
+    const lv2i* ent = (const lv2i*)(img + L.off_life);
+    if (lane < d.E && ((ent[lane].x >> 16) & 1)) {
+        const int32_t p = pos[lane];
+        const int x = unpack_x(p), y = unpack_y(p);
+#pragma unroll
+        for (int a = 0; a < NOBS; a++) {
+            const int32_t ap = pos[a];
+            const int dx = x - (unpack_x(ap) - WW / 2), dy = y - (unpack_y(ap) - WW / 2);
+            if (dx >= 0 && dy >= 0 && dx < WW && dy < WW) img[a * PLANE + dy * WW + dx] = (uint8_t)(lane + 1);
+        }
+    }
+}
+
 template <typename T, int NOBS>
 __global__ void __launch_bounds__(256, ZS_OBS_PIPE_WAVES) k_obs_pipe(Dev d, T* out, ObsLayout L, int env0, int env1) {
     extern __shared__ __align__(16) uint8_t smem[];
     constexpr int WW = 21, PLANE = WW * WW, PER = (PLANE + 63) / 64;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int stat_words = 4 * d.DW;
-    lu32* st = (lu32*)smem;
-    obs_stage_static(d, st, threadIdx.x, blockDim.x);
+    lv4u* st4 = (lv4u*)smem;
+    obs_stage_static4(d, st4, threadIdx.x, blockDim.x);
     __syncthreads();
     const int waves = gridDim.x * 4;
     int e = env0 + xcd_remap(blockIdx.x, gridDim.x) * 4 + wave;
     if (e >= env1) return;
     lu8* img = (lu8*)(smem + stat_words * 4 + wave * L.bytes);
-    li32* pos = (li32*)(img + L.off_pos);
-    li32* life = (li32*)(img + L.off_life);
-    li32* cw = (li32*)(img + L.off_cw);
-    lu32* dead = (lu32*)(img + L.off_dead);
-    lu32* opres = (lu32*)(img + L.off_opres);
-    li32* hp = (li32*)(img + L.off_hp);
+    const li32* pos = (const li32*)(img + L.off_pos);
     const bool ch = d.obs_enc == ZS_ENC_CHANNELS;
     const int C = ch ? 3 : 1;
     const int code_s = lane < d.A ? (ch ? d.agent_codes[lane < d.A ? lane : 0] : ZS_THING_AGENT)
@@ -395,33 +478,10 @@ __global__ void __launch_bounds__(256, ZS_OBS_PIPE_WAVES) k_obs_pipe(Dev d, T* o
     ObsPrefetch f;
     obs_prefetch(d, e, f);
     for (; e < env1; e += waves) {
-        // the image of env e from the registers
-        for (int w = lane; w < L.win / 4; w += 64) ((lu32*)img)[w] = 0u;
-        if (lane < d.E) {
-            pos[lane] = f.pos;
-            life[lane] = f.life;
-            cw[lane] = code_s | (f.wp << 8) | (f.pr << 16);
-        }
-#pragma unroll
-        for (int i = 0; i < OBS_PF_D; i++)
-            if (lane + 64 * i < d.DW) dead[lane + 64 * i] = f.dead[i];
-        if (lane < d.OW) opres[lane] = f.opres;
-#pragma unroll
-        for (int i = 0; i < OBS_PF_H; i++)
-            if (lane + 64 * i < d.O) hp[lane + 64 * i] = f.hp[i];
+        obs_build_compact(d, L, img, f, code_s, lane);  // the image of env e from the registers
         obs_prefetch(d, min(e + waves, env1 - 1), f);  // the next env (the last wave re-reads its own)
         wave_sync();
-        // window map
-        if (lane < d.E && ((cw[lane] >> 16) & 1)) {
-            const int32_t p = pos[lane];
-            const int x = unpack_x(p), y = unpack_y(p);
-#pragma unroll
-            for (int a = 0; a < NOBS; a++) {
-                const int32_t ap = pos[a];
-                const int dx = x - (unpack_x(ap) - WW / 2), dy = y - (unpack_y(ap) - WW / 2);
-                if (dx >= 0 && dy >= 0 && dx < WW && dy < WW) img[a * PLANE + dy * WW + dx] = (uint8_t)(lane + 1);
-            }
-        }
+        obs_window_compact<NOBS>(d, L, img, lane);
         wave_sync();
         // the store stream
 #pragma unroll 1
@@ -436,7 +496,7 @@ __global__ void __launch_bounds__(256, ZS_OBS_PIPE_WAVES) k_obs_pipe(Dev d, T* o
                 const int cc = cell < PLANE ? cell : PLANE - 1;
                 const int r = cc / WW, q = cc - r * WW;
                 int code, lf, weapon;
-                obs_cell_fast(d, L, st, img, wm, cc, ox + q, oy + r, code, lf, weapon);
+                obs_cell_lds(d, L, st4, img, wm, cc, ox + q, oy + r, code, lf, weapon);
                 if (cell < PLANE) obs_store(o, PLANE, cell, ch, code, lf, weapon);
             }
         }
@@ -445,8 +505,6 @@ __global__ void __launch_bounds__(256, ZS_OBS_PIPE_WAVES) k_obs_pipe(Dev d, T* o
 }
 
 // 16-B store stream of one staged observation block (k_obs_lds, k_obs_gather<..., true>)
-typedef unsigned int zs_v4u __attribute__((ext_vector_type(4)));
-typedef unsigned int zs_v2u __attribute__((ext_vector_type(2)));
 
 // staging bytes per wave: one channels block at any 16-B phase of its destination
 __host__ __device__ constexpr int obs_lds_slot_bytes(int tsize) { return ((3 * 441 * tsize + 31) / 16) * 16; }
@@ -620,6 +678,21 @@ __device__ __forceinline__ void zs_buf_store(__amdgpu_buffer_rsrc_t r, uint32_t 
     }
 }
 
+// Store throttle: at most ZS_OBS_THR of the wave's memory operations in flight after each 16-B store
+// (-1: none).  HBM write bandwidth on this part falls when the whole chip keeps tens of thousands of
+// 1-KB wave stores in flight (tools/probe/storeceil.hip: a flat 16-B store stream reaches 6.6-6.7
+// TB/s with ~2-4 MB in flight chip-wide, 5.0-5.4 TB/s with 2048-4096 waves issuing unthrottled).
+#ifndef ZS_OBS_THR
+#define ZS_OBS_THR -1
+#endif
+#define ZS_STR2(x) #x
+#define ZS_STR(x) ZS_STR2(x)
+__device__ __forceinline__ void obs_store_throttle() {
+#if ZS_OBS_THR >= 0
+    asm volatile("s_waitcnt vmcnt(" ZS_STR(ZS_OBS_THR) ")" ::: "memory");
+#endif
+}
+
 // Stream one staged block to o: slot element k + mis / sizeof(T) holds output element k, so the
 // 16-B chunk q of the destination (counted from the 16-B boundary at or below o) reads the aligned
 // slot elements [q * VPC, (q + 1) * VPC).  The partial chunks at the two ends are element stores.
@@ -645,6 +718,7 @@ __device__ __forceinline__ void obs_stage_flush(const lu8* slot, T* o, int lane)
         }
         __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)((k >= k0 && k < kend) ? (uint32_t)(16 * k - mis) : ZS_OOB), 0,
                                                0);
+        obs_store_throttle();
     }
     const int nhead = mis ? (16 - mis) / TS : 0, tail0 = (16 * kend - mis) / TS, ntail = (nb - 16 * kend) / TS;
     const int idx = lane < nhead ? lane : (lane >= 32 && lane - 32 < ntail) ? tail0 + lane - 32 : -1;
@@ -661,54 +735,24 @@ __global__ void __launch_bounds__(256, ZS_OBS_PIPE_WAVES) k_obs_lds(Dev d, T* ou
     // the buffer resources of the flush need no waterfall loop
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int stat_words = 4 * d.DW;
-    lu32* st = (lu32*)smem;
-    obs_stage_static(d, st, threadIdx.x, blockDim.x);
+    lv4u* st4 = (lv4u*)smem;
+    obs_stage_static4(d, st4, threadIdx.x, blockDim.x);
     __syncthreads();
     const int waves = gridDim.x * 4;
     int e = env0 + xcd_remap(blockIdx.x, gridDim.x) * 4 + wave;
     if (e >= env1) return;
     lu8* img = (lu8*)(smem + stat_words * 4 + wave * (L.bytes + SLOT));
     lu8* slot = img + L.bytes;  // 16-B aligned: the static tables, L.bytes and SLOT are multiples of 16
-    li32* pos = (li32*)(img + L.off_pos);
-    li32* life = (li32*)(img + L.off_life);
-    li32* cw = (li32*)(img + L.off_cw);
-    lu32* dead = (lu32*)(img + L.off_dead);
-    lu32* opres = (lu32*)(img + L.off_opres);
-    li32* hp = (li32*)(img + L.off_hp);
+    const li32* pos = (const li32*)(img + L.off_pos);
     const int code_s = lane < d.A ? d.agent_codes[lane < d.A ? lane : 0] : (lane < d.A + d.P ? ZS_THING_PLAYER : ZS_THING_ZOMBIE);
-    // the image of an env from its prefetched registers
-    auto build = [&](const ObsPrefetch& f) {
-        for (int w = lane; w < L.win / 4; w += 64) ((lu32*)img)[w] = 0u;
-        if (lane < d.E) {
-            pos[lane] = f.pos;
-            life[lane] = f.life;
-            cw[lane] = code_s | (f.wp << 8) | (f.pr << 16);
-        }
-#pragma unroll
-        for (int i = 0; i < OBS_PF_D; i++)
-            if (lane + 64 * i < d.DW) dead[lane + 64 * i] = f.dead[i];
-        if (lane < d.OW) opres[lane] = f.opres;
-#pragma unroll
-        for (int i = 0; i < OBS_PF_H; i++)
-            if (lane + 64 * i < d.O) hp[lane + 64 * i] = f.hp[i];
-    };
+    auto build = [&](const ObsPrefetch& f) { obs_build_compact(d, L, img, f, code_s, lane); };
     // Two envs of prefetch in flight: the loads of env e + 2 * waves are issued before the stores of
     // env e and consumed after those of env e + waves, so a load has two envs' store streams to
     // return in.  Between the loads and the wait for them everything is straight-line (agents
     // unrolled, flush stores unconditional), so that wait leaves the stores in flight.
     auto process = [&](int e) {
         wave_sync();
-        // window map
-        if (lane < d.E && ((cw[lane] >> 16) & 1)) {
-            const int32_t p = pos[lane];
-            const int x = unpack_x(p), y = unpack_y(p);
-#pragma unroll
-            for (int a = 0; a < NOBS; a++) {
-                const int32_t ap = pos[a];
-                const int dx = x - (unpack_x(ap) - WW / 2), dy = y - (unpack_y(ap) - WW / 2);
-                if (dx >= 0 && dy >= 0 && dx < WW && dy < WW) img[a * PLANE + dy * WW + dx] = (uint8_t)(lane + 1);
-            }
-        }
+        obs_window_compact<NOBS>(d, L, img, lane);
         wave_sync();
 #pragma unroll
         for (int a = 0; a < NOBS; a++) {
@@ -717,20 +761,22 @@ __global__ void __launch_bounds__(256, ZS_OBS_PIPE_WAVES) k_obs_lds(Dev d, T* ou
             const lu8* wm = img + a * PLANE;
             T* o = out + ((size_t)e * NOBS + a) * 3 * PLANE;
             ZS_LDS S* ot = (ZS_LDS S*)slot + (int)((uintptr_t)o & 15) / TS;
+            if (!(ZS_OBS_DIAG & 16)) {  // diagnostic builds: 16 skips the encoding, 8 the stores
 #pragma unroll
-            for (int i = 0; i < PER; i++) {
-                const int cell = lane + 64 * i;
-                const int cc = cell < PLANE ? cell : PLANE - 1, r = cc / WW, q = cc - r * WW;
-                int code, lf, weapon;
-                obs_cell_fast(d, L, st, img, wm, cc, ox + q, oy + r, code, lf, weapon);
-                if (cell < PLANE) {
-                    ot[cell] = (S)code;
-                    ot[PLANE + cell] = (S)lf;
-                    ot[2 * PLANE + cell] = (S)weapon;
+                for (int i = 0; i < PER; i++) {
+                    const int cell = lane + 64 * i;
+                    const int cc = cell < PLANE ? cell : PLANE - 1, r = cc / WW, q = cc - r * WW;
+                    int code, lf, weapon;
+                    obs_cell_lds(d, L, st4, img, wm, cc, ox + q, oy + r, code, lf, weapon);
+                    if (cell < PLANE) {
+                        ot[cell] = (S)code;
+                        ot[PLANE + cell] = (S)lf;
+                        ot[2 * PLANE + cell] = (S)weapon;
+                    }
                 }
             }
             wave_sync();
-            obs_stage_flush(slot, o, lane);
+            if (!(ZS_OBS_DIAG & 8)) obs_stage_flush(slot, o, lane);
             wave_sync();
         }
     };

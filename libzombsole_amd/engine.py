@@ -57,8 +57,13 @@ def load_library(path=None):
     L.zs_profile_read.argtypes = [vp, C.POINTER(C.c_double)]
     L.zs_debug_stamps.argtypes = [vp, vp, vp, i32]
     L.zs_describe.argtypes = [vp, C.c_char_p, i32]
-    L.zs_debug_lists.argtypes = [vp, C.POINTER(i32), vp]
+    # an older build selected by ZS_ENGINE_LIB for an A/B (tools/ab.sh) may lack newer diagnostics
+    optional = {"zs_debug_lists"} if os.environ.get("ZS_ENGINE_LIB") and path is None else set()
     for s in SYMBOLS:
+        if s in optional and not hasattr(L, s):
+            continue
+        if s == "zs_debug_lists":
+            L.zs_debug_lists.argtypes = [vp, C.POINTER(i32), vp]
         if s != "zs_last_error":
             getattr(L, s).restype = C.c_int
     if path is None:
