@@ -257,6 +257,7 @@ struct zs_handle {
     ObsLayout obs_l;  // k_obs per-wave LDS image
     int obs_wpg;      // k_obs waves (envs) per workgroup
     int obs_pipe = 0;      // k_obs_pipe<NOBS> usable (NOBS = 1, 2, 4), else 0
+    int obs_walk = 0;      // k_obs_lds env walk (zs_obs.hpp): 0 strided, 1 one region per XCD (ZS_OBS_WALK)
     int obs_lds = 0;       // k_obs_pipe's walk with LDS-staged 16-B stores (k_obs_lds), channels encoding
     size_t obs_lds_bytes = 0;
     int obs_gather = 0;    // else k_obs_gather<NOBS> usable (NOBS = 1, 2, 4), else 0 (k_obs)
@@ -419,9 +420,14 @@ static bool getenv_off(const char* name) {
 static int choose_layout(zs_handle* h, int want_g, bool fused, int obs_bytes) {
     Dev& d = h->d;
     const int kMax = 64 * 1024;
-    // measured: G=16 and 32 beat 8 and 64 at C3 (E=12, tools/sweep_lanes.sh); G=32 beats 16 and 64
-    // at C4 (E=54: the decisions spread over more lanes)
+    // A launch of many resident rounds is bound by the envs it keeps in flight per CU (k_tick at C3:
+    // 19 -> 15 resident workgroups of G = 8 took the launch from 121 to 153 us), a one-round launch by
+    // the latency of one workgroup.  Measured on one MI355X: G = 8 beats 16 when G = 16 needs more
+    // than two rounds (C3, 65536 envs, E = 12: 121 vs 140 us), G = 16 beats 8 at 8192 and 16384 envs
+    // and at C5 (E = 24); G = 32 beats 16 at C4 (E = 54: the decisions spread over more lanes).
+    const int wave_cap = 4 * ZS_STEP_WAVES;  // one-wave workgroups per CU the register budget admits
     int g0 = want_g > 0 ? want_g : (d.E > 32 ? 32 : 16);
+    if (want_g <= 0 && d.E <= 16 && (long)d.N > 2L * wave_cap * 256 * (64 / 16)) g0 = 8;
     int cand_full = (d.W * d.H <= 65535) ? d.ncand : 0;
     // RNG window: a plain step draws about 1.5 words per actor (shuffle) plus one per attack or heal
     // in range (C4, 54 actors: median 82 words); a window that runs dry sends the leader to HBM
@@ -442,7 +448,7 @@ static int choose_layout(zs_handle* h, int want_g, bool fused, int obs_bytes) {
                     int bytes = tick_layout(ne, d.E, d.DW, rw, cand, lst, d.A, obs_bytes).bytes;
                     if (fused) bytes = std::max(bytes, reset_lds_bytes(d.E, d.DW, d.ncand, lst, obs_bytes));
                     if (bytes > kMax) continue;
-                    int res = std::min(want, 160 * 1024 / bytes);
+                    int res = std::min(std::min(want, wave_cap), 160 * 1024 / bytes);
                     h->want = want;
                     if (res > best_res) {
                         best_res = res;
@@ -670,6 +676,7 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
         // up to 4 per CU.  It pays when every wave walks several envs (C3 65536 envs; at 8192, one env
         // per wave, k_obs_pipe's per-cell stores measured 33 vs 36 us).  ZS_OBS_LDS=0/1 forces either,
         // ZS_OBS_WGS sets the workgroups per CU.
+        if (getenv("ZS_OBS_WALK")) h->obs_walk = atoi(getenv("ZS_OBS_WALK"));
         if (h->obs_pipe && d.obs_enc == ZS_ENC_CHANNELS && !getenv_off("ZS_OBS_LDS")) {
             const int ts = d.obs_dtype == ZS_DTYPE_I64 ? 8 : d.obs_dtype == ZS_DTYPE_I32 ? 4 : 2;
             const size_t lb = (size_t)d.obs_stat * 4 + 4 * ((size_t)L.bytes + (size_t)obs_stage_slot_bytes(ts));
@@ -838,7 +845,8 @@ static int launch_obs(zs_handle* h, void* obs, const uint8_t* mask, hipStream_t 
 #define ZS_PIPE(TT, NB)                                                                                                 \
     do {                                                                                                                \
         if (h->obs_lds)                                                                                                 \
-            hipLaunchKernelGGL((k_obs_lds<TT, NB>), dim3(g), dim3(256), lds, s, d, (TT*)obs, h->obs_l, env0, env1);    \
+            hipLaunchKernelGGL((k_obs_lds<TT, NB>), dim3(g), dim3(256), lds, s, d, (TT*)obs, h->obs_l, env0, env1,     \
+                               (g % 8) == 0 ? h->obs_walk : 0);                                                 \
         else                                                                                                            \
             hipLaunchKernelGGL((k_obs_pipe<TT, NB>), dim3(g), dim3(256), lds, s, d, (TT*)obs, h->obs_l, env0, env1);   \
     } while (0)

@@ -683,7 +683,7 @@ __device__ __forceinline__ void zs_buf_store(__amdgpu_buffer_rsrc_t r, uint32_t 
 // 1-KB wave stores in flight (tools/probe/storeceil.hip: a flat 16-B store stream reaches 6.6-6.7
 // TB/s with ~2-4 MB in flight chip-wide, 5.0-5.4 TB/s with 2048-4096 waves issuing unthrottled).
 #ifndef ZS_OBS_THR
-#define ZS_OBS_THR -1
+#define ZS_OBS_THR 2  // measured on one MI355X, C3 k_obs_lds 343 -> 315 us (4 runs each; vmcnt 1/3/4/6 no better)
 #endif
 #define ZS_STR2(x) #x
 #define ZS_STR(x) ZS_STR2(x)
@@ -726,7 +726,7 @@ __device__ __forceinline__ void obs_stage_flush(const lu8* slot, T* o, int lane)
 }
 
 template <typename T, int NOBS>
-__global__ void __launch_bounds__(256, ZS_OBS_PIPE_WAVES) k_obs_lds(Dev d, T* out, ObsLayout L, int env0, int env1) {
+__global__ void __launch_bounds__(256, ZS_OBS_PIPE_WAVES) k_obs_lds(Dev d, T* out, ObsLayout L, int env0, int env1, int walk) {
     extern __shared__ __align__(16) uint8_t smem[];
     typedef typename obs_stage<T>::type S;
     constexpr int WW = 21, PLANE = WW * WW, PER = (PLANE + 63) / 64, TS = (int)sizeof(T);
@@ -738,9 +738,21 @@ __global__ void __launch_bounds__(256, ZS_OBS_PIPE_WAVES) k_obs_lds(Dev d, T* ou
     lv4u* st4 = (lv4u*)smem;
     obs_stage_static4(d, st4, threadIdx.x, blockDim.x);
     __syncthreads();
-    const int waves = gridDim.x * 4;
-    int e = env0 + xcd_remap(blockIdx.x, gridDim.x) * 4 + wave;
-    if (e >= env1) return;
+    // walk 0: every wave strides over [env0, env1) by the launch's wave count, XCD-contiguous blocks of
+    // envs per round; walk 1 (grid a multiple of 8): XCD x owns the x-th eighth of the range and its
+    // workgroups walk it, so each XCD's stores stream through one region of the tensor
+    int waves = gridDim.x * 4, e, hi = env1;
+    if (walk == 1) {
+        const int x = blockIdx.x & 7, nj = gridDim.x >> 3, r = (env1 - env0 + 7) >> 3;
+        const int lo = env0 + x * r;
+        hi = min(env1, lo + r);
+        waves = nj * 4;
+        e = lo + (int)(blockIdx.x >> 3) * 4 + wave;
+    } else {
+        e = env0 + xcd_remap(blockIdx.x, gridDim.x) * 4 + wave;
+    }
+    if (e >= hi) return;
+    env1 = hi;
     lu8* img = (lu8*)(smem + stat_words * 4 + wave * (L.bytes + SLOT));
     lu8* slot = img + L.bytes;  // 16-B aligned: the static tables, L.bytes and SLOT are multiples of 16
     const li32* pos = (const li32*)(img + L.off_pos);
