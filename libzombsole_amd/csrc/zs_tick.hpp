@@ -85,8 +85,9 @@ struct TickLayout {
     int bytes;
 };
 
-// per-env LDS scalars (MISC rows); rows MISC_N.. hold prev_life[A] then listed[A]
-enum { MISC_T = 0, MISC_DEATHS, MISC_ZD, MISC_EPSTEPS, MISC_PREVZD, MISC_SERIAL, MISC_ODIRTY, MISC_NONPOS, MISC_N };
+// per-env LDS scalars (MISC rows); rows MISC_N.. hold prev_life[A] then listed[A].  MISC_NMOVED and
+// MISC_NORD are scratch rows of the tick's leader / group hand-off (not staged from or to HBM).
+enum { MISC_T = 0, MISC_DEATHS, MISC_ZD, MISC_EPSTEPS, MISC_PREVZD, MISC_SERIAL, MISC_ODIRTY, MISC_NMOVED, MISC_NORD, MISC_N };
 
 __host__ __device__ inline TickLayout tick_layout(int ne, int E, int DW, int rw_cap, int cand_cap, int lists_cap,
                                                   int A, int obs_bytes = 0) {
@@ -689,7 +690,7 @@ __device__ __forceinline__ void rules_check(const Dev& d, const Grp& c, int& end
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void env_step_leader(const Dev& d, Grp& c, const int32_t* actions, double* rew, uint8_t* done_out,
                                 uint8_t* trunc_out, uint8_t* listed_out) {
-    const int A = d.A, E = d.E;
+    const int A = d.A;
     SUB_DECL
     SUB(0);
     // World.get_actions (core.py:80-101): deferred (RNG-drawing) decisions in dict order
@@ -707,6 +708,7 @@ __device__ __forceinline__ void env_step_leader(const Dev& d, Grp& c, const int3
             trunc_out[c.e] = 0;
             c.fin = 0;
             c.respawn = 0;
+            MISC(c, MISC_NMOVED) = -1;  // no cleanup, no second leader part
             return;
         }
         if (LK(c, s) == K_DEFER) {
@@ -756,50 +758,85 @@ __device__ __forceinline__ void env_step_leader(const Dev& d, Grp& c, const int3
         }
     }
     SUB(2);
-    {  // dict order after the tick's moves: unmoved in old order, then movers in execution order
-        int m = 0;
-        for (int k = 0; k < c.n_order; k++) {
-            int s = LO(c, k);
-            if (LR(c, s) != 255) LO(c, m++) = (uint8_t)s;
-        }
-        for (int j = 0; j < nmoved; j++) LO(c, m++) = LM(c, j);
-    }
-    // clean_dead_things (core.py:121-138)
-    if (c.odirty) {
-        for (int w = 0; w < d.OW; w++) {
+    // the group's lanes rebuild the dict order and clean up the dead (env_cleanup_group)
+    MISC(c, MISC_NMOVED) = nmoved;
+    MISC(c, MISC_NORD) = c.n_order;
+    MISC(c, MISC_DEATHS) = c.deaths;
+    MISC(c, MISC_ZD) = c.zd;
+    MISC(c, MISC_ODIRTY) = c.odirty;
+}
+
+// clean_dead_things (core.py:121-138) and the dict order after the tick's moves (unmoved things in the
+// old order, then the movers in execution order, core.py:158-159), by the G lanes of the env: every
+// entry is a lane of a chunk, the survivors are compacted with a ballot, the dead ones leave a DeadBody
+// (any order: two things never share a cell) and are counted with LDS atomics.  The obstacles that
+// dropped to life <= 0 go the same way (one word of present bits per lane).
+template <int G>
+__device__ __forceinline__ void env_cleanup_group(const Dev& d, Grp& c, bool run) {
+    const int A = d.A, j = c.j;
+    const int nm = run ? MISC(c, MISC_NMOVED) : -1;
+    run = run && nm >= 0;  // nm < 0: this step re-raised an agent's exception (debug) and ended there
+    const int K = run ? MISC(c, MISC_NORD) : 0;
+    if (run && MISC(c, MISC_ODIRTY)) {
+        for (int w = j; w < d.OW; w += G) {
             uint32_t* pw = &d.obst_present[(size_t)c.e * d.OW + w];
-            uint32_t dead = *pw & d.obst_nonpos[(size_t)c.e * d.OW + w];
+            const uint32_t pv = *pw;
+            uint32_t dead = pv & d.obst_nonpos[(size_t)c.e * d.OW + w];
             if (dead) {
-                *pw &= ~dead;
-                c.deaths += __popc(dead);
+                *pw = pv & ~dead;
+                __hip_atomic_fetch_add(&MISC(c, MISC_DEATHS), (int)__popc(dead), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 while (dead) {
-                    int oi = 32 * w + __ffs(dead) - 1;
+                    const int32_t op = d.obst_xy[32 * w + __ffs(dead) - 1];
                     dead &= dead - 1;
-                    int32_t op = d.obst_xy[oi];
-                    bm_clr(c, unpack_y(op) * d.W + unpack_x(op));
+                    const int cell = unpack_y(op) * d.W + unpack_x(op);
+                    __hip_atomic_fetch_and(&c.bm[IX(c, cell >> 5)], ~(1u << (cell & 31)), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
             }
         }
-        c.odirty = 0;
     }
-    {
-        uint32_t* deadbits = d.dead + (size_t)c.e * d.DW;
-        int m = 0;
-        for (int k = 0; k < c.n_order; k++) {
-            int s = LO(c, k);
-            if (LL(c, s) <= 0) {
-                int p = LP(c, s), cell = unpack_y(p) * d.W + unpack_x(p);
-                deadbits[cell >> 5] |= 1u << (cell & 31);  // DeadBody decoration
-                bm_clr(c, cell);
+    const int total = run ? K + nm : 0;
+    uint32_t* deadbits = d.dead + (size_t)c.e * d.DW;
+    int kept = 0;
+    for (int b0 = 0; b0 < total; b0 += G) {
+        const int idx = b0 + j;
+        int s = 0;
+        bool keep = false;
+        if (idx < total) {
+            s = idx < K ? LO(c, idx) : LM(c, idx - K);
+            const bool incl = idx >= K || LR(c, s) != 255;
+            keep = incl && LL(c, s) > 0;
+            if (incl && !keep) {
+                const int32_t p = LP(c, s);
+                const int cell = unpack_y(p) * d.W + unpack_x(p);
+                __hip_atomic_fetch_or(&deadbits[cell >> 5], 1u << (cell & 31), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);  // DeadBody decoration
+                __hip_atomic_fetch_and(&c.bm[IX(c, cell >> 5)], ~(1u << (cell & 31)), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
                 LPR(c, s) = 0;
-                c.deaths++;
-                if (s >= A + d.P) c.zd++;
-            } else {
-                LO(c, m++) = (uint8_t)s;
+                __hip_atomic_fetch_add(&MISC(c, MISC_DEATHS), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (s >= A + d.P)
+                    __hip_atomic_fetch_add(&MISC(c, MISC_ZD), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
         }
-        c.n_order = m;
+        const unsigned long long bal = __ballot(keep);
+        const unsigned long long gb = G == 64 ? bal : (bal >> (c.g * G)) & ((1ull << G) - 1ull);
+        if (keep) LO(c, kept + __popcll(gb & ((1ull << j) - 1ull))) = (uint8_t)s;
+        kept += __popcll(gb);
     }
+    if (run && j == 0) MISC(c, MISC_NORD) = kept;
+}
+
+// the rest of the tick after the group's cleanup (leader)
+__device__ __forceinline__ void env_step_leader_b(const Dev& d, Grp& c, double* rew, uint8_t* done_out, uint8_t* trunc_out,
+                                                  uint8_t* listed_out) {
+    const int A = d.A, E = d.E;
+    SUB_DECL
+    SUB(0);
+    c.n_order = MISC(c, MISC_NORD);
+    c.deaths = MISC(c, MISC_DEATHS);
+    c.zd = MISC(c, MISC_ZD);
+    c.odirty = 0;
     SUB(3);
     // reward_tracker.update (gym/reward.py:30-35, 77-86)
     double rs = 0.0;
@@ -984,7 +1021,7 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
         else if (f == MISC_PREVZD) mval = d.scal[S_PREVZD * N + e];
         else if (f == MISC_SERIAL) mval = d.scal[S_SERIAL * N + e];
         else if (f == MISC_ODIRTY) mval = d.scal[S_ODIRTY * N + e];
-        else if (f == MISC_NONPOS) mval = 0;
+        else if (f == MISC_NMOVED || f == MISC_NORD) mval = 0;
         else if (f < MISC_N + A) mval = d.prev_life[(size_t)(f - MISC_N) * N + e];
         else mval = d.listed[(size_t)(f - MISC_N - A) * N + e];
         // occupancy is rebuilt here, not kept in HBM: the map's obstacle cells (static, shared by every
@@ -1052,7 +1089,7 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
             else if (f == MISC_PREVZD) v = d.scal[S_PREVZD * N + e];
             else if (f == MISC_SERIAL) v = d.scal[S_SERIAL * N + e];
             else if (f == MISC_ODIRTY) v = d.scal[S_ODIRTY * N + e];
-            else if (f == MISC_NONPOS) v = 0;
+            else if (f == MISC_NMOVED || f == MISC_NORD) v = 0;
             else if (f < MISC_N + A) v = d.prev_life[(size_t)(f - MISC_N) * N + e];
             else v = d.listed[(size_t)(f - MISC_N - A) * N + e];
             MISC(c, f) = v;
@@ -1148,6 +1185,12 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
         c.serial = MISC(c, MISC_SERIAL);
         c.odirty = MISC(c, MISC_ODIRTY);
         env_step_leader(d, c, actions, rew, done_out, trunc_out, listed_out);
+    }
+    wave_sync();
+    env_cleanup_group<G>(d, c, stepping);
+    wave_sync();
+    if (leader && stepping) {
+        if (MISC(c, MISC_NMOVED) >= 0) env_step_leader_b(d, c, rew, done_out, trunc_out, listed_out);
         if (c.fin && (d.flags & ZS_FLAG_AUTORESET)) {
             needs_reset = 1;
             // rebuilt by the next call's reset work; a list holds each env at most once, so an index
@@ -1192,7 +1235,7 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
             else if (f == MISC_PREVZD) d.scal[S_PREVZD * N + e] = v;
             else if (f == MISC_SERIAL) d.scal[S_SERIAL * N + e] = v;
             else if (f == MISC_ODIRTY) d.scal[S_ODIRTY * N + e] = v;
-            else if (f == MISC_NONPOS) {
+            else if (f == MISC_NMOVED || f == MISC_NORD) {
             } else if (f < MISC_N + A) d.prev_life[(size_t)(f - MISC_N) * N + e] = v;
             else d.listed[(size_t)(f - MISC_N - A) * N + e] = (uint8_t)v;
         }
