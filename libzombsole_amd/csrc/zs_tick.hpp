@@ -693,9 +693,12 @@ __device__ __forceinline__ void env_step_leader(const Dev& d, Grp& c, const int3
     const int A = d.A;
     SUB_DECL
     SUB(0);
-    // World.get_actions (core.py:80-101): deferred (RNG-drawing) decisions in dict order
-    int nact = 0;
-    for (int k = 0; k < c.n_order; k++) {
+    // World.get_actions (core.py:80-101): deferred (RNG-drawing) decisions in dict order (the action
+    // list is already compacted when there are none)
+    int nact = MISC(c, MISC_NMOVED);
+    const bool serial = nact < 0;
+    if (serial) nact = 0;
+    for (int k = 0; k < c.n_order && serial; k++) {
         int s = LO(c, k);
         if (LK(c, s) == K_RAISE) {
             // this agent's next_step raised and the env re-raises (debug, core.py:96-99): the step
@@ -824,19 +827,50 @@ __device__ __forceinline__ void env_cleanup_group(const Dev& d, Grp& c, bool run
         if (keep) LO(c, kept + __popcll(gb & ((1ull << j) - 1ull))) = (uint8_t)s;
         kept += __popcll(gb);
     }
-    if (run && j == 0) MISC(c, MISC_NORD) = kept;
+    // what the leader's respawn and rules read, from the cleaned-up table: present zombies, any player
+    // alive (Rules.players_alive), any agent alive, an alive player off the objectives (Safehouse)
+    int nz = 0;
+    unsigned long long pa = 0ull, aa = 0ull, off = 0ull;
+    const unsigned long long gmask = G == 64 ? ~0ull : ((1ull << G) - 1ull) << (c.g * G);
+    for (int s0 = 0; s0 < (run ? d.E : 0); s0 += G) {
+        const int s = s0 + j;
+        bool z = false, al = false, ag = false, o = false;
+        if (s < d.E) {
+            if (s >= A + d.P) {
+                z = LPR(c, s) != 0;
+            } else {
+                al = LL(c, s) > 0;
+                ag = al && s < A;
+                if (al && d.rules == ZS_RULES_SAFEHOUSE) {
+                    const int32_t p = LP(c, s);
+                    const int cell = unpack_y(p) * d.W + unpack_x(p);
+                    o = !((d.objbits[cell >> 5] >> (cell & 31)) & 1u);
+                }
+            }
+        }
+        nz += __popcll(__ballot(z) & gmask);
+        pa |= __ballot(al) & gmask;
+        aa |= __ballot(ag) & gmask;
+        off |= __ballot(o) & gmask;
+    }
+    if (run && j == 0) {
+        MISC(c, MISC_NORD) = kept;
+        MISC(c, MISC_NMOVED) = nz | (pa ? 1 << 16 : 0) | (aa ? 1 << 17 : 0) | (off ? 1 << 18 : 0);
+    }
 }
 
 // the rest of the tick after the group's cleanup (leader)
 __device__ __forceinline__ void env_step_leader_b(const Dev& d, Grp& c, double* rew, uint8_t* done_out, uint8_t* trunc_out,
                                                   uint8_t* listed_out) {
-    const int A = d.A, E = d.E;
+    const int A = d.A;
     SUB_DECL
     SUB(0);
     c.n_order = MISC(c, MISC_NORD);
     c.deaths = MISC(c, MISC_DEATHS);
     c.zd = MISC(c, MISC_ZD);
     c.odirty = 0;
+    const int gfl = MISC(c, MISC_NMOVED);
+    const int nz = gfl & 0xffff, pa = (gfl >> 16) & 1, aa = (gfl >> 17) & 1, off = (gfl >> 18) & 1;
     SUB(3);
     // reward_tracker.update (gym/reward.py:30-35, 77-86)
     double rs = 0.0;
@@ -856,29 +890,32 @@ __device__ __forceinline__ void env_step_leader_b(const Dev& d, Grp& c, double* 
     // spawn_zombies_to_maintain_minimum (game.py:196-201).  Deferred: the respawn is the step's
     // last RNG consumer and nothing below reads the new zombies except Extermination's "any zombie
     // alive", which only needs to know whether one more zombie gets placed (a free spawn cell).
-    int za0 = 0;
+    int za0 = 0, spawned = 0;
     c.respawn = 0;
-    {
-        int nz = 0;
-        for (int s = A + d.P; s < E; s++) nz += LPR(c, s);
-        if (nz < d.minimum_zombies) {
-            if (d.defer_respawn) {
-                c.respawn = 1;
-                if (nz == 0 && d.rules == ZS_RULES_EXTERMINATION) za0 = any_free_spawn(d, c);
-            } else {
-                spawn_zombies(d, c, d.minimum_zombies - nz);
-            }
+    if (nz < d.minimum_zombies) {
+        if (d.defer_respawn) {
+            c.respawn = 1;
+            if (nz == 0 && d.rules == ZS_RULES_EXTERMINATION) za0 = any_free_spawn(d, c);
+        } else {
+            spawn_zombies(d, c, d.minimum_zombies - nz);
+            spawned = 1;
         }
     }
-    // rules and end-of-game reward (gym_env.py:130-141, gym/multiagent_env.py:143-162)
+    // rules and end-of-game reward (gym_env.py:130-141, gym/multiagent_env.py:143-162); the group's
+    // counts stand unless this step placed zombies (Extermination then looks again)
     int ended, won, tr = 0;
-    rules_check(d, c, ended, won, za0);
+    if (d.rules == ZS_RULES_EVACUATION || (spawned && d.rules == ZS_RULES_EXTERMINATION)) {
+        rules_check(d, c, ended, won, za0);
+    } else {
+        won = pa;
+        ended = d.rules == ZS_RULES_EXTERMINATION ? (!pa || !(nz > 0 || za0))
+                : d.rules == ZS_RULES_SAFEHOUSE   ? (!pa || !off)
+                                                  : !pa;
+    }
     double end_reward = 0.0;
     if (ended) {
         end_reward = won ? 10.0 : -10.0;
     } else {
-        int aa = 0;
-        for (int a = 0; a < A; a++) aa |= LL(c, a) > 0;
         if (!aa) {
             tr = 1;
             end_reward = -10.0;
@@ -1158,6 +1195,29 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
             LK(c, s) = (uint8_t)kind;
             LT(c, s) = tgt;
         }
+    }
+    wave_sync();
+    if (stepping) {
+        // the action list of get_actions (core.py:80-101) in dict order, compacted by the group when no
+        // decision was deferred to the leader (RNG-drawing) or raises: MISC_NMOVED = its length, else -1
+        int nact = 0;
+        unsigned long long special = 0ull;
+        for (int b0 = 0; b0 < n_order; b0 += G) {
+            const int k = b0 + j;
+            int s = 0, kk = K_NONE;
+            if (k < n_order) {
+                s = LO(c, k);
+                kk = LK(c, s);
+            }
+            const bool keep = kk == K_MOVE || kk == K_ATTACK || kk == K_HEAL;
+            const unsigned long long sb = __ballot(kk == K_DEFER || kk == K_RAISE);
+            const unsigned long long kb = __ballot(keep);
+            const unsigned long long gk = G == 64 ? kb : (kb >> (g * G)) & ((1ull << G) - 1ull);
+            special |= G == 64 ? sb : (sb >> (g * G)) & ((1ull << G) - 1ull);
+            if (keep) LPE(c, nact + __popcll(gk & ((1ull << j) - 1ull))) = (uint8_t)s;
+            nact += __popcll(gk);
+        }
+        if (j == 0) MISC(c, MISC_NMOVED) = special ? -1 : nact;
     }
     wave_sync();
     STAMP(2);
