@@ -181,7 +181,8 @@ struct Grp {
 
 // ---------------------------------------------------------------------------
 // RNG: the leader draws pre-tempered words from the LDS window; when it runs dry it reloads
-// the next rw_cap words from the ring by itself (twisting serially if the ring is behind).
+// the next rw_step words (the window size; rw_cap is only the LDS capacity) from the ring by itself
+// (twisting serially if the ring is behind).
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void rng_reload(const Dev& d, Grp& c) {
     uint32_t st = st_advance(c.st0, c.wlen);
@@ -193,12 +194,12 @@ __device__ __forceinline__ void rng_reload(const Dev& d, Grp& c) {
         off = 0;
         ready = 0;
     }
-    int n = d.rw_cap;
+    int n = d.rw_step;  // a multiple of 4 (32 .. 512)
     if ((int)off + n > ZS_MT_N && !ready) {
         mt_twist_serial(ring + (slot ^ 1u) * ZS_MT_N, ring + slot * ZS_MT_N);
         ready = 1;
     }
-    for (int i0 = 0; i0 < n; i0 += 4) {  // 4 loads in flight (n is a multiple of 64)
+    for (int i0 = 0; i0 < n; i0 += 4) {  // 4 loads in flight (a wider batch costs every caller registers)
         uint32_t v[4];
 #pragma unroll
         for (int u = 0; u < 4; u++) {
@@ -238,8 +239,14 @@ __device__ __forceinline__ int rng_int(const Dev& d, Grp& c, int a, int b) { ret
 __device__ __forceinline__ bool in_bounds(const Dev& d, int x, int y) { return x >= 0 && y >= 0 && x < d.W && y < d.H; }
 
 __device__ __forceinline__ bool bm_test(const Grp& c, int cell) { return (c.bm[IX(c, cell >> 5)] >> (cell & 31)) & 1u; }
-__device__ __forceinline__ void bm_set(Grp& c, int cell) { c.bm[IX(c, cell >> 5)] |= 1u << (cell & 31); }
-__device__ __forceinline__ void bm_clr(Grp& c, int cell) { c.bm[IX(c, cell >> 5)] &= ~(1u << (cell & 31)); }
+// set / clear as LDS atomics whose result is unused (ds_or_b32 / ds_and_b32): nothing waits on them, and
+// a later read of the word by this wave is ordered after them
+__device__ __forceinline__ void bm_set(Grp& c, int cell) {
+    __hip_atomic_fetch_or(&c.bm[IX(c, cell >> 5)], 1u << (cell & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void bm_clr(Grp& c, int cell) {
+    __hip_atomic_fetch_and(&c.bm[IX(c, cell >> 5)], ~(1u << (cell & 31)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 
 // things.get(position) is not None
 __device__ __forceinline__ bool occupied(const Dev& d, const Grp& c, int x, int y) {
@@ -730,11 +737,24 @@ __device__ __forceinline__ void env_step_leader(const Dev& d, Grp& c, const int3
         LPE(c, j) = tmp;
     }
     SUB(1);
-    // execute_actions (core.py:103-119)
+    // execute_actions (core.py:103-119).  The next action's actor, kind, target and position are read
+    // ahead: nothing this action does changes them (every actor acts once, and only its own action moves it).
     int nmoved = 0;
+    int s_n = 0, kind_n = K_NONE, tgt_n = 0, p_n = 0;
+    if (nact > 0) {
+        s_n = LPE(c, 0);
+        kind_n = LK(c, s_n);
+        tgt_n = LT(c, s_n);
+        p_n = LP(c, s_n);
+    }
     for (int i = 0; i < nact; i++) {
-        int s = LPE(c, i), kind = LK(c, s), tgt = LT(c, s);
-        int p = LP(c, s), x = unpack_x(p), y = unpack_y(p);
+        const int s = s_n, kind = kind_n, tgt = tgt_n, p = p_n, x = unpack_x(p), y = unpack_y(p);
+        if (i + 1 < nact) {
+            s_n = LPE(c, i + 1);
+            kind_n = LK(c, s_n);
+            tgt_n = LT(c, s_n);
+            p_n = LP(c, s_n);
+        }
         if (kind == K_MOVE) {  // thing_move (core.py:140-166)
             int tx = unpack_x(tgt), ty = unpack_y(tgt);
             if (in_bounds(d, tx, ty) && !bm_test(c, ty * d.W + tx) && d2(x, y, tx, ty) <= 1) {
