@@ -75,15 +75,23 @@ def parse():
     return a
 
 
-def algorithmic_bytes(E, A, occ_bytes, obs_bytes_per_env, mt_words):
-    """SURVEY.md §8(d) per env-step figures, split by kernel.
+# mean MT19937 words drawn per env-step of each preset's workload (oracle/zs_oracle.c, uniform Discrete(7)
+# agents, 24 envs x 300 steps: C2/C3 12.2, C5 23.2; C4 median 82)
+MT_WORDS = {"c2": 12, "c3": 12, "c4": 82, "c5": 23}
 
-    tick: entity SoA read+write (E x 12 B x 2) + MT state (8 B) + MT words consumed x 4 B
-          + occupancy bitmap read (W*H/8 B) + actions (A x 12 B) + rewards (8A) + 3 flag bytes
+
+def algorithmic_bytes(E, A, OW, obs_bytes_per_env, mt_words):
+    """Algorithmic HBM bytes per env-step, split by kernel.
+
+    tick: entity SoA read + write (E x (pos 4 + life 4 + weapon 1 + present 1 + order 1) x 2)
+          + per-env scalars read + write (9 x 4 x 2) + reward tracker / env.agents rows (A x 5 x 2)
+          + RNG stream state (4 x 2) + obstacle-present bits read (4 x OW)
+          + MT words drawn x 12 (the word read, and its share of the twist that made it: 4 read + 4 write)
+          + actions (12 A) + rewards (8 A) + done / truncated / listed (2 + A)
     obs : observation bytes written (A x 3 x 21 x 21 x 8 B for int64)
     The step launch (k_step) carries both when it writes the observations itself (fobs).
     """
-    tick = 2 * E * 12 + 8 + 4 * mt_words + occ_bytes + A * 12 + 8 * A + 3
+    tick = 22 * E + 72 + 10 * A + 8 + 4 * OW + 12 * mt_words + 12 * A + 8 * A + 2 + A
     return tick, obs_bytes_per_env
 
 
@@ -264,8 +272,8 @@ def main():
     m = eng.builder.map
     E = args.agents + args.zombies
     obs_per_env = eng.obs[0].numel() * eng.obs.element_size()
-    mt_words = 40  # measured average MT words per env-step for this workload
-    tick_b, obs_b = algorithmic_bytes(E, args.agents, (m.size[0] * m.size[1] + 7) // 8, obs_per_env, mt_words)
+    n_obst = len(m.obstacles)
+    tick_b, obs_b = algorithmic_bytes(E, args.agents, (n_obst + 31) // 32, obs_per_env, MT_WORDS.get(args.config, 12))
     # per-step kernel time (a step may run its tick and observation kernels in several env chunks
     # on two streams: sum the launches of each kind per step)
     tick_ms = prof["tick_ms"] / prof_steps

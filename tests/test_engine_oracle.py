@@ -224,3 +224,14 @@ def test_city128_gather_paths(staged, monkeypatch):
     run_parity(lambda n: _abi.multi_env_config(n, "safehouse", [], "city128", ["0", "1", "2", "3"],
                                                initial_zombies=50, minimum_zombies=50),
                24, 30, check_state_every=15)
+
+
+def test_rng_window_reload(monkeypatch):
+    """A 32-word RNG window on 54-actor envs (median 82 draws per step): the tick's leader runs its
+    window dry and reloads it from the ring several times per step (core.py:76 shuffle, :168-202
+    attack / heal draws), bit-exact."""
+    monkeypatch.setenv("ZS_RW_NEED", "32")
+    run_parity(lambda n: _abi.multi_env_config(n, "safehouse", [], "city128", ["0", "1", "2", "3"],
+                                               initial_zombies=50, minimum_zombies=50),
+               24, 30, check_state_every=15)
+    run_parity(c2, 128, 60, check_state_every=30, graph=True)
