@@ -199,7 +199,7 @@ __global__ void k_set_state(Dev d, int e, const int32_t* buf) {
     int any_nonpos = 0;
     for (int o = 0; o < d.O; o++) {
         int v = *r++;
-        d.obst_hp[(size_t)e * d.O + o] = v;
+        d.obst_hp[(size_t)e * d.O + o] = (int16_t)v;
         uint32_t* w = &d.obst_nonpos[(size_t)e * d.OW + (o >> 5)];
         *w = v <= 0 ? (*w | (1u << (o & 31))) : (*w & ~(1u << (o & 31)));
         any_nonpos |= v <= 0;
@@ -259,6 +259,8 @@ struct zs_handle {
     int obs_pipe = 0;      // k_obs_pipe<NOBS> usable (NOBS = 1, 2, 4), else 0
     int obs_walk = 0;      // k_obs_lds env walk (zs_obs.hpp): 0 strided, 1 one region per XCD (ZS_OBS_WALK)
     int obs_lds = 0;       // k_obs_pipe's walk with LDS-staged 16-B stores (k_obs_lds), channels encoding
+    int obs_ring = 0;      // k_obs_ring: encoder and writer waves through an LDS ring (ZS_OBS_RING)
+    size_t obs_ring_bytes = 0;
     size_t obs_lds_bytes = 0;
     int obs_gather = 0;    // else k_obs_gather<NOBS> usable (NOBS = 1, 2, 4), else 0 (k_obs)
     int obs_gather_staged = 0;  // k_obs_gather through LDS-staged 16-B stores
@@ -692,6 +694,26 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
                 h->obs_pipe_wgs = wgs;
             }
         }
+        // k_obs_ring (zs_obs.hpp): the k_obs_lds shape with dedicated writer waves.  ZS_OBS_RING=1 enables.
+        if (h->obs_lds && d.obs_enc == ZS_ENC_CHANNELS) {
+            const int ts = d.obs_dtype == ZS_DTYPE_I64 ? 8 : d.obs_dtype == ZS_DTYPE_I32 ? 4 : 2;
+            const size_t rb = (size_t)ring_lds_bytes(16 * d.DW, L.bytes, ts, nobs);
+            const char* rg = getenv("ZS_OBS_RING");
+            if (rb <= 160 * 1024 && rg && atoi(rg) != 0) {
+                const void* fn = nullptr;
+#define ZS_RING_FN(TT)                                                             \
+    fn = nobs == 1 ? (const void*)k_obs_ring<TT, 1> : nobs == 2 ? (const void*)k_obs_ring<TT, 2> \
+                                                                : (const void*)k_obs_ring<TT, 4>
+                if (ts == 8) ZS_RING_FN(int64_t);
+                else if (ts == 4) ZS_RING_FN(int32_t);
+                else ZS_RING_FN(int16_t);
+#undef ZS_RING_FN
+                if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)rb) == hipSuccess) {
+                    h->obs_ring = 1;
+                    h->obs_ring_bytes = rb;
+                }
+            }
+        }
         // k_obs_gather when the store-stream kernel does not apply (e.g. city128's 3689 obstacles):
         // window-only static words and HP instead of per-env staging.  ZS_OBS_GATHER=0 disables.
         if (!h->obs_pipe && !world && d.obs_w == 21 && (nobs == 1 || nobs == 2 || nobs == 4) &&
@@ -841,6 +863,31 @@ static int launch_obs(zs_handle* h, void* obs, const uint8_t* mask, hipStream_t 
     int i0 = -1, i1 = -1;
     if (h->prof) HIPCHK(hipEventRecord(prof_event(h, &i0), s));
     if (env1 < 0) env1 = d.N;
+    if (!mask && h->obs_ring) {  // encoder / writer waves, one workgroup per CU
+        const unsigned g = (unsigned)std::min(env1 - env0, 256);
+        const size_t lds = h->obs_ring_bytes;
+#define ZS_RING(TT, NB) hipLaunchKernelGGL((k_obs_ring<TT, NB>), dim3(g), dim3(64 * (RING_ENC + RING_WRT)), lds, s, d, \
+                                           (TT*)obs, h->obs_l, env0, env1)
+#define ZS_RING_T(TT)                   \
+    if (h->obs_pipe == 1) ZS_RING(TT, 1); \
+    else if (h->obs_pipe == 2) ZS_RING(TT, 2); \
+    else ZS_RING(TT, 4)
+        if (d.obs_dtype == ZS_DTYPE_I64) {
+            ZS_RING_T(int64_t);
+        } else if (d.obs_dtype == ZS_DTYPE_I32) {
+            ZS_RING_T(int32_t);
+        } else {
+            ZS_RING_T(int16_t);
+        }
+#undef ZS_RING_T
+#undef ZS_RING
+        HIPCHK(hipGetLastError());
+        if (h->prof) {
+            HIPCHK(hipEventRecord(prof_event(h, &i1), s));
+            h->ev_obs.push_back({i0, i1});
+        }
+        return ZS_OK;
+    }
     if (!mask && h->obs_pipe) {  // every env of [env0, env1), registered shape: the prefetching store stream
         const unsigned g = (unsigned)std::min((env1 - env0 + 3) / 4, 256 * h->obs_pipe_wgs);
         const size_t lds = h->obs_lds ? h->obs_lds_bytes : (size_t)d.obs_stat * 4 + 4 * (size_t)h->obs_l.bytes;
@@ -1213,6 +1260,12 @@ extern "C" int zs_get_state(zs_handle* h, int32_t env, int32_t* buf_host, void* 
 extern "C" int zs_set_state(zs_handle* h, int32_t env, const int32_t* buf_host, void* stream) {
     if (!h || !buf_host) return fail(ZS_EINVAL, "null argument");
     if (env < 0 || env >= h->d.N) return fail(ZS_EINVAL, "env index out of range");
+    {  // obstacle HP is kept as int16 in HBM (every reachable value fits: MAX_LIFE 200 down to the damage of
+       // one tick below zero); refuse a poke outside that range instead of wrapping it
+        const int32_t* hp = buf_host + ZS_STATE_HEADER + ZS_STATE_ENTITY_WORDS * h->d.E + h->d.E;
+        for (int o = 0; o < h->d.O; o++)
+            if (hp[o] < -32768 || hp[o] > 32767) return fail(ZS_EINVAL, "obstacle life outside the int16 range");
+    }
     hipStream_t s = (hipStream_t)stream;
     HIPCHK(hipSetDevice(h->device));
     HIPCHK(hipMemcpyAsync(h->d_state, buf_host, sizeof(int32_t) * h->state_words, hipMemcpyHostToDevice, s));

@@ -115,7 +115,7 @@ struct Dev {
     int32_t* scal;
     int32_t* prev_life;
     uint8_t* listed;
-    int32_t* obst_hp;
+    int16_t* obst_hp;  // [N][O]; int16: MAX_LIFE 200 down to one tick's damage below 0 (half the obs kernels' reads)
     uint32_t* obst_present;
     uint32_t* obst_nonpos;
     uint32_t* dead;

@@ -412,7 +412,7 @@ __device__ __forceinline__ void obs_prefetch(const Dev& d, int e, ObsPrefetch& f
 #pragma unroll
     for (int i = 0; i < OBS_PF_D; i++) f.dead[i] = dr[min(lane + 64 * i, d.DW - 1)];
     f.opres = d.obst_present[(size_t)ed * d.OW + min(lane, d.OW - 1)];
-    const int32_t* hr = d.obst_hp + (size_t)eh * d.O;
+    const int16_t* hr = d.obst_hp + (size_t)eh * d.O;
 #pragma unroll
     for (int i = 0; i < OBS_PF_H; i++) f.hp[i] = hr[min(lane + 64 * i, d.O - 1)];
 }
@@ -565,7 +565,7 @@ __global__ void __launch_bounds__(256) k_obs_gather(Dev d, T* out, const uint8_t
     const lu32* opres = (const lu32*)(img + L.off_opres);
     const bool ch = d.obs_enc == ZS_ENC_CHANNELS;
     const int C = ch ? 3 : 1;
-    const int32_t* hrow = d.obst_hp + (size_t)e * d.O;
+    const int16_t* hrow = d.obst_hp + (size_t)e * d.O;
     uint32_t sc[NOBS][PER];
     int32_t hv[NOBS][PER];
     // static words of the window cells (out-of-bounds cells read cell 0, discarded below)
@@ -649,9 +649,10 @@ __global__ void __launch_bounds__(256) k_obs_gather(Dev d, T* out, const uint8_t
 template <typename T> struct obs_stage { typedef T type; };
 template <> struct obs_stage<int64_t> { typedef int32_t type; };
 
-// staging bytes per wave: one channels block, shifted by the destination's 16-B phase in elements
-__host__ __device__ constexpr int obs_stage_slot_bytes(int tsize) {
-    return (((3 * 441 + 16 / tsize) * (tsize == 8 ? 4 : tsize) + 15) / 16) * 16;
+// staging bytes: nblk consecutive channels blocks (one agent's, or every agent's of an env), shifted
+// by the destination's 16-B phase in elements
+__host__ __device__ constexpr int obs_stage_slot_bytes(int tsize, int nblk = 1) {
+    return (((nblk * 3 * 441 + 16 / tsize) * (tsize == 8 ? 4 : tsize) + 15) / 16) * 16;
 }
 
 // Stream one staged block to o: slot element k + mis / sizeof(T) holds output element k, so the
@@ -696,10 +697,10 @@ __device__ __forceinline__ void obs_store_throttle() {
 // Stream one staged block to o: slot element k + mis / sizeof(T) holds output element k, so the
 // 16-B chunk q of the destination (counted from the 16-B boundary at or below o) reads the aligned
 // slot elements [q * VPC, (q + 1) * VPC).  The partial chunks at the two ends are element stores.
-template <typename T>
+template <typename T, int NBLK = 1, int THR = ZS_OBS_THR>
 __device__ __forceinline__ void obs_stage_flush(const lu8* slot, T* o, int lane) {
     typedef typename obs_stage<T>::type S;
-    constexpr int TS = (int)sizeof(T), VPC = 16 / TS, NB = 3 * 441 * TS;
+    constexpr int TS = (int)sizeof(T), VPC = 16 / TS, NB = NBLK * 3 * 441 * TS;
     constexpr int NCH = (NB + 15 + 15) / 16;
     const int mis = (int)((uintptr_t)o & 15), shift = mis / TS;
     const ZS_LDS S* sv = (const ZS_LDS S*)slot;
@@ -718,7 +719,7 @@ __device__ __forceinline__ void obs_stage_flush(const lu8* slot, T* o, int lane)
         }
         __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)((k >= k0 && k < kend) ? (uint32_t)(16 * k - mis) : ZS_OOB), 0,
                                                0);
-        obs_store_throttle();
+        if (THR >= 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(THR < 0 ? 0 : THR) : "memory");
     }
     const int nhead = mis ? (16 - mis) / TS : 0, tail0 = (16 * kend - mis) / TS, ntail = (nb - 16 * kend) / TS;
     const int idx = lane < nhead ? lane : (lane >= 32 && lane - 32 < ntail) ? tail0 + lane - 32 : -1;
@@ -807,5 +808,116 @@ __global__ void __launch_bounds__(256, ZS_OBS_PIPE_WAVES) k_obs_lds(Dev d, T* ou
         e += waves;
         if (e >= env1) break;
         build(fa);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_obs_ring: k_obs_lds with the encoding and the store stream on different waves.  A workgroup of
+// RING_ENC encoder waves and RING_WRT writer waves walks envs b, b + G, ... (b = its XCD-contiguous
+// index, G = the grid); encoder waves build an env's image from prefetched registers and encode every
+// agent's block side by side into a ring slot of LDS (at the env's 16-B phase), writer waves stream
+// whole envs from the ring as 16-B stores.  Only RING_WRT waves per CU store, so the chip keeps fewer
+// streams in flight (tools/probe/storeceil.hip: one contiguous block per wave reaches 5.3 TB/s at 2048
+// storing waves, 5.7 at 1024), and the encoders never wait on their own stores.
+// Slot protocol (LDS, this workgroup only): state[q] = 2t + 1 once env t of the workgroup is encoded
+// into slot q = t % RING_SLOTS, 2t + 2 once it is streamed out; the encoder of env t first waits for
+// 2(t - RING_SLOTS) + 2.  Both sides walk t upwards, so the smallest unencoded t always has its slot
+// drained eventually: no wait cycle.  Every wave leaves after its last env.
+// ---------------------------------------------------------------------------
+#ifndef RING_ENC
+#define RING_ENC 6
+#endif
+#ifndef RING_WRT
+#define RING_WRT 2
+#endif
+#ifndef RING_SLOTS
+#define RING_SLOTS 8
+#endif
+#ifndef RING_THR
+#define RING_THR 8
+#endif
+__host__ __device__ constexpr int ring_lds_bytes(int stat_bytes, int img_bytes, int tsize, int nobs) {
+    return stat_bytes + RING_ENC * img_bytes + RING_SLOTS * obs_stage_slot_bytes(tsize, nobs) + 16 * RING_SLOTS;
+}
+
+// The hand-off is LDS-only: a wave's LDS operations complete in order, so waiting for its own LDS
+// traffic (lgkmcnt(0)) before the state store orders the slot's data before the state, and a reader's
+// LDS reads after it sees the state see the data.  No memory fence: a workgroup release would also wait
+// for the writer's global stores still in flight (vmcnt), which is the stream this kernel keeps going.
+__device__ __forceinline__ int ring_state_load(const ZS_LDS int* p) { return *(const volatile ZS_LDS int*)p; }
+__device__ __forceinline__ void ring_state_store(ZS_LDS int* p, int v) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    *(volatile ZS_LDS int*)p = v;
+}
+__device__ __forceinline__ void ring_wait(const ZS_LDS int* p, int v) {
+    while (ring_state_load(p) != v) __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");
+}
+
+template <typename T, int NOBS>
+__global__ void __launch_bounds__(64 * (RING_ENC + RING_WRT), 1) k_obs_ring(Dev d, T* out, ObsLayout L, int env0, int env1) {
+    extern __shared__ __align__(16) uint8_t smem[];
+    typedef typename obs_stage<T>::type S;
+    constexpr int WW = 21, PLANE = WW * WW, PER = (PLANE + 63) / 64, TS = (int)sizeof(T);
+    constexpr int SLOT = obs_stage_slot_bytes(TS, NOBS), BLK = NOBS * 3 * PLANE;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int stat_bytes = 16 * d.DW;
+    lv4u* st4 = (lv4u*)smem;
+    lu8* slots = (lu8*)(smem + stat_bytes + RING_ENC * L.bytes);
+    ZS_LDS int* state = (ZS_LDS int*)(slots + RING_SLOTS * SLOT);
+    obs_stage_static4(d, st4, threadIdx.x, blockDim.x);
+    if (threadIdx.x < RING_SLOTS) state[threadIdx.x] = 0;
+    __syncthreads();
+    const int G = gridDim.x;
+    const int e_first = env0 + xcd_remap(blockIdx.x, G);
+    const int count = e_first < env1 ? (env1 - e_first + G - 1) / G : 0;  // envs of this workgroup
+    if (wave >= RING_ENC) {  // writer
+        for (int t = wave - RING_ENC; t < count; t += RING_WRT) {
+            const int q = t % RING_SLOTS;
+            ring_wait(&state[q], 2 * t + 1);
+            const int e = e_first + t * G;
+            obs_stage_flush<T, NOBS, RING_THR>(slots + q * SLOT, out + (size_t)e * BLK, lane);
+            ring_state_store(&state[q], 2 * t + 2);
+        }
+        return;
+    }
+    // encoder
+    lu8* img = (lu8*)(smem + stat_bytes + wave * L.bytes);
+    const li32* pos = (const li32*)(img + L.off_pos);
+    const int code_s = lane < d.A ? d.agent_codes[lane < d.A ? lane : 0] : (lane < d.A + d.P ? ZS_THING_PLAYER : ZS_THING_ZOMBIE);
+    int t = wave;
+    if (t >= count) return;
+    ObsPrefetch f;
+    obs_prefetch(d, e_first + t * G, f);
+    for (; t < count; t += RING_ENC) {
+        const int e = e_first + t * G;
+        obs_build_compact(d, L, img, f, code_s, lane);
+        if (t + RING_ENC < count) obs_prefetch(d, e + RING_ENC * G, f);
+        wave_sync();
+        obs_window_compact<NOBS>(d, L, img, lane);
+        const int q = t % RING_SLOTS;
+        if (t >= RING_SLOTS) ring_wait(&state[q], 2 * (t - RING_SLOTS) + 2);
+        wave_sync();
+        ZS_LDS S* ot0 = (ZS_LDS S*)(slots + q * SLOT) + (int)((uintptr_t)(out + (size_t)e * BLK) & 15) / TS;
+#pragma unroll
+        for (int a = 0; a < NOBS; a++) {
+            const int32_t ap = pos[a];
+            const int ox = unpack_x(ap) - WW / 2, oy = unpack_y(ap) - WW / 2;
+            const lu8* wm = img + a * PLANE;
+            ZS_LDS S* ot = ot0 + a * 3 * PLANE;
+#pragma unroll
+            for (int i = 0; i < PER; i++) {
+                const int cell = lane + 64 * i;
+                const int cc = cell < PLANE ? cell : PLANE - 1, r = cc / WW, q2 = cc - r * WW;
+                int code, lf, weapon;
+                obs_cell_lds(d, L, st4, img, wm, cc, ox + q2, oy + r, code, lf, weapon);
+                if (cell < PLANE) {
+                    ot[cell] = (S)code;
+                    ot[PLANE + cell] = (S)lf;
+                    ot[2 * PLANE + cell] = (S)weapon;
+                }
+            }
+        }
+        ring_state_store(&state[q], 2 * t + 1);
     }
 }

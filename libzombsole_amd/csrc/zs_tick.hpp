@@ -279,7 +279,7 @@ __device__ __forceinline__ void set_target_life(const Dev& d, Grp& c, int tgt, i
         return;
     }
     int oi = -tgt - 1;
-    d.obst_hp[(size_t)c.e * d.O + oi] = v;
+    d.obst_hp[(size_t)c.e * d.O + oi] = (int16_t)v;
     uint32_t* w = &d.obst_nonpos[(size_t)c.e * d.OW + (oi >> 5)];
     uint32_t bit = 1u << (oi & 31);
     *w = v <= 0 ? (*w | bit) : (*w & ~bit);

@@ -134,6 +134,7 @@ PATHS = {
     "obs_gather_lds": {"ZS_FOBS": "0", "ZS_OBS_PIPE": "0", "ZS_OBS_GATHER_LDS": "1"},  # ... with 16-B stores
     "obs_pipe_cells": {"ZS_OBS_LDS": "0"},          # k_obs_pipe's per-cell stores instead of k_obs_lds
     "obs_lds": {"ZS_OBS_LDS": "1"},                 # k_obs_lds at any env count
+    "obs_ring": {"ZS_OBS_LDS": "1", "ZS_OBS_RING": "1"},  # encoder / writer waves through an LDS ring
     "obs_scan": {"ZS_OBS_WIN": "0"},                # per-cell entity scan instead of the window map
     "obs_scan_in_step": {"ZS_OBS_WIN": "0", "ZS_FOBS": "1"},
     "obs_scell": {"ZS_OBS_STAT": "0"},              # per-cell static words instead of LDS bitmaps
