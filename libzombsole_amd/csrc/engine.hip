@@ -200,6 +200,7 @@ __global__ void k_set_state(Dev d, int e, const int32_t* buf) {
     for (int o = 0; o < d.O; o++) {
         int v = *r++;
         d.obst_hp[(size_t)e * d.O + o] = (int16_t)v;
+        d.hp_dirty[e] = 0xffffffffu;
         uint32_t* w = &d.obst_nonpos[(size_t)e * d.OW + (o >> 5)];
         *w = v <= 0 ? (*w | (1u << (o & 31))) : (*w & ~(1u << (o & 31)));
         any_nonpos |= v <= 0;
@@ -623,6 +624,15 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
     TRY(dalloc(h, &d.prev_life, (size_t)d.A * N));
     TRY(dalloc(h, &d.listed, (size_t)d.A * N));
     TRY(dalloc(h, &d.obst_hp, (size_t)d.O * N));
+    TRY(dalloc(h, &d.hp_dirty, N));
+    {
+        std::vector<int16_t> init(std::max(d.O, 1), 0);
+        for (int i = 0; i < d.O; i++) init[i] = (int16_t)(okind[i] == ZS_THING_BOX ? 10 : 200);  // Box / Wall MAX_LIFE
+        int16_t* p_init;
+        TRY(dupload(h, &p_init, init));
+        d.hp_init = p_init;
+        d.hp_chunk = std::max(1, (d.O + 31) / 32);
+    }
     TRY(dalloc(h, &d.obst_present, (size_t)d.OW * N));
     TRY(dalloc(h, &d.obst_nonpos, (size_t)d.OW * N));
     TRY(dalloc(h, &d.dead, (size_t)d.DW * N));

@@ -116,6 +116,12 @@ struct Dev {
     int32_t* prev_life;
     uint8_t* listed;
     int16_t* obst_hp;  // [N][O]; int16: MAX_LIFE 200 down to one tick's damage below 0 (half the obs kernels' reads)
+    // [N]: bit k set once an obstacle of chunk k (obstacles k * hp_chunk .. + hp_chunk - 1) may have left
+    // its MAX_LIFE (set_target_life, zs_set_state); a clean chunk's HP is hp_init's, so the observation
+    // kernels read it from that shared static row (cache-resident) instead of the env's row in HBM
+    uint32_t* hp_dirty;
+    const int16_t* hp_init;  // [O] Box / Wall MAX_LIFE
+    int hp_chunk;            // ceil(O / 32)
     uint32_t* obst_present;
     uint32_t* obst_nonpos;
     uint32_t* dead;

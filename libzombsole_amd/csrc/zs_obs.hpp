@@ -393,11 +393,14 @@ struct ObsPrefetch {
     uint32_t dead[OBS_PF_D];
     uint32_t opres;                   // lane w < OW
     int32_t hp[OBS_PF_H];
+    uint32_t dirty_ahead;             // d.hp_dirty of the env this prefetch was told to look ahead to
 };
 
 // Every load is unconditional (addresses clamped into the row): a load under a lane predicate
 // becomes a branch whose join needs the loaded value, i.e. a wait right after the prefetch.
-__device__ __forceinline__ void obs_prefetch(const Dev& d, int e, ObsPrefetch& f) {
+// dirty = d.hp_dirty[e], loaded by an earlier prefetch (its `ahead` env): an obstacle of a clean chunk
+// reads hp_init instead of the env's row, and the address select waits on nothing in flight.
+__device__ __forceinline__ void obs_prefetch(const Dev& d, int e, int ahead, uint32_t dirty, ObsPrefetch& f) {
     const int lane = threadIdx.x & 63, N = d.N;
     const int s = lane < d.E ? lane : d.E - 1;
 #ifndef ZS_OBS_DIAG
@@ -414,7 +417,11 @@ __device__ __forceinline__ void obs_prefetch(const Dev& d, int e, ObsPrefetch& f
     f.opres = d.obst_present[(size_t)ed * d.OW + min(lane, d.OW - 1)];
     const int16_t* hr = d.obst_hp + (size_t)eh * d.O;
 #pragma unroll
-    for (int i = 0; i < OBS_PF_H; i++) f.hp[i] = hr[min(lane + 64 * i, d.O - 1)];
+    for (int i = 0; i < OBS_PF_H; i++) {
+        const int o = min(lane + 64 * i, d.O - 1);
+        f.hp[i] = (((dirty >> (o / d.hp_chunk)) & 1u) ? hr : d.hp_init)[o];
+    }
+    f.dirty_ahead = d.hp_dirty[ahead];
 }
 
 // The compact image (obs_cell_lds) of one env from its prefetched registers.  Lane l holds the HP of
@@ -476,10 +483,12 @@ __global__ void __launch_bounds__(256, ZS_OBS_PIPE_WAVES) k_obs_pipe(Dev d, T* o
     const int code_s = lane < d.A ? (ch ? d.agent_codes[lane < d.A ? lane : 0] : ZS_THING_AGENT)
                                   : (lane < d.A + d.P ? ZS_THING_PLAYER : ZS_THING_ZOMBIE);
     ObsPrefetch f;
-    obs_prefetch(d, e, f);
+    obs_prefetch(d, e, min(e + waves, env1 - 1), d.hp_dirty[e], f);
     for (; e < env1; e += waves) {
         obs_build_compact(d, L, img, f, code_s, lane);  // the image of env e from the registers
-        obs_prefetch(d, min(e + waves, env1 - 1), f);  // the next env (the last wave re-reads its own)
+        // the next env (the last wave re-reads its own), with the hp_dirty word its prefetch loaded
+        const int en = min(e + waves, env1 - 1);
+        obs_prefetch(d, en, min(en + waves, env1 - 1), f.dirty_ahead, f);
         wave_sync();
         obs_window_compact<NOBS>(d, L, img, lane);
         wave_sync();
@@ -552,6 +561,7 @@ __global__ void __launch_bounds__(256) k_obs_gather(Dev d, T* out, const uint8_t
     lu8* img = (lu8*)(smem + wave * (L.bytes + SLOT));
     lu8* slot = img + L.bytes;
     const int N = d.N, W = d.W, H = d.H;
+    const uint32_t hpd = d.hp_dirty[e];  // arrives with obs_build's loads, used two load rounds later
     obs_build(d, L, img, e, [&](int s, int& p, int& lf, int& wp, int& pr) {
         p = d.pos[(size_t)s * N + e];
         lf = d.life[(size_t)s * N + e];
@@ -581,13 +591,16 @@ __global__ void __launch_bounds__(256) k_obs_gather(Dev d, T* out, const uint8_t
             sc[a][i] = (uint32_t)d.scell[inb ? y * W + x : 0];
         }
     }
-    // HP of the window cells' obstacles (cells without one read obstacle 0, discarded below)
+    // HP of the window cells' obstacles (cells without one read obstacle 0, discarded below); a clean
+    // chunk's HP from the shared hp_init row
+    const uint32_t dirty = hpd;
 #pragma unroll
     for (int a = 0; a < NOBS; a++)
 #pragma unroll
         for (int i = 0; i < PER; i++) {
             const int oi = (int)(sc[a][i] & SC_OBST_MASK) - 1;
-            hv[a][i] = hrow[oi > 0 ? oi : 0];
+            const int o = oi > 0 ? oi : 0;
+            hv[a][i] = (((dirty >> (o / d.hp_chunk)) & 1u) ? hrow : d.hp_init)[o];
         }
     // the store stream: LDS and registers only
 #pragma unroll 1
@@ -794,16 +807,25 @@ __global__ void __launch_bounds__(256, ZS_OBS_PIPE_WAVES) k_obs_lds(Dev d, T* ou
         }
     };
     ObsPrefetch fa, fb;
-    obs_prefetch(d, e, fa);
-    obs_prefetch(d, min(e + waves, env1 - 1), fb);
+    {
+        const int e1 = min(e + waves, env1 - 1);
+        obs_prefetch(d, e, min(e + 2 * waves, env1 - 1), d.hp_dirty[e], fa);
+        obs_prefetch(d, e1, min(e1 + 2 * waves, env1 - 1), d.hp_dirty[e1], fb);
+    }
     build(fa);
     for (;;) {
-        obs_prefetch(d, min(e + 2 * waves, env1 - 1), fa);
+        {
+            const int en = min(e + 2 * waves, env1 - 1);
+            obs_prefetch(d, en, min(en + 2 * waves, env1 - 1), fa.dirty_ahead, fa);
+        }
         process(e);
         e += waves;
         if (e >= env1) break;
         build(fb);
-        obs_prefetch(d, min(e + 2 * waves, env1 - 1), fb);
+        {
+            const int en = min(e + 2 * waves, env1 - 1);
+            obs_prefetch(d, en, min(en + 2 * waves, env1 - 1), fb.dirty_ahead, fb);
+        }
         process(e);
         e += waves;
         if (e >= env1) break;
@@ -888,11 +910,17 @@ __global__ void __launch_bounds__(64 * (RING_ENC + RING_WRT), 1) k_obs_ring(Dev 
     int t = wave;
     if (t >= count) return;
     ObsPrefetch f;
-    obs_prefetch(d, e_first + t * G, f);
+    {
+        const int e0 = e_first + t * G;
+        obs_prefetch(d, e0, t + RING_ENC < count ? e0 + RING_ENC * G : e0, d.hp_dirty[e0], f);
+    }
     for (; t < count; t += RING_ENC) {
         const int e = e_first + t * G;
         obs_build_compact(d, L, img, f, code_s, lane);
-        if (t + RING_ENC < count) obs_prefetch(d, e + RING_ENC * G, f);
+        if (t + RING_ENC < count) {
+            const int en = e + RING_ENC * G;
+            obs_prefetch(d, en, t + 2 * RING_ENC < count ? en + RING_ENC * G : en, f.dirty_ahead, f);
+        }
         wave_sync();
         obs_window_compact<NOBS>(d, L, img, lane);
         const int q = t % RING_SLOTS;

@@ -280,6 +280,7 @@ __device__ __forceinline__ void set_target_life(const Dev& d, Grp& c, int tgt, i
     }
     int oi = -tgt - 1;
     d.obst_hp[(size_t)c.e * d.O + oi] = (int16_t)v;
+    d.hp_dirty[c.e] |= 1u << (oi / d.hp_chunk);
     uint32_t* w = &d.obst_nonpos[(size_t)c.e * d.OW + (oi >> 5)];
     uint32_t bit = 1u << (oi & 31);
     *w = v <= 0 ? (*w | bit) : (*w & ~bit);
