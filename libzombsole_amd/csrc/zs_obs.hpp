@@ -847,16 +847,16 @@ __global__ void __launch_bounds__(256, ZS_OBS_PIPE_WAVES) k_obs_lds(Dev d, T* ou
 // drained eventually: no wait cycle.  Every wave leaves after its last env.
 // ---------------------------------------------------------------------------
 #ifndef RING_ENC
-#define RING_ENC 6
+#define RING_ENC 12
 #endif
 #ifndef RING_WRT
-#define RING_WRT 2
+#define RING_WRT 4
 #endif
 #ifndef RING_SLOTS
 #define RING_SLOTS 8
 #endif
 #ifndef RING_THR
-#define RING_THR 8
+#define RING_THR 16
 #endif
 __host__ __device__ constexpr int ring_lds_bytes(int stat_bytes, int img_bytes, int tsize, int nobs) {
     return stat_bytes + RING_ENC * img_bytes + RING_SLOTS * obs_stage_slot_bytes(tsize, nobs) + 16 * RING_SLOTS;

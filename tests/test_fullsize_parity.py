@@ -122,10 +122,26 @@ def test_c2_4096_graph():
 
 
 def test_c2_4096_one_obs_workgroup_per_cu(monkeypatch):
-    """ZS_OBS_WGS=1: the persistent observation kernel at 1 workgroup per CU walks 4 envs per wave at 4 096."""
+    """ZS_OBS_WGS=1: the persistent observation kernel (k_obs_lds, the int64 ring off) at 1 workgroup
+    per CU walks 4 envs per wave at 4 096."""
     monkeypatch.setenv("ZS_OBS_WGS", "1")
     monkeypatch.setenv("ZS_OBS_LDS", "1")
+    monkeypatch.setenv("ZS_OBS_RING", "0")
     run_full(c3, 4096, 40, seed0=99)
+
+
+def test_c2_4096_ring(monkeypatch):
+    """k_obs_ring (encoder / writer waves through an LDS ring; C3's default) at 4 096 envs: 16 envs per
+    workgroup, every ring slot reused."""
+    monkeypatch.setenv("ZS_OBS_LDS", "1")
+    monkeypatch.setenv("ZS_OBS_RING", "1")
+    run_full(c3, 4096, 40, seed0=1234)
+
+
+def test_c5_65536_int16_ring(monkeypatch):
+    """k_obs_ring on C5's int16 blocks of 4 agents (10 584-B envs, two 16-B phases)."""
+    monkeypatch.setenv("ZS_OBS_RING", "1")
+    run_full(c5, 65536, 12, min_resets=0)
 
 
 def test_c2_4096_one_obs_workgroup_per_cu_cells(monkeypatch):
