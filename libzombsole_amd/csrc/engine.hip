@@ -213,6 +213,7 @@ __global__ void k_set_state(Dev d, int e, const int32_t* buf) {
     for (int a = 0; a < d.A; a++) d.prev_life[(size_t)a * N + e] = *r++;
     for (int a = 0; a < d.A; a++) d.listed[(size_t)a * N + e] = (uint8_t)*r++;
     for (int w = 0; w < d.DW; w++) d.dead[(size_t)e * d.DW + w] = (uint32_t)*r++;
+    d.dead_dirty[e] = 0xffffffffu;
 }
 
 __global__ void k_init_pending(Dev d, int* list, int* count) {
@@ -636,6 +637,14 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
     TRY(dalloc(h, &d.obst_present, (size_t)d.OW * N));
     TRY(dalloc(h, &d.obst_nonpos, (size_t)d.OW * N));
     TRY(dalloc(h, &d.dead, (size_t)d.DW * N));
+    TRY(dalloc(h, &d.dead_dirty, N));
+    {
+        std::vector<uint32_t> zero(std::max(d.DW, 1), 0u);
+        uint32_t* p_zero;
+        TRY(dupload(h, &p_zero, zero));
+        d.dead_zero = p_zero;
+        d.dead_chunk = std::max(1, (d.DW + 31) / 32);
+    }
     TRY(dalloc(h, &d.ring, (size_t)ZS_RING_WORDS * N));
     TRY(dalloc(h, &d.rngst, N));
     TRY(dalloc(h, &d.seeds, N));

@@ -122,6 +122,12 @@ struct Dev {
     uint32_t* hp_dirty;
     const int16_t* hp_init;  // [O] Box / Wall MAX_LIFE
     int hp_chunk;            // ceil(O / 32)
+    // [N]: bit k set once a dead-body word of chunk k (words k * dead_chunk .. + dead_chunk - 1) may be
+    // non-zero (tick cleanup, zs_set_state; k_reset clears it with the row): the prefetching observation
+    // kernels read a clean chunk from dead_zero, so an env with few bodies reads few dead words
+    uint32_t* dead_dirty;
+    const uint32_t* dead_zero;  // [DW] zeros
+    int dead_chunk;             // ceil(DW / 32)
     uint32_t* obst_present;
     uint32_t* obst_nonpos;
     uint32_t* dead;

@@ -393,14 +393,18 @@ struct ObsPrefetch {
     uint32_t dead[OBS_PF_D];
     uint32_t opres;                   // lane w < OW
     int32_t hp[OBS_PF_H];
-    uint32_t dirty_ahead;             // d.hp_dirty of the env this prefetch was told to look ahead to
+    zs_v2u dirty_ahead;               // obs_dirty of the env this prefetch was told to look ahead to
 };
+
+// {hp_dirty, dead_dirty} of env e
+__device__ __forceinline__ zs_v2u obs_dirty(const Dev& d, int e) { return zs_v2u{d.hp_dirty[e], d.dead_dirty[e]}; }
 
 // Every load is unconditional (addresses clamped into the row): a load under a lane predicate
 // becomes a branch whose join needs the loaded value, i.e. a wait right after the prefetch.
-// dirty = d.hp_dirty[e], loaded by an earlier prefetch (its `ahead` env): an obstacle of a clean chunk
-// reads hp_init instead of the env's row, and the address select waits on nothing in flight.
-__device__ __forceinline__ void obs_prefetch(const Dev& d, int e, int ahead, uint32_t dirty, ObsPrefetch& f) {
+// dirty = obs_dirty(d, e), loaded by an earlier prefetch (its `ahead` env): an obstacle of a clean HP
+// chunk reads hp_init instead of the env's row, a clean dead-body chunk reads dead_zero, and the address
+// selects wait on nothing in flight.
+__device__ __forceinline__ void obs_prefetch(const Dev& d, int e, int ahead, zs_v2u dirty, ObsPrefetch& f) {
     const int lane = threadIdx.x & 63, N = d.N;
     const int s = lane < d.E ? lane : d.E - 1;
 #ifndef ZS_OBS_DIAG
@@ -413,15 +417,18 @@ __device__ __forceinline__ void obs_prefetch(const Dev& d, int e, int ahead, uin
     f.pr = d.present[(size_t)s * N + ee];
     const uint32_t* dr = d.dead + (size_t)ed * d.DW;
 #pragma unroll
-    for (int i = 0; i < OBS_PF_D; i++) f.dead[i] = dr[min(lane + 64 * i, d.DW - 1)];
+    for (int i = 0; i < OBS_PF_D; i++) {
+        const int w = min(lane + 64 * i, d.DW - 1);
+        f.dead[i] = (((dirty.y >> (w / d.dead_chunk)) & 1u) ? dr : d.dead_zero)[w];
+    }
     f.opres = d.obst_present[(size_t)ed * d.OW + min(lane, d.OW - 1)];
     const int16_t* hr = d.obst_hp + (size_t)eh * d.O;
 #pragma unroll
     for (int i = 0; i < OBS_PF_H; i++) {
         const int o = min(lane + 64 * i, d.O - 1);
-        f.hp[i] = (((dirty >> (o / d.hp_chunk)) & 1u) ? hr : d.hp_init)[o];
+        f.hp[i] = (((dirty.x >> (o / d.hp_chunk)) & 1u) ? hr : d.hp_init)[o];
     }
-    f.dirty_ahead = d.hp_dirty[ahead];
+    f.dirty_ahead = obs_dirty(d, ahead);
 }
 
 // The compact image (obs_cell_lds) of one env from its prefetched registers.  Lane l holds the HP of
@@ -483,10 +490,10 @@ __global__ void __launch_bounds__(256, ZS_OBS_PIPE_WAVES) k_obs_pipe(Dev d, T* o
     const int code_s = lane < d.A ? (ch ? d.agent_codes[lane < d.A ? lane : 0] : ZS_THING_AGENT)
                                   : (lane < d.A + d.P ? ZS_THING_PLAYER : ZS_THING_ZOMBIE);
     ObsPrefetch f;
-    obs_prefetch(d, e, min(e + waves, env1 - 1), d.hp_dirty[e], f);
+    obs_prefetch(d, e, min(e + waves, env1 - 1), obs_dirty(d, e), f);
     for (; e < env1; e += waves) {
         obs_build_compact(d, L, img, f, code_s, lane);  // the image of env e from the registers
-        // the next env (the last wave re-reads its own), with the hp_dirty word its prefetch loaded
+        // the next env (the last wave re-reads its own), with the dirty masks its prefetch loaded
         const int en = min(e + waves, env1 - 1);
         obs_prefetch(d, en, min(en + waves, env1 - 1), f.dirty_ahead, f);
         wave_sync();
@@ -809,8 +816,8 @@ __global__ void __launch_bounds__(256, ZS_OBS_PIPE_WAVES) k_obs_lds(Dev d, T* ou
     ObsPrefetch fa, fb;
     {
         const int e1 = min(e + waves, env1 - 1);
-        obs_prefetch(d, e, min(e + 2 * waves, env1 - 1), d.hp_dirty[e], fa);
-        obs_prefetch(d, e1, min(e1 + 2 * waves, env1 - 1), d.hp_dirty[e1], fb);
+        obs_prefetch(d, e, min(e + 2 * waves, env1 - 1), obs_dirty(d, e), fa);
+        obs_prefetch(d, e1, min(e1 + 2 * waves, env1 - 1), obs_dirty(d, e1), fb);
     }
     build(fa);
     for (;;) {
@@ -912,7 +919,7 @@ __global__ void __launch_bounds__(64 * (RING_ENC + RING_WRT), 1) k_obs_ring(Dev 
     ObsPrefetch f;
     {
         const int e0 = e_first + t * G;
-        obs_prefetch(d, e0, t + RING_ENC < count ? e0 + RING_ENC * G : e0, d.hp_dirty[e0], f);
+        obs_prefetch(d, e0, t + RING_ENC < count ? e0 + RING_ENC * G : e0, obs_dirty(d, e0), f);
     }
     for (; t < count; t += RING_ENC) {
         const int e = e_first + t * G;

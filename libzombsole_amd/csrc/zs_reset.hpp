@@ -112,6 +112,7 @@ __device__ __forceinline__ void reset_env_wave(const Dev& d, const ResetLds& L, 
         L.bm[w] = d.obstbits[w];
         d.dead[(size_t)e * d.DW + w] = 0;
     }
+    if (lane == 0) d.dead_dirty[e] = 0u;
     int nonpos = 0;
     for (int w = lane; w < d.OW; w += 64) {
         int nb = min(32, d.O - 32 * w);

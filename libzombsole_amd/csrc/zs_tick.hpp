@@ -835,6 +835,8 @@ __device__ __forceinline__ void env_cleanup_group(const Dev& d, Grp& c, bool run
                 const int cell = unpack_y(p) * d.W + unpack_x(p);
                 __hip_atomic_fetch_or(&deadbits[cell >> 5], 1u << (cell & 31), __ATOMIC_RELAXED,
                                       __HIP_MEMORY_SCOPE_AGENT);  // DeadBody decoration
+                __hip_atomic_fetch_or(&d.dead_dirty[c.e], 1u << ((cell >> 5) / d.dead_chunk), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
                 __hip_atomic_fetch_and(&c.bm[IX(c, cell >> 5)], ~(1u << (cell & 31)), __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_WORKGROUP);
                 LPR(c, s) = 0;
