@@ -32,6 +32,7 @@ __global__ void __launch_bounds__(64, ZS_STEP_WAVES) k_step(Dev d, int n_reset, 
                                              uint8_t* done_out, uint8_t* trunc_out, uint8_t* listed_out,
                                              uint8_t* reset_out, int* reset_list, int* reset_count,
                                              const int* cur_list, const int* cur_count, int* err_out, void* obs_out) {
+    if (d.gstep_adv && blockIdx.x == 0 && threadIdx.x == 0) *d.gstep_adv += 1;
     if ((int)blockIdx.x < n_reset)
         reset_role(d, 1, cur_list, cur_count, nullptr, err_out, blockIdx.x, n_reset, d.fobs ? obs_out : nullptr);
     else
@@ -104,17 +105,21 @@ __global__ void k_gen_actions(Dev d, uint64_t step, int n_discrete, int32_t* act
     act[(size_t)i * 3 + 2] = c_discrete[id][2];
 }
 
-// The work-list counters a step appends to; inside zs_step_graph's graph also the policy's step
-// counter, advanced here, after k_gen_actions_dev (earlier in the same stream) has read it.
-__global__ void k_zero2(int* a, int* b, uint64_t* step) {
+// The work-list counters a step appends to (eager zs_step; inside zs_step_graph's graph
+// k_gen_actions_dev zeroes them).
+__global__ void k_zero2(int* a, int* b) {
     if (threadIdx.x == 0 && a) *a = 0;
     if (threadIdx.x == 1 && b) *b = 0;
-    if (threadIdx.x == 2 && step) *step += 1;
 }
 
-// The same policy with the step read from device memory (zs_step_graph); k_zero2 advances it.
-__global__ void __launch_bounds__(256) k_gen_actions_dev(Dev d, const uint64_t* ctr, int n_discrete, int32_t* act) {
+// The same policy with the step read from device memory (zs_step_graph; the step launch advances
+// it, Dev::gstep_adv).  Its first workgroup also zeroes the work-list counters the step appends to
+// (k_zero2's job in eager steps): one launch fewer ahead of the tick.
+__global__ void __launch_bounds__(256) k_gen_actions_dev(Dev d, const uint64_t* ctr, int n_discrete, int32_t* act,
+                                                         int* z0, int* z1) {
     const uint64_t step = ctr[0];
+    if (blockIdx.x == 0 && threadIdx.x == 0 && z0) *z0 = 0;
+    if (blockIdx.x == 0 && threadIdx.x == 1 && z1) *z1 = 0;
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < d.N * d.A) {
         int e = i / d.A, a = i - e * d.A;
@@ -271,8 +276,9 @@ struct zs_handle {
     // pending-reset lists), replayed on the caller's stream; keyed by the caller's buffers
     hipGraphExec_t gexec[2] = {nullptr, nullptr};
     const void* gkey[8] = {};
-    uint64_t* d_gstep = nullptr;  // [0] policy step counter (k_gen_actions_dev reads, k_zero2 advances)
+    uint64_t* d_gstep = nullptr;  // [0] policy step counter (k_gen_actions_dev reads, the step launch advances)
     int capturing = 0;            // zs_step is being captured by zs_step_graph
+    int forked = 0;               // zs_step_graph recorded ev_rfork itself (before its policy launch)
     int memset_nodes = 0;         // ZS_GRAPH_MEMSET=1: list counters zeroed by hipMemsetAsync (diagnostic)
     // step pipeline: the tick in `chunks` env ranges on the caller's stream, each range's observations
     // on s_obs as soon as its tick is done
@@ -1115,7 +1121,8 @@ extern "C" int zs_step(zs_handle* h, const int32_t* actions_dev, void* obs_dev, 
         side = h->reset_side != 0;
         hipStream_t rs = s;
         if (side) {  // fork: the reset work sees everything the caller queued before this call
-            HIPCHK(hipEventRecord(h->ev_rfork, s));
+            // (zs_step_graph records the fork ahead of its policy launch: the actions are not an input)
+            if (!h->forked) HIPCHK(hipEventRecord(h->ev_rfork, s));
             HIPCHK(hipStreamWaitEvent(h->s_reset, h->ev_rfork, 0));
             rs = h->s_reset;
         }
@@ -1134,12 +1141,15 @@ extern "C" int zs_step(zs_handle* h, const int32_t* actions_dev, void* obs_dev, 
     if (h->memset_nodes) {
         HIPCHK(hipMemsetAsync(h->d_rcount + q, 0, sizeof(int), s));
         if (h->d.defer_respawn) HIPCHK(hipMemsetAsync(h->d.resp_count, 0, sizeof(int), s));
-        if (h->capturing) hipLaunchKernelGGL(k_zero2, dim3(1), dim3(64), 0, s, nullptr, nullptr, h->d_gstep);
-    } else {
-        hipLaunchKernelGGL(k_zero2, dim3(1), dim3(64), 0, s, h->d_rcount + q, h->d.defer_respawn ? h->d.resp_count : nullptr,
-                           h->capturing ? h->d_gstep : nullptr);
+    } else if (!h->capturing) {
+        hipLaunchKernelGGL(k_zero2, dim3(1), dim3(64), 0, s, h->d_rcount + q, h->d.defer_respawn ? h->d.resp_count : nullptr);
     }
     HIPCHK(hipGetLastError());
+    struct GstepScope {  // the step launch advances the graph's policy counter while capturing
+        Dev& d;
+        GstepScope(Dev& dd, uint64_t* g) : d(dd) { d.gstep_adv = g; }
+        ~GstepScope() { d.gstep_adv = nullptr; }
+    } gscope(h->d, h->capturing ? h->d_gstep : nullptr);
     const int K = (!h->fused && !h->d.fobs && obs_dev) ? h->chunks : 1;
     if (K > 1) {
         if (side) HIPCHK(hipStreamWaitEvent(s, h->ev_rjoin, 0));
@@ -1151,6 +1161,7 @@ extern "C" int zs_step(zs_handle* h, const int32_t* actions_dev, void* obs_dev, 
             rc = launch_tick(h, actions_dev, rewards_dev, done_dev, trunc_dev, listed_dev, reset_dev, h->d_rlist[q],
                              h->d_rcount + q, nullptr, s, c0, c1);
             if (rc) return rc;
+            h->d.gstep_adv = nullptr;  // advanced once per step
             HIPCHK(hipEventRecord(h->ev_chunk[c], s));
             HIPCHK(hipStreamWaitEvent(h->s_obs, h->ev_chunk[c], 0));
             rc = launch_obs(h, obs_dev, nullptr, h->s_obs, c0, c1);
@@ -1229,9 +1240,21 @@ extern "C" int zs_step_graph(zs_handle* h, uint64_t step0, int32_t n_discrete, i
                 break;
             }
             const int n = h->d.N * h->d.A;
+            if (!h->fused && h->reset_side) {  // the reset work does not wait for the policy
+                if (hipEventRecord(h->ev_rfork, cs) != hipSuccess) {
+                    (void)hipStreamEndCapture(cs, &graph);
+                    if (graph) (void)hipGraphDestroy(graph);
+                    rc = fail(ZS_EHIP, "hipEventRecord (reset fork) failed");
+                    break;
+                }
+                h->forked = 1;
+            }
+            const bool zero = !h->memset_nodes;  // the step's work-list counters (k_zero2 in eager steps)
             hipLaunchKernelGGL(k_gen_actions_dev, dim3((n + 255) / 256), dim3(256), 0, cs, h->d, h->d_gstep, n_discrete,
-                               actions_dev);
+                               actions_dev, zero ? h->d_rcount + (1 - h->rpar) : nullptr,
+                               zero && h->d.defer_respawn ? h->d.resp_count : nullptr);
             rc = zs_step(h, actions_dev, obs_dev, rewards_dev, done_dev, trunc_dev, listed_dev, reset_dev, cs);
+            h->forked = 0;
             hipError_t ce = hipStreamEndCapture(cs, &graph);
             if (rc == ZS_OK && ce != hipSuccess) rc = fail(ZS_EHIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(ce));
             if (rc == ZS_OK) {

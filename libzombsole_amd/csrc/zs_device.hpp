@@ -133,6 +133,9 @@ struct Dev {
     uint32_t* dead;
     uint32_t* ring;
     uint32_t* rngst;
+    // inside zs_step_graph's graph: the policy's step counter, advanced by the step launch's first
+    // workgroup (k_gen_actions_dev, earlier in the same stream, has read it); null otherwise
+    uint64_t* gstep_adv;
     uint64_t* seeds;
     int32_t* cand;
     int* resp_list;   // envs whose respawn the tick deferred to k_respawn [N]

@@ -1354,6 +1354,7 @@ template <int G>
 __global__ void __launch_bounds__(64, ZS_STEP_WAVES) k_tick(Dev d, const int32_t* actions, double* rew, uint8_t* done_out,
                                              uint8_t* trunc_out, uint8_t* listed_out, uint8_t* reset_out,
                                              int* reset_list, int* reset_count, void* obs_out, int env0, int env1) {
+    if (d.gstep_adv && blockIdx.x == 0 && threadIdx.x == 0) *d.gstep_adv += 1;
     tick_wg<G>(d, xcd_remap(blockIdx.x, gridDim.x), actions, rew, done_out, trunc_out, listed_out, reset_out, reset_list,
                reset_count, obs_out, env0, env1);
 }
