@@ -905,7 +905,7 @@ __global__ void __launch_bounds__(64 * (RING_ENC + RING_WRT), 1) k_obs_ring(Dev 
             const int q = t % RING_SLOTS;
             ring_wait(&state[q], 2 * t + 1);
             const int e = e_first + t * G;
-            obs_stage_flush<T, NOBS, RING_THR>(slots + q * SLOT, out + (size_t)e * BLK, lane);
+            if (!(ZS_OBS_DIAG & 8)) obs_stage_flush<T, NOBS, RING_THR>(slots + q * SLOT, out + (size_t)e * BLK, lane);
             ring_state_store(&state[q], 2 * t + 2);
         }
         return;
@@ -935,7 +935,7 @@ __global__ void __launch_bounds__(64 * (RING_ENC + RING_WRT), 1) k_obs_ring(Dev 
         wave_sync();
         ZS_LDS S* ot0 = (ZS_LDS S*)(slots + q * SLOT) + (int)((uintptr_t)(out + (size_t)e * BLK) & 15) / TS;
 #pragma unroll
-        for (int a = 0; a < NOBS; a++) {
+        for (int a = 0; a < ((ZS_OBS_DIAG & 16) ? 0 : NOBS); a++) {
             const int32_t ap = pos[a];
             const int ox = unpack_x(ap) - WW / 2, oy = unpack_y(ap) - WW / 2;
             const lu8* wm = img + a * PLANE;
