@@ -891,7 +891,9 @@ static int launch_obs(zs_handle* h, void* obs, const uint8_t* mask, hipStream_t 
     if (h->prof) HIPCHK(hipEventRecord(prof_event(h, &i0), s));
     if (env1 < 0) env1 = d.N;
     if (!mask && h->obs_ring) {  // encoder / writer waves, one workgroup per CU
-        const unsigned g = (unsigned)std::min(env1 - env0, 256);
+        const int ts = d.obs_dtype == ZS_DTYPE_I64 ? 8 : d.obs_dtype == ZS_DTYPE_I32 ? 4 : 2;
+        const int pair = ring_pair(ts, h->obs_pipe);
+        const unsigned g = (unsigned)std::min((env1 - env0 + pair - 1) / pair, 256);
         const size_t lds = h->obs_ring_bytes;
 #define ZS_RING(TT, NB) hipLaunchKernelGGL((k_obs_ring<TT, NB>), dim3(g), dim3(64 * (RING_ENC + RING_WRT)), lds, s, d, \
                                            (TT*)obs, h->obs_l, env0, env1)

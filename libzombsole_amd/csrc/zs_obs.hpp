@@ -848,10 +848,13 @@ __global__ void __launch_bounds__(256, ZS_OBS_PIPE_WAVES) k_obs_lds(Dev d, T* ou
 // whole envs from the ring as 16-B stores.  Only RING_WRT waves per CU store, so the chip keeps fewer
 // streams in flight (tools/probe/storeceil.hip: one contiguous block per wave reaches 5.3 TB/s at 2048
 // storing waves, 5.7 at 1024), and the encoders never wait on their own stores.
-// Slot protocol (LDS, this workgroup only): state[q] = 2t + 1 once env t of the workgroup is encoded
-// into slot q = t % RING_SLOTS, 2t + 2 once it is streamed out; the encoder of env t first waits for
-// 2(t - RING_SLOTS) + 2.  Both sides walk t upwards, so the smallest unencoded t always has its slot
-// drained eventually: no wait cycle.  Every wave leaves after its last env.
+// The ring's unit is one env, or two adjacent envs when that makes the unit's output 16-B aligned
+// (ring_pair); a unit's envs are encoded by different encoder waves into one slot and streamed out
+// by one writer as one contiguous block.
+// Slot protocol (LDS, this workgroup only): per slot q and env h of the unit, state = 2u + 1 once env
+// h of unit u (q = u % slots) is encoded, 2u + 2 once the unit is streamed out; the encoder of unit
+// u first waits for 2(u - slots) + 2.  Both sides walk upwards, so the smallest unencoded env always
+// has its slot drained eventually: no wait cycle.  Every wave leaves after its last env.
 // ---------------------------------------------------------------------------
 #ifndef RING_ENC
 #define RING_ENC 12
@@ -865,8 +868,16 @@ __global__ void __launch_bounds__(256, ZS_OBS_PIPE_WAVES) k_obs_lds(Dev d, T* ou
 #ifndef RING_THR
 #define RING_THR 16
 #endif
+// Envs per ring unit: two when one env's block ends off a 16-B boundary and two end on one (C5's
+// int16 10 584-B envs): a unit is then one aligned, contiguous stream, with no partial 16-B chunk
+// shared by two writers.
+__host__ __device__ constexpr int ring_pair(int tsize, int nobs) {
+    return (nobs * 3 * 441 * tsize) % 16 != 0 && (2 * nobs * 3 * 441 * tsize) % 16 == 0 ? 2 : 1;
+}
 __host__ __device__ constexpr int ring_lds_bytes(int stat_bytes, int img_bytes, int tsize, int nobs) {
-    return stat_bytes + RING_ENC * img_bytes + RING_SLOTS * obs_stage_slot_bytes(tsize, nobs) + 16 * RING_SLOTS;
+    return stat_bytes + RING_ENC * img_bytes +
+           (RING_SLOTS / ring_pair(tsize, nobs)) * obs_stage_slot_bytes(tsize, nobs * ring_pair(tsize, nobs)) +
+           16 * RING_SLOTS;
 }
 
 // The hand-off is LDS-only: a wave's LDS operations complete in order, so waiting for its own LDS
@@ -888,25 +899,36 @@ __global__ void __launch_bounds__(64 * (RING_ENC + RING_WRT), 1) k_obs_ring(Dev 
     extern __shared__ __align__(16) uint8_t smem[];
     typedef typename obs_stage<T>::type S;
     constexpr int WW = 21, PLANE = WW * WW, PER = (PLANE + 63) / 64, TS = (int)sizeof(T);
-    constexpr int SLOT = obs_stage_slot_bytes(TS, NOBS), BLK = NOBS * 3 * PLANE;
+    constexpr int PAIR = ring_pair(TS, NOBS), US = RING_SLOTS / PAIR;  // envs per unit, unit slots
+    constexpr int SLOT = obs_stage_slot_bytes(TS, NOBS * PAIR), BLK = NOBS * 3 * PLANE;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int stat_bytes = 16 * d.DW;
     lv4u* st4 = (lv4u*)smem;
     lu8* slots = (lu8*)(smem + stat_bytes + RING_ENC * L.bytes);
-    ZS_LDS int* state = (ZS_LDS int*)(slots + RING_SLOTS * SLOT);
+    // state[PAIR * slot + h]: the protocol word of the unit's env h
+    ZS_LDS int* state = (ZS_LDS int*)(slots + US * SLOT);
     obs_stage_static4(d, st4, threadIdx.x, blockDim.x);
     if (threadIdx.x < RING_SLOTS) state[threadIdx.x] = 0;
     __syncthreads();
+    // unit g covers envs env0 + PAIR * g + h (h < PAIR, below env1); this workgroup's units are
+    // g_first, g_first + G, ...; its items (envs) t = PAIR * u + h, the last one possibly absent
     const int G = gridDim.x;
-    const int e_first = env0 + xcd_remap(blockIdx.x, G);
-    const int count = e_first < env1 ? (env1 - e_first + G - 1) / G : 0;  // envs of this workgroup
+    const int g_first = xcd_remap(blockIdx.x, G), n_units = (env1 - env0 + PAIR - 1) / PAIR;
+    const int ucount = g_first < n_units ? (n_units - g_first + G - 1) / G : 0;
+    const int count = ucount ? min(PAIR * ucount, env1 - env0 - PAIR * (g_first + (ucount - 1) * G) + PAIR * (ucount - 1))
+                             : 0;
+    auto unit_env = [&](int u) { return env0 + PAIR * (g_first + u * G); };
     if (wave >= RING_ENC) {  // writer
-        for (int t = wave - RING_ENC; t < count; t += RING_WRT) {
-            const int q = t % RING_SLOTS;
-            ring_wait(&state[q], 2 * t + 1);
-            const int e = e_first + t * G;
-            if (!(ZS_OBS_DIAG & 8)) obs_stage_flush<T, NOBS, RING_THR>(slots + q * SLOT, out + (size_t)e * BLK, lane);
-            ring_state_store(&state[q], 2 * t + 2);
+        for (int u = wave - RING_ENC; u < ucount; u += RING_WRT) {
+            const int q = u % US, e = unit_env(u);
+            const bool whole = PAIR * u + PAIR <= count;
+            for (int h = 0; h < PAIR; h++)
+                if (PAIR * u + h < count) ring_wait(&state[PAIR * q + h], 2 * u + 1);
+            if (!(ZS_OBS_DIAG & 8)) {
+                if (whole) obs_stage_flush<T, NOBS * PAIR, RING_THR>(slots + q * SLOT, out + (size_t)e * BLK, lane);
+                else obs_stage_flush<T, NOBS, RING_THR>(slots + q * SLOT, out + (size_t)e * BLK, lane);
+            }
+            for (int h = 0; h < PAIR; h++) ring_state_store(&state[PAIR * q + h], 2 * u + 2);
         }
         return;
     }
@@ -914,26 +936,24 @@ __global__ void __launch_bounds__(64 * (RING_ENC + RING_WRT), 1) k_obs_ring(Dev 
     lu8* img = (lu8*)(smem + stat_bytes + wave * L.bytes);
     const li32* pos = (const li32*)(img + L.off_pos);
     const int code_s = lane < d.A ? d.agent_codes[lane < d.A ? lane : 0] : (lane < d.A + d.P ? ZS_THING_PLAYER : ZS_THING_ZOMBIE);
+    auto item_env = [&](int t) { return unit_env(t / PAIR) + t % PAIR; };
     int t = wave;
     if (t >= count) return;
     ObsPrefetch f;
-    {
-        const int e0 = e_first + t * G;
-        obs_prefetch(d, e0, t + RING_ENC < count ? e0 + RING_ENC * G : e0, obs_dirty(d, e0), f);
-    }
+    obs_prefetch(d, item_env(t), t + RING_ENC < count ? item_env(t + RING_ENC) : item_env(t), obs_dirty(d, item_env(t)), f);
     for (; t < count; t += RING_ENC) {
-        const int e = e_first + t * G;
+        const int u = t / PAIR, h = t % PAIR, e = item_env(t);
         obs_build_compact(d, L, img, f, code_s, lane);
         if (t + RING_ENC < count) {
-            const int en = e + RING_ENC * G;
-            obs_prefetch(d, en, t + 2 * RING_ENC < count ? en + RING_ENC * G : en, f.dirty_ahead, f);
+            const int en = item_env(t + RING_ENC);
+            obs_prefetch(d, en, t + 2 * RING_ENC < count ? item_env(t + 2 * RING_ENC) : en, f.dirty_ahead, f);
         }
         wave_sync();
         obs_window_compact<NOBS>(d, L, img, lane);
-        const int q = t % RING_SLOTS;
-        if (t >= RING_SLOTS) ring_wait(&state[q], 2 * (t - RING_SLOTS) + 2);
+        const int q = u % US;
+        if (u >= US) ring_wait(&state[PAIR * q + h], 2 * (u - US) + 2);
         wave_sync();
-        ZS_LDS S* ot0 = (ZS_LDS S*)(slots + q * SLOT) + (int)((uintptr_t)(out + (size_t)e * BLK) & 15) / TS;
+        ZS_LDS S* ot0 = (ZS_LDS S*)(slots + q * SLOT) + (int)((uintptr_t)(out + (size_t)(e - h) * BLK) & 15) / TS + h * BLK;
 #pragma unroll
         for (int a = 0; a < ((ZS_OBS_DIAG & 16) ? 0 : NOBS); a++) {
             const int32_t ap = pos[a];
@@ -953,6 +973,6 @@ __global__ void __launch_bounds__(64 * (RING_ENC + RING_WRT), 1) k_obs_ring(Dev 
                 }
             }
         }
-        ring_state_store(&state[q], 2 * t + 1);
+        ring_state_store(&state[PAIR * q + h], 2 * u + 1);
     }
 }

@@ -144,6 +144,13 @@ def test_c5_65536_int16_ring(monkeypatch):
     run_full(c5, 65536, 12, min_resets=0)
 
 
+def test_c5_odd_int16_ring_pairs(monkeypatch):
+    """k_obs_ring's two-env units (C5's int16 envs end on 16-B boundaries in pairs) over an odd env
+    count: one workgroup's last unit holds a single env."""
+    monkeypatch.setenv("ZS_OBS_RING", "1")
+    run_full(c5, 4097, 24, seed0=555, min_resets=0)
+
+
 def test_c2_4096_one_obs_workgroup_per_cu_cells(monkeypatch):
     """The same walk through k_obs_pipe's per-cell stores."""
     monkeypatch.setenv("ZS_OBS_WGS", "1")
