@@ -85,71 +85,49 @@ __device__ __forceinline__ uint32_t wr_sub(const R& r, int q) {
     return q == 0 ? r.word[0] : q == 1 ? r.word[1] : q == 2 ? r.word[2] : r.word[3];
 }
 
-#define WR_H 4  // rejection hypotheses evaluated per batch (one ballot each)
-
 // `count` consecutive draws _randbelow(b_t), b_t = n - t * dstep (dstep 0: a fixed bound; 1: the
 // decreasing bounds of a Fisher-Yates pass), all in wave-uniform control flow.  Draw t consumes
 // words until one word w gives (w >> (32 - bitlen(b_t))) < b_t (random.py:239-249).
 //
-// One round per 64-word sub-block: lane l evaluates its word under each hypothesis "h words of
-// this round before me were rejected" (then it serves draw t = idx - h, idx = l - start), one
-// ballot per hypothesis, WR_H hypotheses per batch; the scalar unit walks the chain of first
-// rejections h = 0, 1, 2, ... and evaluates further batches until the chain reaches the end of the
-// sub-block (or of the draws), so a round resolves any number of rejections.  Every accepted lane
-// then hands its draw's value to put(t, value) for t < krec.  Advances r past the consumed words.
+// One round per 64-word sub-block: the word of lane l serves draw t_l = done + (l - start) - H_l,
+// H_l = the rejected words of this round before lane l, a sequential definition.  It is solved as a
+// fixed point: from H = 0, every lane evaluates its word, one ballot gives the rejections, prefix
+// counts give the next H; the first lane is exact after one pass and lane start + j after j + 1, so
+// the iteration ends, and a pass that leaves the ballot unchanged satisfies the recurrence at every
+// lane, i.e. is its solution.  A change of H moves a lane's bound by one (dstep 1) or not at all
+// (dstep 0), which flips its outcome only at a bit-length or threshold edge: usually two passes.
+// Every accepted lane then hands its draw's value to put(t, value) for t < krec.  Advances r past
+// the consumed words.
 template <class R, class Put>
 __device__ __forceinline__ void wave_draws(R& r, int n, int dstep, int count, int krec, Put put) {
     const int lane = threadIdx.x;
+    const unsigned long long below = (1ull << lane) - 1ull;
     int done = 0;
     while (done < count) {
         if (r.pos >= WR_BLOCK) rng_block_load(r, st_advance(r.st, WR_BLOCK));
         const int q = r.pos >> 6, base = q << 6, start = r.pos - base;
         const uint32_t w = wr_sub(r, q);
         const int idx = lane - start;
-        unsigned long long rmask = 0;
-        int c = start, end = start;
-        for (int hb = 0; c < 64; hb += WR_H) {
-            unsigned long long rej[WR_H], live[WR_H];
-#pragma unroll
-            for (int u = 0; u < WR_H; u++) {
-                const int h = hb + u;
-                int t = done + idx - h;  // draw this word serves under hypothesis h
-                bool lv = idx >= h && t < count;
-                int b = n - t * dstep;
-                int kk = 32 - __clz(max(b, 1));
-                bool rj = lv && (w >> (32 - kk)) >= (uint32_t)b;
-                rej[u] = __ballot(rj);
-                live[u] = __ballot(lv);
-            }
-            // walk the chain of rejections through this batch
-            bool resolved = false;
-#pragma unroll
-            for (int u = 0; u < WR_H; u++) {
-                const unsigned long long from = ~0ull << c;  // c < 64 here
-                unsigned long long m = rej[u] & from, lm = live[u] & from;
-                if (!m) {  // every live word from c on is accepted
-                    end = lm ? 64 - __clzll((long long)lm) : c;
-                    resolved = true;
-                    break;
-                }
-                int p = __ffsll((long long)m) - 1;
-                rmask |= 1ull << p;
-                c = p + 1;
-                end = c;
-                if (c >= 64) break;
-            }
-            if (resolved) break;
-        }
-        // accepted lanes in [start, end) store the value of the draw they served
-        const bool mine = lane >= start && lane < end && !((rmask >> lane) & 1ull);
-        const int hl = __popcll(rmask & ((1ull << lane) - 1ull));
-        const int t = done + idx - hl;
-        if (mine && t < krec) {
-            int b = n - t * dstep;
+        unsigned long long rej = 0ull, prev;
+        int t;
+        bool lv, rj;
+        do {
+            prev = rej;
+            t = done + idx - __popcll(rej & below);
+            lv = idx >= 0 && t < count;
+            const int b = n - t * dstep;
+            const int kk = 32 - __clz(max(b, 1));
+            rj = lv && (w >> (32 - kk)) >= (uint32_t)b;
+            rej = __ballot(rj);
+        } while (rej != prev);
+        // live lanes (t < count) are a prefix of [start, 64): t never decreases along the lanes
+        const unsigned long long live = __ballot(lv);
+        if (lv && !rj && t < krec) {
+            const int b = n - t * dstep;
             put(t, w >> (32 - (32 - __clz(b))));
         }
-        done += (end - start) - __popcll(rmask);
-        r.pos = base + end;
+        done += __popcll(live) - __popcll(rej);
+        r.pos = base + 64 - __clzll((long long)live);
     }
     wave_sync();
 }
