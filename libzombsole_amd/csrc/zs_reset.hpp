@@ -107,6 +107,9 @@ __device__ __forceinline__ void reset_env_wave(const Dev& d, const ResetLds& L, 
     const int lane = threadIdx.x, N = d.N, E = d.E, A = d.A, P = d.P;
     RST_DECL
     RST(0);
+    // the stream state first: the ring staging below waits on it
+    const uint32_t st_in = d.rngst[e];
+    const int serial0 = d.scal[S_SERIAL * N + e];
     // new World: the map's obstacles (all present, HP carried over), no things, no decoration
     for (int w = lane; w < d.DW; w += 64) {
         L.bm[w] = d.obstbits[w];
@@ -129,7 +132,6 @@ __device__ __forceinline__ void reset_env_wave(const Dev& d, const ResetLds& L, 
     WaveRng r;
     r.ring = d.ring + (size_t)e * ZS_RING_WORDS;
     r.lr = L.tw;
-    const uint32_t st_in = d.rngst[e];
     wave_rng_stage(r, st_in);
     rng_block_load(r, st_in);
     RST(1);
@@ -164,7 +166,7 @@ __device__ __forceinline__ void reset_env_wave(const Dev& d, const ResetLds& L, 
         }
     }
     wave_sync();
-    int n_order = 0, serial = d.scal[S_SERIAL * N + e];
+    int n_order = 0, serial = serial0;
     int rc = ZS_OK;
     RST(2);
     // spawn_players, spawn_agents (game.py:181-187): fail_if_cant=True

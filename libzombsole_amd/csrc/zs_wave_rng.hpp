@@ -23,12 +23,28 @@ struct WaveRng {
 };
 
 // stage the env's ring into LDS: the current slot, and the next one when it is already twisted
+// (both slots' loads in one round: 10 words per lane each)
 __device__ __forceinline__ void wave_rng_stage(WaveRng& r, uint32_t st) {
+    constexpr int K = (ZS_MT_N + 63) / 64;
     const uint32_t slot = (st >> 10) & 1u, ready = (st >> 11) & 1u;
     const int lane = threadIdx.x;
-    stage_in(r.ring + slot * ZS_MT_N, ZS_MT_N, lane, 64, r.lr + slot * ZS_MT_N, [](int k) { return k; });
-    if (ready)
-        stage_in(r.ring + (slot ^ 1u) * ZS_MT_N, ZS_MT_N, lane, 64, r.lr + (slot ^ 1u) * ZS_MT_N, [](int k) { return k; });
+    const uint32_t* a = r.ring + slot * ZS_MT_N;
+    const uint32_t* b = r.ring + (slot ^ 1u) * ZS_MT_N;
+    uint32_t va[K], vb[K];
+#pragma unroll
+    for (int u = 0; u < K; u++) va[u] = a[min(lane + 64 * u, ZS_MT_N - 1)];
+    if (ready) {
+#pragma unroll
+        for (int u = 0; u < K; u++) vb[u] = b[min(lane + 64 * u, ZS_MT_N - 1)];
+    }
+#pragma unroll
+    for (int u = 0; u < K; u++)
+        if (lane + 64 * u < ZS_MT_N) r.lr[slot * ZS_MT_N + lane + 64 * u] = va[u];
+    if (ready) {
+#pragma unroll
+        for (int u = 0; u < K; u++)
+            if (lane + 64 * u < ZS_MT_N) r.lr[(slot ^ 1u) * ZS_MT_N + lane + 64 * u] = vb[u];
+    }
     r.dirty = 0;
     wave_sync();
 }
