@@ -271,6 +271,7 @@ struct zs_handle {
     size_t obs_lds_bytes = 0;
     int obs_gather = 0;    // else k_obs_gather<NOBS> usable (NOBS = 1, 2, 4), else 0 (k_obs)
     int obs_gather_staged = 0;  // k_obs_gather through LDS-staged 16-B stores
+    int obs_gather_stat = 0;    // k_obs_gather reads the static words from LDS tables (ZS_OBS_GATHER_STAT)
     ObsLayout obs_gl;      // its per-wave image
     // zs_step_graph: one captured hipGraph per autoreset-list parity (the step alternates the two
     // pending-reset lists), replayed on the caller's stream; keyed by the caller's buffers
@@ -754,7 +755,11 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
                 const int ts = d.obs_dtype == ZS_DTYPE_I64 ? 8 : d.obs_dtype == ZS_DTYPE_I32 ? 4 : 2;
                 const char* gl = getenv("ZS_OBS_GATHER_LDS");
                 h->obs_gather_staged = d.obs_enc == ZS_ENC_CHANNELS && (gl ? atoi(gl) != 0 : false) &&
-                                       4 * (G.bytes + obs_lds_slot_bytes(ts)) <= 64 * 1024;
+                                       4 * (G.bytes + obs_stage_slot_bytes(ts)) + (d.obs_stat ? 16 * d.DW : 0) <= 64 * 1024;
+                // static words from the LDS tables (rank order, as obs_stat) instead of a global load
+                // round per window cell
+                const size_t gb = 4 * ((size_t)G.bytes + (h->obs_gather_staged ? obs_stage_slot_bytes(ts) : 0));
+                h->obs_gather_stat = d.obs_stat && gb + 16 * (size_t)d.DW <= 64 * 1024 && !getenv_off("ZS_OBS_GATHER_STAT");
             }
         }
         // with the store-stream kernel available the observations are its job (measured faster than
@@ -951,13 +956,14 @@ static int launch_obs(zs_handle* h, void* obs, const uint8_t* mask, hipStream_t 
     if (h->obs_gather) {  // one env per wave, four per workgroup, window-only fetches
         const unsigned g = (unsigned)((d.N + 3) / 4);
         const int ts = d.obs_dtype == ZS_DTYPE_I64 ? 8 : d.obs_dtype == ZS_DTYPE_I32 ? 4 : 2;
-        const size_t lds = 4 * ((size_t)h->obs_gl.bytes + (h->obs_gather_staged ? obs_lds_slot_bytes(ts) : 0));
+        const size_t lds = 4 * ((size_t)h->obs_gl.bytes + (h->obs_gather_staged ? obs_stage_slot_bytes(ts) : 0)) +
+                           (h->obs_gather_stat ? 16 * (size_t)d.DW : 0);
 #define ZS_GATH(TT, NB)                                                                                              \
     do {                                                                                                             \
         if (h->obs_gather_staged)                                                                                    \
-            hipLaunchKernelGGL((k_obs_gather<TT, NB, true>), dim3(g), dim3(256), lds, s, d, (TT*)obs, mask, h->obs_gl); \
+            hipLaunchKernelGGL((k_obs_gather<TT, NB, true>), dim3(g), dim3(256), lds, s, d, (TT*)obs, mask, h->obs_gl, h->obs_gather_stat); \
         else                                                                                                         \
-            hipLaunchKernelGGL((k_obs_gather<TT, NB, false>), dim3(g), dim3(256), lds, s, d, (TT*)obs, mask, h->obs_gl); \
+            hipLaunchKernelGGL((k_obs_gather<TT, NB, false>), dim3(g), dim3(256), lds, s, d, (TT*)obs, mask, h->obs_gl, h->obs_gather_stat); \
     } while (0)
 #define ZS_GATH_T(TT)                         \
     if (h->obs_gather == 1) ZS_GATH(TT, 1);     \

@@ -520,141 +520,6 @@ __global__ void __launch_bounds__(256, ZS_OBS_PIPE_WAVES) k_obs_pipe(Dev d, T* o
     }
 }
 
-// 16-B store stream of one staged observation block (k_obs_lds, k_obs_gather<..., true>)
-
-// staging bytes per wave: one channels block at any 16-B phase of its destination
-__host__ __device__ constexpr int obs_lds_slot_bytes(int tsize) { return ((3 * 441 * tsize + 31) / 16) * 16; }
-
-// Stream one staged channels block (3 x 441 values of T, written at slot + (o & 15)) to o: every
-// full 16-B chunk one aligned 16-B store, the partial chunks at the two ends element stores.
-template <typename T>
-__device__ __forceinline__ void obs_block_flush(const lu8* slot, T* o, int lane) {
-    constexpr int TS = (int)sizeof(T), ABYTES = 3 * 441 * TS, NCH = obs_lds_slot_bytes(TS) / 16;
-    const int mis = (int)((uintptr_t)o & 15);
-    const ZS_LDS T* ot = (const ZS_LDS T*)(slot + mis);
-    // chunk k = bytes [16k, 16k + 16) from the 16-B boundary at or below the block start
-    uint8_t* g0 = (uint8_t*)o - mis;
-    const int nb = mis + ABYTES, kend = nb >> 4, k0 = mis ? 1 : 0;
-#pragma unroll
-    for (int i = 0; i < (NCH + 63) / 64; i++) {
-        const int k = lane + 64 * i;
-        if (k >= k0 && k < kend) *(zs_v4u*)(g0 + 16 * k) = *(const ZS_LDS zs_v4u*)(slot + 16 * k);
-    }
-    const int nhead = mis ? (16 - mis) / TS : 0, tail0 = (16 * kend - mis) / TS, ntail = (nb - 16 * kend) / TS;
-    if (lane < nhead) o[lane] = ot[lane];
-    else if (lane >= 32 && lane - 32 < ntail) o[tail0 + lane - 32] = ot[tail0 + lane - 32];
-}
-
-// ---------------------------------------------------------------------------
-// k_obs_gather: the registered shape (surroundings, width 21, NOBS observations per env) on maps
-// whose obstacle HP row is too large to stage per env (city128: 3689 obstacles, 14.7 KB, which
-// left k_obs one wave per CU slot).  Only the observed cells' data is fetched: per lane, the
-// static per-cell words of its NOBS x 7 window cells, then the HP of those cells' obstacles, each
-// batch issued as one group of loads before any store (one wait per batch, no global load inside
-// the store loop).  The wave image holds the window maps, entities, dead-body and obstacle-present
-// bits only (~5 KB at city128), so four waves per workgroup and many workgroups per CU hide the two
-// load round trips.
-// ---------------------------------------------------------------------------
-// STAGED: channels blocks go through an LDS slot per wave and out as 16-B stores (obs_block_flush).
-template <typename T, int NOBS, bool STAGED>
-__global__ void __launch_bounds__(256) k_obs_gather(Dev d, T* out, const uint8_t* mask, ObsLayout L) {
-    extern __shared__ __align__(16) uint8_t smem[];
-    constexpr int WW = 21, PLANE = WW * WW, PER = (PLANE + 63) / 64;
-    constexpr int SLOT = STAGED ? obs_lds_slot_bytes((int)sizeof(T)) : 0;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int e = xcd_remap(blockIdx.x, gridDim.x) * 4 + wave;
-    if (e >= d.N) return;
-    if (mask && !mask[e]) return;
-    lu8* img = (lu8*)(smem + wave * (L.bytes + SLOT));
-    lu8* slot = img + L.bytes;
-    const int N = d.N, W = d.W, H = d.H;
-    const uint32_t hpd = d.hp_dirty[e];  // arrives with obs_build's loads, used two load rounds later
-    obs_build(d, L, img, e, [&](int s, int& p, int& lf, int& wp, int& pr) {
-        p = d.pos[(size_t)s * N + e];
-        lf = d.life[(size_t)s * N + e];
-        wp = d.weapon[(size_t)s * N + e];
-        pr = d.present[(size_t)s * N + e];
-    });
-    const li32* pos = (const li32*)(img + L.off_pos);
-    const li32* life = (const li32*)(img + L.off_life);
-    const li32* cw = (const li32*)(img + L.off_cw);
-    const lu32* dead = (const lu32*)(img + L.off_dead);
-    const lu32* opres = (const lu32*)(img + L.off_opres);
-    const bool ch = d.obs_enc == ZS_ENC_CHANNELS;
-    const int C = ch ? 3 : 1;
-    const int16_t* hrow = d.obst_hp + (size_t)e * d.O;
-    uint32_t sc[NOBS][PER];
-    int32_t hv[NOBS][PER];
-    // static words of the window cells (out-of-bounds cells read cell 0, discarded below)
-#pragma unroll
-    for (int a = 0; a < NOBS; a++) {
-        const int32_t ap = pos[a];
-        const int ox = unpack_x(ap) - WW / 2, oy = unpack_y(ap) - WW / 2;
-#pragma unroll
-        for (int i = 0; i < PER; i++) {
-            const int cc = min(lane + 64 * i, PLANE - 1), r = cc / WW, q = cc - r * WW;
-            const int x = ox + q, y = oy + r;
-            const bool inb = (unsigned)x < (unsigned)W && (unsigned)y < (unsigned)H;
-            sc[a][i] = (uint32_t)d.scell[inb ? y * W + x : 0];
-        }
-    }
-    // HP of the window cells' obstacles (cells without one read obstacle 0, discarded below); a clean
-    // chunk's HP from the shared hp_init row
-    const uint32_t dirty = hpd;
-#pragma unroll
-    for (int a = 0; a < NOBS; a++)
-#pragma unroll
-        for (int i = 0; i < PER; i++) {
-            const int oi = (int)(sc[a][i] & SC_OBST_MASK) - 1;
-            const int o = oi > 0 ? oi : 0;
-            hv[a][i] = (((dirty >> (o / d.hp_chunk)) & 1u) ? hrow : d.hp_init)[o];
-        }
-    // the store stream: LDS and registers only
-#pragma unroll 1
-    for (int a = 0; a < NOBS; a++) {
-        const int32_t ap = pos[a];
-        const int ox = unpack_x(ap) - WW / 2, oy = unpack_y(ap) - WW / 2;
-        const lu8* wm = img + a * PLANE;
-        T* o = out + ((size_t)e * NOBS + a) * C * PLANE;
-#pragma unroll
-        for (int i = 0; i < PER; i++) {
-            const int cell = lane + 64 * i;
-            const int cc = cell < PLANE ? cell : PLANE - 1, r = cc / WW, q = cc - r * WW;
-            const int x = ox + q, y = oy + r;
-            const bool inb = (unsigned)x < (unsigned)W && (unsigned)y < (unsigned)H;
-            const int c = inb ? y * W + x : 0;
-            const uint32_t bit = 1u << (c & 31);
-            const int sb = wm[cc];
-            const int v = cw[sb ? sb - 1 : 0], elife = life[sb ? sb - 1 : 0];
-            const uint32_t s = sc[a][i];
-            const int oi = (int)(s & SC_OBST_MASK) - 1;
-            const bool obp = oi >= 0 && ((opres[(oi > 0 ? oi : 0) >> 5] >> (oi & 31)) & 1u);
-            int code = (dead[c >> 5] & bit) ? ZS_THING_DEADBODY : (s & SC_OBJ_BIT) ? ZS_THING_OBJECTIVE : ZS_THING_NONE;
-            code = obp ? (int)((s >> SC_KIND_SHIFT) & 7u) : code;
-            code = sb ? (v & 255) : code;
-            code = inb ? code : ZS_THING_WALL;
-            int lf = sb ? elife : (obp ? hv[a][i] : 0);
-            lf = inb ? lf : 200;
-            const int weapon = (inb && sb) ? ((v >> 8) & 255) : 0;
-            if (STAGED) {
-                ZS_LDS T* ot = (ZS_LDS T*)(slot + ((uintptr_t)o & 15));
-                if (cell < PLANE) {
-                    ot[cell] = (T)code;
-                    ot[PLANE + cell] = (T)lf;
-                    ot[2 * PLANE + cell] = (T)weapon;
-                }
-            } else if (cell < PLANE) {
-                obs_store(o, PLANE, cell, ch, code, lf, weapon);
-            }
-        }
-        if (STAGED) {
-            wave_sync();
-            obs_block_flush(slot, o, lane);
-            wave_sync();
-        }
-    }
-}
-
 // ---------------------------------------------------------------------------
 // k_obs_lds: k_obs_pipe's persistent walk and register prefetch, but each observation block
 // (3 x 441 values, channels encoding) is first computed into a wave-private LDS slot, laid out at
@@ -744,6 +609,139 @@ __device__ __forceinline__ void obs_stage_flush(const lu8* slot, T* o, int lane)
     const int nhead = mis ? (16 - mis) / TS : 0, tail0 = (16 * kend - mis) / TS, ntail = (nb - 16 * kend) / TS;
     const int idx = lane < nhead ? lane : (lane >= 32 && lane - 32 < ntail) ? tail0 + lane - 32 : -1;
     zs_buf_store<T>(r, idx >= 0 ? (uint32_t)(idx * TS) : ZS_OOB, (T)sv[(idx >= 0 ? idx : 0) + shift]);
+}
+
+// ---------------------------------------------------------------------------
+// k_obs_gather: the registered shape (surroundings, width 21, NOBS observations per env) on maps
+// whose obstacle HP row is too large to stage per env (city128: 3689 obstacles, 14.7 KB, which
+// left k_obs one wave per CU slot).  Only the observed cells' data is fetched: per lane, the
+// static per-cell words of its NOBS x 7 window cells, then the HP of those cells' obstacles, each
+// batch issued as one group of loads before any store (one wait per batch, no global load inside
+// the store loop).  The wave image holds the window maps, entities, dead-body and obstacle-present
+// bits only (~5 KB at city128), so four waves per workgroup and many workgroups per CU hide the two
+// load round trips.
+// ---------------------------------------------------------------------------
+// STAGED: channels blocks go through an LDS slot per wave (in obs_stage_t, at the destination's 16-B
+// phase) and out as throttled 16-B buffer stores (obs_stage_flush, as k_obs_lds).
+// stat (uniform): the map's static tables (obs_stage_static4, 16 * DW bytes at the start of the
+// workgroup's LDS) give each window cell's static word (obstacle rank, kind, objective bit) by LDS
+// reads, so the HP loads follow the env's first load round directly (two dependent load rounds
+// instead of three).
+template <typename T, int NOBS, bool STAGED>
+__global__ void __launch_bounds__(256) k_obs_gather(Dev d, T* out, const uint8_t* mask, ObsLayout L, int stat) {
+    extern __shared__ __align__(16) uint8_t smem[];
+    constexpr int WW = 21, PLANE = WW * WW, PER = (PLANE + 63) / 64;
+    typedef typename obs_stage<T>::type S;
+    constexpr int TS = (int)sizeof(T), SLOT = STAGED ? obs_stage_slot_bytes(TS) : 0;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int e = xcd_remap(blockIdx.x, gridDim.x) * 4 + wave;
+    const bool act = e < d.N && !(mask && !mask[e]);
+    if (!stat && !act) return;
+    const lv4u* st4 = (const lv4u*)smem;
+    lu8* img = (lu8*)(smem + (stat ? 16 * d.DW : 0) + wave * (L.bytes + SLOT));
+    lu8* slot = img + L.bytes;
+    const int N = d.N, W = d.W, H = d.H;
+    if (stat) obs_stage_static4(d, (lv4u*)smem, threadIdx.x, blockDim.x);
+    uint32_t hpd = 0;  // arrives with obs_build's loads, used one load round later
+    if (act) {
+        hpd = d.hp_dirty[e];
+        obs_build(d, L, img, e, [&](int s, int& p, int& lf, int& wp, int& pr) {
+            p = d.pos[(size_t)s * N + e];
+            lf = d.life[(size_t)s * N + e];
+            wp = d.weapon[(size_t)s * N + e];
+            pr = d.present[(size_t)s * N + e];
+        });
+    }
+    if (stat) __syncthreads();
+    if (!act) return;
+    const li32* pos = (const li32*)(img + L.off_pos);
+    const li32* life = (const li32*)(img + L.off_life);
+    const li32* cw = (const li32*)(img + L.off_cw);
+    const lu32* dead = (const lu32*)(img + L.off_dead);
+    const lu32* opres = (const lu32*)(img + L.off_opres);
+    const bool ch = d.obs_enc == ZS_ENC_CHANNELS;
+    const int C = ch ? 3 : 1;
+    const int16_t* hrow = d.obst_hp + (size_t)e * d.O;
+    uint32_t sc[NOBS][PER];
+    int32_t hv[NOBS][PER];
+    // static words of the window cells (out-of-bounds cells read cell 0, discarded below)
+#pragma unroll
+    for (int a = 0; a < NOBS; a++) {
+        const int32_t ap = pos[a];
+        const int ox = unpack_x(ap) - WW / 2, oy = unpack_y(ap) - WW / 2;
+#pragma unroll
+        for (int i = 0; i < PER; i++) {
+            const int cc = min(lane + 64 * i, PLANE - 1), r = cc / WW, q = cc - r * WW;
+            const int x = ox + q, y = oy + r;
+            const bool inb = (unsigned)x < (unsigned)W && (unsigned)y < (unsigned)H;
+            const int c = inb ? y * W + x : 0;
+            if (stat) {  // the scell word (engine.hip) from the static tables
+                const uint32_t bit = 1u << (c & 31);
+                const zs_v4u sw = st4[c >> 5];
+                const uint32_t ob = (sw.x & bit) ? (sw.w + __popc(sw.x & (bit - 1u)) + 1u) |
+                                                       ((uint32_t)((sw.y & bit) ? ZS_THING_BOX : ZS_THING_WALL) << SC_KIND_SHIFT)
+                                                 : 0u;
+                sc[a][i] = ob | ((sw.z & bit) ? SC_OBJ_BIT : 0u);
+            } else {
+                sc[a][i] = (uint32_t)d.scell[c];
+            }
+        }
+    }
+    // HP of the window cells' obstacles (cells without one read obstacle 0, discarded below); a clean
+    // chunk's HP from the shared hp_init row
+    const uint32_t dirty = hpd;
+#pragma unroll
+    for (int a = 0; a < NOBS; a++)
+#pragma unroll
+        for (int i = 0; i < PER; i++) {
+            const int oi = (int)(sc[a][i] & SC_OBST_MASK) - 1;
+            const int o = oi > 0 ? oi : 0;
+            hv[a][i] = (((dirty >> (o / d.hp_chunk)) & 1u) ? hrow : d.hp_init)[o];
+        }
+    // the store stream: LDS and registers only
+#pragma unroll 1
+    for (int a = 0; a < NOBS; a++) {
+        const int32_t ap = pos[a];
+        const int ox = unpack_x(ap) - WW / 2, oy = unpack_y(ap) - WW / 2;
+        const lu8* wm = img + a * PLANE;
+        T* o = out + ((size_t)e * NOBS + a) * C * PLANE;
+#pragma unroll
+        for (int i = 0; i < PER; i++) {
+            const int cell = lane + 64 * i;
+            const int cc = cell < PLANE ? cell : PLANE - 1, r = cc / WW, q = cc - r * WW;
+            const int x = ox + q, y = oy + r;
+            const bool inb = (unsigned)x < (unsigned)W && (unsigned)y < (unsigned)H;
+            const int c = inb ? y * W + x : 0;
+            const uint32_t bit = 1u << (c & 31);
+            const int sb = wm[cc];
+            const int v = cw[sb ? sb - 1 : 0], elife = life[sb ? sb - 1 : 0];
+            const uint32_t s = sc[a][i];
+            const int oi = (int)(s & SC_OBST_MASK) - 1;
+            const bool obp = oi >= 0 && ((opres[(oi > 0 ? oi : 0) >> 5] >> (oi & 31)) & 1u);
+            int code = (dead[c >> 5] & bit) ? ZS_THING_DEADBODY : (s & SC_OBJ_BIT) ? ZS_THING_OBJECTIVE : ZS_THING_NONE;
+            code = obp ? (int)((s >> SC_KIND_SHIFT) & 7u) : code;
+            code = sb ? (v & 255) : code;
+            code = inb ? code : ZS_THING_WALL;
+            int lf = sb ? elife : (obp ? hv[a][i] : 0);
+            lf = inb ? lf : 200;
+            const int weapon = (inb && sb) ? ((v >> 8) & 255) : 0;
+            if (STAGED) {
+                ZS_LDS S* ot = (ZS_LDS S*)slot + (int)((uintptr_t)o & 15) / TS;
+                if (cell < PLANE) {
+                    ot[cell] = (S)code;
+                    ot[PLANE + cell] = (S)lf;
+                    ot[2 * PLANE + cell] = (S)weapon;
+                }
+            } else if (cell < PLANE) {
+                obs_store(o, PLANE, cell, ch, code, lf, weapon);
+            }
+        }
+        if (STAGED) {
+            wave_sync();
+            obs_stage_flush<T>(slot, o, lane);
+            wave_sync();
+        }
+    }
 }
 
 template <typename T, int NOBS>

@@ -132,6 +132,7 @@ PATHS = {
     "obs_k_obs": {"ZS_FOBS": "0", "ZS_OBS_PIPE": "0", "ZS_OBS_GATHER": "0"},  # one-env-per-wave k_obs
     "obs_gather": {"ZS_FOBS": "0", "ZS_OBS_PIPE": "0"},  # window-only fetches (k_obs_gather)
     "obs_gather_lds": {"ZS_FOBS": "0", "ZS_OBS_PIPE": "0", "ZS_OBS_GATHER_LDS": "1"},  # ... with 16-B stores
+    "obs_gather_scell": {"ZS_FOBS": "0", "ZS_OBS_PIPE": "0", "ZS_OBS_GATHER_STAT": "0"},  # ... global static words
     "obs_pipe_cells": {"ZS_OBS_LDS": "0"},          # k_obs_pipe's per-cell stores instead of k_obs_lds
     "obs_lds": {"ZS_OBS_LDS": "1"},                 # k_obs_lds at any env count
     "obs_ring": {"ZS_OBS_LDS": "1", "ZS_OBS_RING": "1"},  # encoder / writer waves through an LDS ring
@@ -218,10 +219,13 @@ def test_store_stream_every_phase(monkeypatch):
                64, 60, n_discrete=6, check_state_every=30)
 
 
+@pytest.mark.parametrize("stat", ["0", "1"])
 @pytest.mark.parametrize("staged", ["0", "1"])
-def test_city128_gather_paths(staged, monkeypatch):
-    """C4's observation kernel (k_obs_gather), per-cell stores and LDS-staged 16-B stores."""
+def test_city128_gather_paths(staged, stat, monkeypatch):
+    """C4's observation kernel (k_obs_gather), per-cell stores and LDS-staged 16-B stores; static
+    words from the LDS tables (default) or one global load per window cell."""
     monkeypatch.setenv("ZS_OBS_GATHER_LDS", staged)
+    monkeypatch.setenv("ZS_OBS_GATHER_STAT", stat)
     run_parity(lambda n: _abi.multi_env_config(n, "safehouse", [], "city128", ["0", "1", "2", "3"],
                                                initial_zombies=50, minimum_zombies=50),
                24, 30, check_state_every=15)
