@@ -262,6 +262,19 @@ def main():
             eng.step()
         torch.cuda.synchronize()
     prof = eng.profile_read()
+    # the mix of the timed window: episodes ending per step (each is an autoreset at the next step,
+    # on the reset side stream), sampled over a few untimed steps that continue the same trajectories
+    mix_steps = 20
+    eng.profile(False)
+    ends = torch.zeros(2, dtype=torch.int64, device=eng.device)
+    for _ in range(mix_steps):
+        step += 1
+        eng.gen_actions(step, 7)
+        eng.step()
+        ends[0] += eng.done.sum()
+        ends[1] += eng.trunc.sum()
+    torch.cuda.synchronize()
+    ends = ends.tolist()
     if distributed:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -316,7 +329,10 @@ def main():
                    "minimum_zombies": args.min_zombies, "obs_dtype": args.obs_dtype,
                    "parallelism": "env-sharded x%d (%s)" % (
                        world, "RCCL all-gather of obs + rewards/done per step" if gather
-                       else "no data-path collective"), "launch": launch},
+                       else "no data-path collective"), "launch": launch,
+                   "episode_ends_per_step": {"done": ends[0] / mix_steps, "truncated": ends[1] / mix_steps,
+                                             "fraction_of_envs": ends[0] / mix_steps / n_local,
+                                             "sample": "%d untimed steps after the timed window, rank 0" % mix_steps}},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
                      "algorithmic_bytes_per_step": dom_b * n_local,
