@@ -272,6 +272,7 @@ struct zs_handle {
     int obs_gather = 0;    // else k_obs_gather<NOBS> usable (NOBS = 1, 2, 4), else 0 (k_obs)
     int obs_gather_staged = 0;  // k_obs_gather through LDS-staged 16-B stores
     int obs_gather_stat = 0;    // k_obs_gather reads the static words from LDS tables (ZS_OBS_GATHER_STAT)
+    int resp_overlap = 0;       // k_respawn + its envs' observations on s_obs beside the others' (ZS_RESPAWN_OVERLAP)
     ObsLayout obs_gl;      // its per-wave image
     // zs_step_graph: one captured hipGraph per autoreset-list parity (the step alternates the two
     // pending-reset lists), replayed on the caller's stream; keyed by the caller's buffers
@@ -810,6 +811,17 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
             if (h->chunks > 1 && hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) != hipSuccess) h->chunks = 1;
         }
     }
+    // deferred respawns: k_respawn and the observations of its envs on s_obs, beside the observations
+    // of every other env on the caller's stream (the tick marks the deferred envs).  Off unless
+    // ZS_RESPAWN_OVERLAP=1: measured at C4 (2 runs each) 0.409 -> 0.491 ms per step, the two
+    // observation launches and k_respawn contend for the same CUs and the list launch is N / 4 workgroups
+    const char* ro = getenv("ZS_RESPAWN_OVERLAP");
+    if (d.defer_respawn && h->obs_gather && !d.fobs && h->chunks == 1 && ro && atoi(ro) != 0) {
+        h->resp_overlap = hipStreamCreateWithFlags(&h->s_obs, hipStreamNonBlocking) == hipSuccess &&
+                          hipEventCreateWithFlags(&h->ev_chunk[0], hipEventDisableTiming) == hipSuccess &&
+                          hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) == hipSuccess;
+        if (h->resp_overlap) TRY(dalloc(h, &d.resp_mark, (size_t)N));
+    }
     h->memset_nodes = getenv("ZS_GRAPH_MEMSET") && atoi(getenv("ZS_GRAPH_MEMSET")) != 0;
     // side-stream reset work (unfused steps; ZS_RESET_STREAM=0 keeps it on the caller's stream)
     if (!h->fused && !getenv_off("ZS_RESET_STREAM")) {
@@ -889,7 +901,8 @@ extern "C" int zs_seed(zs_handle* h, int32_t env0, int32_t n, const uint64_t* se
     return ZS_OK;
 }
 
-static int launch_obs(zs_handle* h, void* obs, const uint8_t* mask, hipStream_t s, int env0 = 0, int env1 = -1) {
+static int launch_obs(zs_handle* h, void* obs, const uint8_t* mask, hipStream_t s, int env0 = 0, int env1 = -1,
+                      int lmode = 0) {
     const Dev& d = h->d;
     if (!obs) return ZS_OK;
     int i0 = -1, i1 = -1;
@@ -961,9 +974,9 @@ static int launch_obs(zs_handle* h, void* obs, const uint8_t* mask, hipStream_t 
 #define ZS_GATH(TT, NB)                                                                                              \
     do {                                                                                                             \
         if (h->obs_gather_staged)                                                                                    \
-            hipLaunchKernelGGL((k_obs_gather<TT, NB, true>), dim3(g), dim3(256), lds, s, d, (TT*)obs, mask, h->obs_gl, h->obs_gather_stat); \
+            hipLaunchKernelGGL((k_obs_gather<TT, NB, true>), dim3(g), dim3(256), lds, s, d, (TT*)obs, mask, h->obs_gl, h->obs_gather_stat, lmode); \
         else                                                                                                         \
-            hipLaunchKernelGGL((k_obs_gather<TT, NB, false>), dim3(g), dim3(256), lds, s, d, (TT*)obs, mask, h->obs_gl, h->obs_gather_stat); \
+            hipLaunchKernelGGL((k_obs_gather<TT, NB, false>), dim3(g), dim3(256), lds, s, d, (TT*)obs, mask, h->obs_gl, h->obs_gather_stat, lmode); \
     } while (0)
 #define ZS_GATH_T(TT)                         \
     if (h->obs_gather == 1) ZS_GATH(TT, 1);     \
@@ -1184,6 +1197,22 @@ extern "C" int zs_step(zs_handle* h, const int32_t* actions_dev, void* obs_dev, 
                      h->d_rcount + q, obs_dev, s);
     if (rc) return rc;
     h->rpar = q;
+    if (h->d.defer_respawn && h->resp_overlap && obs_dev && !h->d.fobs) {
+        // fork: k_respawn and then the observations of its envs on s_obs; the observations of every
+        // unmarked env on s after the reset join; join.  Marks are written by this step's tick only.
+        HIPCHK(hipEventRecord(h->ev_chunk[0], s));
+        HIPCHK(hipStreamWaitEvent(h->s_obs, h->ev_chunk[0], 0));
+        rc = launch_respawn(h, h->s_obs);
+        if (rc) return rc;
+        rc = launch_obs(h, obs_dev, nullptr, h->s_obs, 0, -1, 2);
+        if (rc) return rc;
+        HIPCHK(hipEventRecord(h->ev_join, h->s_obs));
+        if (side) HIPCHK(hipStreamWaitEvent(s, h->ev_rjoin, 0));
+        rc = launch_obs(h, obs_dev, nullptr, s, 0, -1, 1);
+        if (rc) return rc;
+        HIPCHK(hipStreamWaitEvent(s, h->ev_join, 0));
+        return ZS_OK;
+    }
     if (h->d.defer_respawn) {
         rc = launch_respawn(h, s);
         if (rc) return rc;

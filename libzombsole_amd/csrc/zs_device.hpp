@@ -140,6 +140,7 @@ struct Dev {
     int32_t* cand;
     int* resp_list;   // envs whose respawn the tick deferred to k_respawn [N]
     int* resp_count;
+    uint8_t* resp_mark;  // [N] 1: the tick deferred this env's respawn this step (overlapped observations), or null
 };
 
 __device__ __forceinline__ int32_t pack_xy(int x, int y) { return (int32_t)((uint32_t)(x & 0xffff) | ((uint32_t)y << 16)); }

@@ -627,15 +627,23 @@ __device__ __forceinline__ void obs_stage_flush(const lu8* slot, T* o, int lane)
 // workgroup's LDS) give each window cell's static word (obstacle rank, kind, objective bit) by LDS
 // reads, so the HP loads follow the env's first load round directly (two dependent load rounds
 // instead of three).
+// lmode (uniform): 0 every env (of mask); 1 every env the tick did not mark for k_respawn
+// (d.resp_mark); 2 the envs of d.resp_list (after k_respawn, beside a lmode-1 launch).
 template <typename T, int NOBS, bool STAGED>
-__global__ void __launch_bounds__(256) k_obs_gather(Dev d, T* out, const uint8_t* mask, ObsLayout L, int stat) {
+__global__ void __launch_bounds__(256) k_obs_gather(Dev d, T* out, const uint8_t* mask, ObsLayout L, int stat, int lmode) {
     extern __shared__ __align__(16) uint8_t smem[];
     constexpr int WW = 21, PLANE = WW * WW, PER = (PLANE + 63) / 64;
     typedef typename obs_stage<T>::type S;
     constexpr int TS = (int)sizeof(T), SLOT = STAGED ? obs_stage_slot_bytes(TS) : 0;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int e = xcd_remap(blockIdx.x, gridDim.x) * 4 + wave;
-    const bool act = e < d.N && !(mask && !mask[e]);
+    const int idx0 = xcd_remap(blockIdx.x, gridDim.x) * 4;
+    int e = idx0 + wave;
+    if (lmode == 2) {
+        const int n = min(*d.resp_count, d.N);
+        if (idx0 >= n) return;  // the whole workgroup past the list
+        e = e < n ? d.resp_list[e] : d.N;
+    }
+    const bool act = e < d.N && !(mask && !mask[e]) && !(lmode == 1 && d.resp_mark[e]);
     if (!stat && !act) return;
     const lv4u* st4 = (const lv4u*)smem;
     lu8* img = (lu8*)(smem + (stat ? 16 * d.DW : 0) + wave * (L.bytes + SLOT));

@@ -1252,6 +1252,7 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
         if (listed_out)
             for (int a = 0; a < A; a++) listed_out[(size_t)e * A + a] = 1;
         if (reset_out) reset_out[e] = 1;
+        if (d.resp_mark) d.resp_mark[e] = 0;
         d.scal[S_NEEDRESET * N + e] = 0;
         lst[g] = 1u << 11;  // no MT refill for this env here
     }
@@ -1285,6 +1286,7 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
             const int k = atomicAdd(d.resp_count, 1);
             if ((unsigned)k < (unsigned)N) d.resp_list[k] = e;
         }
+        if (d.resp_mark) d.resp_mark[e] = c.respawn ? 1 : 0;
         if (reset_out) reset_out[e] = 0;
         MISC(c, MISC_T) = c.t;
         MISC(c, MISC_DEATHS) = c.deaths;

@@ -165,6 +165,7 @@ RESPAWN = {
     "leader": {"ZS_DEFER_RESPAWN": "0"},
     "deferred": {"ZS_DEFER_RESPAWN": "1"},
     "deferred_fused": {"ZS_DEFER_RESPAWN": "1", "ZS_FUSED": "1"},
+    "deferred_overlap": {"ZS_DEFER_RESPAWN": "1", "ZS_RESPAWN_OVERLAP": "1"},  # respawned envs' obs on a side stream
     "deferred_unfused_serial_reset": {"ZS_DEFER_RESPAWN": "1", "ZS_FUSED": "0", "ZS_RESET_STREAM": "0"},
 }
 
@@ -193,6 +194,7 @@ GRAPH = {
     "default": {},
     "unfused_side_stream": {"ZS_FUSED": "0"},
     "unfused_serial": {"ZS_FUSED": "0", "ZS_RESET_STREAM": "0"},
+    "respawn_overlap": {"ZS_RESPAWN_OVERLAP": "1"},
 }
 
 
