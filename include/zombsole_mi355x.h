@@ -109,6 +109,16 @@ extern "C" {
 #define ZS_DTYPE_I16 2 /* compact internal form; values fit int16 */
 
 #define ZS_FLAG_AUTORESET 1u /* next-step autoreset: an env that ended is reset by the next zs_step */
+#define ZS_FLAG_DEBUG 2u     /* debug=True envs (core.py:96-99, 115-119): action kind ZS_ACT_RAISE
+                              * stops World.step; without the flag kinds >= 7 are unknown (idle) */
+
+/* ---- range flags (zs_overflow) -------------------------------------------
+ * The reference's obstacle life is an unbounded Python int that carries over resets
+ * (game.py:151-155) and keeps falling each time a destroyed Box/Wall is hit again before
+ * the first cleanup of an episode (core.py:72-78, 168-184).  The engine holds it in int32. */
+#define ZS_OVF_INT16 1u /* an obstacle life went below -32768: ZS_DTYPE_I16 observations saturate it */
+#define ZS_OVF_INT32 2u /* an obstacle life reached -2147483647 and saturated there: from then on
+                         * that env differs from the reference */
 
 /* ---- map description (parsed by the host; zombsole/game.py:45-97) ------- */
 typedef struct zs_map_desc {
@@ -213,6 +223,11 @@ int zs_set_state(zs_handle* h, int32_t env, const int32_t* buf_host, void* strea
 int zs_get_rng(zs_handle* h, int32_t env, uint32_t* state_host, void* stream);
 int zs_set_rng(zs_handle* h, int32_t env, const uint32_t* state_host, void* stream);
 
+/* Sticky ZS_OVF_* flags of the handle (everything queued on `stream` included), OR-ed over all
+ * envs since zs_create or the last call with clear != 0.  Lossless results need
+ * !(flags & ZS_OVF_INT32), and !(flags & ZS_OVF_INT16) for ZS_DTYPE_I16 observations. */
+int zs_overflow(zs_handle* h, uint32_t* flags_host, int32_t clear, void* stream);
+
 /* Diagnostics (not part of the reference surface): when enabled, every k_tick
  * (the step kernel), k_obs (the observation kernel) and k_reset (world rebuild)
  * launch is bracketed by HIP events on its stream.  zs_profile_read synchronizes
@@ -239,8 +254,9 @@ int zs_debug_stamps(zs_handle* h, uint64_t* sum_out, uint64_t* max_out, int32_t 
  *   [5]  needs_reset          [6] n_entities (E)    [7] n_obstacles (O)
  *   [8]  width                [9] height            [10] reward prev zombie_deaths
  *   [11] n_zombies_present    [12] spawn serial counter [13..15] reserved
- *   zs_set_state restores every field except [5] (pending resets stay the engine's) and the
- *   read-only [6..9], [11]
+ *   zs_set_state restores every field except the read-only [6..9], [11]; [5] must equal the
+ *   engine's own flag for that env (pending resets are the engine's work lists), else ZS_EINVAL;
+ *   an obstacle life below -2147483647 is refused (ZS_EINVAL)
  *   [16 .. 16+8E)  entity records: kind, present, x, y, life, weapon, extra, spawn_serial
  *                  (slots: agents [0,A), bots [A,A+P), zombies [A+P,E))
  *   [.. +E)        order: entity slot ids in dict order (first n_order valid)

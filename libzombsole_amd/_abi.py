@@ -27,6 +27,8 @@ OBS_WORLD, OBS_SURROUNDINGS = 0, 1
 ENC_SIMPLE, ENC_CHANNELS = 0, 1
 DTYPE_I32, DTYPE_I64, DTYPE_I16 = 0, 1, 2
 FLAG_AUTORESET = 1
+FLAG_DEBUG = 2
+OVF_INT16, OVF_INT32 = 1, 2  # zs_overflow range flags
 STATE_HEADER, STATE_ENTITY_WORDS = 16, 8
 
 DTYPE_NP = {DTYPE_I32: np.int32, DTYPE_I64: np.int64, DTYPE_I16: np.int16}
@@ -138,7 +140,7 @@ class ConfigBuilder(object):
 
     def __init__(self, num_envs, map_, rules, agent_weapons, agent_codes, bot_types, initial_zombies,
                  minimum_zombies, reward_mode, obs_scope, obs_encoding, obs_width, obs_dtype,
-                 max_episode_steps=0, autoreset=True, lanes_per_env=0):
+                 max_episode_steps=0, autoreset=True, lanes_per_env=0, debug=False):
         m = map_ if isinstance(map_, Map) else load_map(map_)
         self.map = m
 
@@ -162,7 +164,8 @@ class ConfigBuilder(object):
         self.cfg = zs_config(int(num_envs), md, int(rules), len(self._aw), p32(self._aw), p32(self._ac),
                              len(self._bt), p32(self._bt), int(initial_zombies), int(minimum_zombies),
                              int(reward_mode), int(obs_scope), int(obs_encoding), int(obs_width),
-                             int(obs_dtype), int(max_episode_steps), FLAG_AUTORESET if autoreset else 0,
+                             int(obs_dtype), int(max_episode_steps),
+                             (FLAG_AUTORESET if autoreset else 0) | (FLAG_DEBUG if debug else 0),
                              int(lanes_per_env))
 
     @property
@@ -191,7 +194,7 @@ class ConfigBuilder(object):
 def single_env_config(num_envs, rules_name, player_names, map_name, agent_id, initial_zombies=0,
                       minimum_zombies=0, observation_scope="world", observation_position_encoding="simple",
                       agent_weapon="rifle", max_episode_steps=0, obs_dtype=DTYPE_I32, autoreset=True,
-                      lanes_per_env=0):
+                      lanes_per_env=0, debug=False):
     """zs_config for the ZombsoleGymEnv surface (gym_env.py:49-83): one agent + bots."""
     m = load_map(map_name)
     rules = rules_id(rules_name)
@@ -201,13 +204,13 @@ def single_env_config(num_envs, rules_name, player_names, map_name, agent_id, in
     enc = parse_encoding(observation_position_encoding)
     return ConfigBuilder(num_envs, m, rules, weapons, [agent_code(agent_id)], bots, initial_zombies,
                          minimum_zombies, REWARD_SINGLE, scope, enc, width, obs_dtype, max_episode_steps,
-                         autoreset, lanes_per_env)
+                         autoreset, lanes_per_env, debug)
 
 
 def multi_env_config(num_envs, rules_name, player_names, map_name, agent_ids, initial_zombies=0,
                      minimum_zombies=0, observation_surroundings_width=21,
                      observation_position_encoding_style="channels", agent_weapons="rifle",
-                     max_episode_steps=0, obs_dtype=DTYPE_I64, autoreset=True, lanes_per_env=0):
+                     max_episode_steps=0, obs_dtype=DTYPE_I64, autoreset=True, lanes_per_env=0, debug=False):
     """zs_config for the MultiagentZombsoleEnv surface (gym/multiagent_env.py:25-78)."""
     w = int(observation_surroundings_width)
     if (w % 2 == 0) or (w <= 1):
@@ -221,4 +224,4 @@ def multi_env_config(num_envs, rules_name, player_names, map_name, agent_ids, in
     weapons = [weapon_id(n) for n in names]
     return ConfigBuilder(num_envs, m, rules, weapons, [agent_code(a) for a in ids], bots, initial_zombies,
                          minimum_zombies, REWARD_MULTI, OBS_SURROUNDINGS, enc, w, obs_dtype,
-                         max_episode_steps, autoreset, lanes_per_env)
+                         max_episode_steps, autoreset, lanes_per_env, debug)

@@ -178,18 +178,22 @@ __global__ void k_get_state(Dev d, int e, int32_t* buf) {
     for (int w = 0; w < d.DW; w++) *r++ = (int32_t)d.dead[(size_t)e * d.DW + w];
 }
 
-__global__ void k_set_state(Dev d, int e, const int32_t* buf) {
+__global__ void k_set_state(Dev d, int e, const int32_t* buf, int* err) {
     if (threadIdx.x != 0) return;
     const int N = d.N, E = d.E;
     const int32_t* b = buf;
+    // needs_reset (b[5]) is the engine's own: pending resets are its work lists (an env on a list with
+    // the flag cleared would be reset and ticked by one call, one off the lists with the flag set would
+    // report a reset without a rebuild), so a record that disagrees is refused, nothing written
+    if (b[5] != d.scal[S_NEEDRESET * N + e]) {
+        *err = ZS_EINVAL;
+        return;
+    }
     d.scal[S_T * N + e] = b[0];
     d.scal[S_DEATHS * N + e] = b[1];
     d.scal[S_ZD * N + e] = b[2];
     d.scal[S_EPSTEPS * N + e] = b[3];
     d.scal[S_NORDER * N + e] = b[4];
-    // b[5] (needs_reset) is not restored: pending resets are the engine's own work lists (an env on
-    // the list with the flag cleared would be reset and ticked by the same call, one off it with the
-    // flag set would report a reset without a rebuild)
     d.scal[S_PREVZD * N + e] = b[10];
     d.scal[S_SERIAL * N + e] = b[12];
     const int32_t* r = b + ZS_STATE_HEADER;
@@ -204,7 +208,7 @@ __global__ void k_set_state(Dev d, int e, const int32_t* buf) {
     int any_nonpos = 0;
     for (int o = 0; o < d.O; o++) {
         int v = *r++;
-        d.obst_hp[(size_t)e * d.O + o] = (int16_t)v;
+        d.obst_hp[(size_t)e * d.O + o] = hp_store_value(d, v);
         d.hp_dirty[e] = 0xffffffffu;
         uint32_t* w = &d.obst_nonpos[(size_t)e * d.OW + (o >> 5)];
         *w = v <= 0 ? (*w | (1u << (o & 31))) : (*w & ~(1u << (o & 31)));
@@ -264,15 +268,12 @@ struct zs_handle {
     ObsLayout obs_l;  // k_obs per-wave LDS image
     int obs_wpg;      // k_obs waves (envs) per workgroup
     int obs_pipe = 0;      // k_obs_pipe<NOBS> usable (NOBS = 1, 2, 4), else 0
-    int obs_walk = 0;      // k_obs_lds env walk (zs_obs.hpp): 0 strided, 1 one region per XCD (ZS_OBS_WALK)
     int obs_lds = 0;       // k_obs_pipe's walk with LDS-staged 16-B stores (k_obs_lds), channels encoding
     int obs_ring = 0;      // k_obs_ring: encoder and writer waves through an LDS ring (ZS_OBS_RING)
     size_t obs_ring_bytes = 0;
     size_t obs_lds_bytes = 0;
     int obs_gather = 0;    // else k_obs_gather<NOBS> usable (NOBS = 1, 2, 4), else 0 (k_obs)
-    int obs_gather_staged = 0;  // k_obs_gather through LDS-staged 16-B stores
     int obs_gather_stat = 0;    // k_obs_gather reads the static words from LDS tables (ZS_OBS_GATHER_STAT)
-    int resp_overlap = 0;       // k_respawn + its envs' observations on s_obs beside the others' (ZS_RESPAWN_OVERLAP)
     ObsLayout obs_gl;      // its per-wave image
     // zs_step_graph: one captured hipGraph per autoreset-list parity (the step alternates the two
     // pending-reset lists), replayed on the caller's stream; keyed by the caller's buffers
@@ -281,14 +282,7 @@ struct zs_handle {
     uint64_t* d_gstep = nullptr;  // [0] policy step counter (k_gen_actions_dev reads, the step launch advances)
     int capturing = 0;            // zs_step is being captured by zs_step_graph
     int forked = 0;               // zs_step_graph recorded ev_rfork itself (before its policy launch)
-    int memset_nodes = 0;         // ZS_GRAPH_MEMSET=1: list counters zeroed by hipMemsetAsync (diagnostic)
-    // step pipeline: the tick in `chunks` env ranges on the caller's stream, each range's observations
-    // on s_obs as soon as its tick is done
-    int chunks = 1;
-    hipStream_t s_obs = nullptr;
-    hipEvent_t ev_chunk[8] = {};
-    hipEvent_t ev_join = nullptr;
-    int obs_pipe_wgs = 8;  // its workgroups per CU
+    int obs_pipe_wgs = 8;  // k_obs_pipe / k_obs_lds workgroups per CU
     // next-step reset work on a side stream, concurrent with the tick (the two touch disjoint envs);
     // the caller's stream joins it before the observations
     int reset_side = 0;
@@ -348,15 +342,6 @@ static int dupload(zs_handle* h, T** p, const std::vector<T>& v) {
 static void free_all(zs_handle* h) {
     for (void* p : h->allocs) (void)hipFree(p);
     h->allocs.clear();
-    for (hipEvent_t& ev : h->ev_chunk)
-        if (ev) {
-            (void)hipEventDestroy(ev);
-            ev = nullptr;
-        }
-    if (h->ev_join) (void)hipEventDestroy(h->ev_join);
-    h->ev_join = nullptr;
-    if (h->s_obs) (void)hipStreamDestroy(h->s_obs);
-    h->s_obs = nullptr;
     if (h->ev_rfork) (void)hipEventDestroy(h->ev_rfork);
     if (h->ev_rjoin) (void)hipEventDestroy(h->ev_rjoin);
     h->ev_rfork = h->ev_rjoin = nullptr;
@@ -634,10 +619,11 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
     TRY(dalloc(h, &d.listed, (size_t)d.A * N));
     TRY(dalloc(h, &d.obst_hp, (size_t)d.O * N));
     TRY(dalloc(h, &d.hp_dirty, N));
+    TRY(dalloc(h, &d.ovf, 1));
     {
-        std::vector<int16_t> init(std::max(d.O, 1), 0);
-        for (int i = 0; i < d.O; i++) init[i] = (int16_t)(okind[i] == ZS_THING_BOX ? 10 : 200);  // Box / Wall MAX_LIFE
-        int16_t* p_init;
+        std::vector<int32_t> init(std::max(d.O, 1), 0);
+        for (int i = 0; i < d.O; i++) init[i] = okind[i] == ZS_THING_BOX ? 10 : 200;  // Box / Wall MAX_LIFE
+        int32_t* p_init;
         TRY(dupload(h, &p_init, init));
         d.hp_init = p_init;
         d.hp_chunk = std::max(1, (d.O + 31) / 32);
@@ -707,7 +693,6 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
         // up to 4 per CU.  It pays when every wave walks several envs (C3 65536 envs; at 8192, one env
         // per wave, k_obs_pipe's per-cell stores measured 33 vs 36 us).  ZS_OBS_LDS=0/1 forces either,
         // ZS_OBS_WGS sets the workgroups per CU.
-        if (getenv("ZS_OBS_WALK")) h->obs_walk = atoi(getenv("ZS_OBS_WALK"));
         if (h->obs_pipe && d.obs_enc == ZS_ENC_CHANNELS && !getenv_off("ZS_OBS_LDS")) {
             const int ts = d.obs_dtype == ZS_DTYPE_I64 ? 8 : d.obs_dtype == ZS_DTYPE_I32 ? 4 : 2;
             const size_t lb = (size_t)d.obs_stat * 4 + 4 * ((size_t)L.bytes + (size_t)obs_stage_slot_bytes(ts));
@@ -751,15 +736,9 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
             if (4 * G.bytes <= 64 * 1024) {
                 h->obs_gather = nobs;
                 h->obs_gl = G;
-                // channels blocks through LDS and out as 16-B stores: off by default, measured even at
-                // C4 (217 vs 218 us: this kernel waits on its two load rounds, not on store issue)
-                const int ts = d.obs_dtype == ZS_DTYPE_I64 ? 8 : d.obs_dtype == ZS_DTYPE_I32 ? 4 : 2;
-                const char* gl = getenv("ZS_OBS_GATHER_LDS");
-                h->obs_gather_staged = d.obs_enc == ZS_ENC_CHANNELS && (gl ? atoi(gl) != 0 : false) &&
-                                       4 * (G.bytes + obs_stage_slot_bytes(ts)) + (d.obs_stat ? 16 * d.DW : 0) <= 64 * 1024;
                 // static words from the LDS tables (rank order, as obs_stat) instead of a global load
                 // round per window cell
-                const size_t gb = 4 * ((size_t)G.bytes + (h->obs_gather_staged ? obs_stage_slot_bytes(ts) : 0));
+                const size_t gb = 4 * (size_t)G.bytes;
                 h->obs_gather_stat = d.obs_stat && gb + 16 * (size_t)d.DW <= 64 * 1024 && !getenv_off("ZS_OBS_GATHER_STAT");
             }
         }
@@ -795,34 +774,6 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
         delete h;
         return fail(ZS_EINVAL, "map too large for the reset kernel's LDS image");
     }
-    // step pipeline over env chunks (zs_step): ZS_CHUNKS=K (2..8) runs the tick in K env ranges and
-    // streams each range's observations on a second stream.  Off by default: measured at 65536 envs,
-    // the persistent observation kernel holds every CU slot, so the overlapping ticks only contend
-    // (K=1 0.586 ms, K=2 0.628, K=4 0.637, K=8 0.697 per step).
-    {
-        const char* ck = getenv("ZS_CHUNKS");
-        h->chunks = 1;
-        if (ck && !h->fused && !d.fobs && h->obs_pipe && !d.defer_respawn) h->chunks = std::max(1, std::min(8, atoi(ck)));
-        if (d.N < 64 * h->chunks) h->chunks = 1;
-        if (h->chunks > 1) {
-            if (hipStreamCreateWithFlags(&h->s_obs, hipStreamNonBlocking) != hipSuccess) h->chunks = 1;
-            for (int c = 0; c < h->chunks && h->chunks > 1; c++)
-                if (hipEventCreateWithFlags(&h->ev_chunk[c], hipEventDisableTiming) != hipSuccess) h->chunks = 1;
-            if (h->chunks > 1 && hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) != hipSuccess) h->chunks = 1;
-        }
-    }
-    // deferred respawns: k_respawn and the observations of its envs on s_obs, beside the observations
-    // of every other env on the caller's stream (the tick marks the deferred envs).  Off unless
-    // ZS_RESPAWN_OVERLAP=1: measured at C4 (2 runs each) 0.409 -> 0.491 ms per step, the two
-    // observation launches and k_respawn contend for the same CUs and the list launch is N / 4 workgroups
-    const char* ro = getenv("ZS_RESPAWN_OVERLAP");
-    if (d.defer_respawn && h->obs_gather && !d.fobs && h->chunks == 1 && ro && atoi(ro) != 0) {
-        h->resp_overlap = hipStreamCreateWithFlags(&h->s_obs, hipStreamNonBlocking) == hipSuccess &&
-                          hipEventCreateWithFlags(&h->ev_chunk[0], hipEventDisableTiming) == hipSuccess &&
-                          hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) == hipSuccess;
-        if (h->resp_overlap) TRY(dalloc(h, &d.resp_mark, (size_t)N));
-    }
-    h->memset_nodes = getenv("ZS_GRAPH_MEMSET") && atoi(getenv("ZS_GRAPH_MEMSET")) != 0;
     // side-stream reset work (unfused steps; ZS_RESET_STREAM=0 keeps it on the caller's stream)
     if (!h->fused && !getenv_off("ZS_RESET_STREAM")) {
         h->reset_side = hipStreamCreateWithFlags(&h->s_reset, hipStreamNonBlocking) == hipSuccess &&
@@ -840,9 +791,9 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
     }
     if (getenv("ZS_VERBOSE"))
         fprintf(stderr, "zs_create: N=%d E=%d G=%d step_lds=%zu resident=%d reset_lds=%zu rw_cap=%d cand_cap=%d "
-                        "lists_cap=%d fused=%d fobs=%d obs_img=%d k_obs_img=%d x%d pipe=%d gather=%d pipe_wgs=%d chunks=%d reset_side=%d defer_respawn=%d\n",
+                        "lists_cap=%d fused=%d fobs=%d obs_img=%d k_obs_img=%d x%d pipe=%d gather=%d pipe_wgs=%d reset_side=%d defer_respawn=%d\n",
                 d.N, d.E, h->G, h->lds, h->resident, h->reset_lds, d.rw_cap, d.cand_cap, d.lists_cap, h->fused,
-                d.fobs, d.obsl.bytes, h->obs_l.bytes, h->obs_wpg, h->obs_pipe, h->obs_gather, h->obs_pipe_wgs, h->chunks,
+                d.fobs, d.obsl.bytes, h->obs_l.bytes, h->obs_wpg, h->obs_pipe, h->obs_gather, h->obs_pipe_wgs,
                 h->reset_side, d.defer_respawn);
     if (d.O > 0) {
         size_t n = N * d.O;
@@ -901,8 +852,7 @@ extern "C" int zs_seed(zs_handle* h, int32_t env0, int32_t n, const uint64_t* se
     return ZS_OK;
 }
 
-static int launch_obs(zs_handle* h, void* obs, const uint8_t* mask, hipStream_t s, int env0 = 0, int env1 = -1,
-                      int lmode = 0) {
+static int launch_obs(zs_handle* h, void* obs, const uint8_t* mask, hipStream_t s, int env0 = 0, int env1 = -1) {
     const Dev& d = h->d;
     if (!obs) return ZS_OK;
     int i0 = -1, i1 = -1;
@@ -941,8 +891,7 @@ static int launch_obs(zs_handle* h, void* obs, const uint8_t* mask, hipStream_t 
 #define ZS_PIPE(TT, NB)                                                                                                 \
     do {                                                                                                                \
         if (h->obs_lds)                                                                                                 \
-            hipLaunchKernelGGL((k_obs_lds<TT, NB>), dim3(g), dim3(256), lds, s, d, (TT*)obs, h->obs_l, env0, env1,     \
-                               (g % 8) == 0 ? h->obs_walk : 0);                                                 \
+            hipLaunchKernelGGL((k_obs_lds<TT, NB>), dim3(g), dim3(256), lds, s, d, (TT*)obs, h->obs_l, env0, env1);   \
         else                                                                                                            \
             hipLaunchKernelGGL((k_obs_pipe<TT, NB>), dim3(g), dim3(256), lds, s, d, (TT*)obs, h->obs_l, env0, env1);   \
     } while (0)
@@ -968,16 +917,9 @@ static int launch_obs(zs_handle* h, void* obs, const uint8_t* mask, hipStream_t 
     }
     if (h->obs_gather) {  // one env per wave, four per workgroup, window-only fetches
         const unsigned g = (unsigned)((d.N + 3) / 4);
-        const int ts = d.obs_dtype == ZS_DTYPE_I64 ? 8 : d.obs_dtype == ZS_DTYPE_I32 ? 4 : 2;
-        const size_t lds = 4 * ((size_t)h->obs_gl.bytes + (h->obs_gather_staged ? obs_stage_slot_bytes(ts) : 0)) +
-                           (h->obs_gather_stat ? 16 * (size_t)d.DW : 0);
-#define ZS_GATH(TT, NB)                                                                                              \
-    do {                                                                                                             \
-        if (h->obs_gather_staged)                                                                                    \
-            hipLaunchKernelGGL((k_obs_gather<TT, NB, true>), dim3(g), dim3(256), lds, s, d, (TT*)obs, mask, h->obs_gl, h->obs_gather_stat, lmode); \
-        else                                                                                                         \
-            hipLaunchKernelGGL((k_obs_gather<TT, NB, false>), dim3(g), dim3(256), lds, s, d, (TT*)obs, mask, h->obs_gl, h->obs_gather_stat, lmode); \
-    } while (0)
+        const size_t lds = 4 * (size_t)h->obs_gl.bytes + (h->obs_gather_stat ? 16 * (size_t)d.DW : 0);
+#define ZS_GATH(TT, NB) \
+    hipLaunchKernelGGL((k_obs_gather<TT, NB>), dim3(g), dim3(256), lds, s, d, (TT*)obs, mask, h->obs_gl, h->obs_gather_stat)
 #define ZS_GATH_T(TT)                         \
     if (h->obs_gather == 1) ZS_GATH(TT, 1);     \
     else if (h->obs_gather == 2) ZS_GATH(TT, 2); \
@@ -1151,68 +1093,26 @@ extern "C" int zs_step(zs_handle* h, const int32_t* actions_dev, void* obs_dev, 
         if (rc) return rc;
         if (side) HIPCHK(hipEventRecord(h->ev_rjoin, h->s_reset));
     }
-    // 2) tick every other env; envs that end now are queued on list[q] for the next call
-    // The work-list counters this call appends to are zeroed by k_zero2, which inside zs_step_graph's
-    // graph also advances the policy step.  Captured 4-byte hipMemsetAsync nodes (ZS_GRAPH_MEMSET=1,
-    // diagnostic) wrote byte patterns instead of zero into these counters, constant per instantiated
-    // graph (0x01010101 / 0x05050505 / 0xC0C0C0C0: profiles/r02_graph_memset_city128.log, from
-    // tools/debug/graph_memset.py); the pending-reset list indexed by such a count was the round-1
-    // replay fault.  Standalone graphs of the same node shapes zero correctly
-    // (profiles/r02_graphprobe_memset.log).  Every list index is bounds-checked in the kernels.
-    if (h->memset_nodes) {
-        HIPCHK(hipMemsetAsync(h->d_rcount + q, 0, sizeof(int), s));
-        if (h->d.defer_respawn) HIPCHK(hipMemsetAsync(h->d.resp_count, 0, sizeof(int), s));
-    } else if (!h->capturing) {
+    // 2) tick every other env; envs that end now are queued on list[q] for the next call.
+    // The work-list counters this call appends to are zeroed by k_zero2 (eager steps) or, inside
+    // zs_step_graph's graph, by the policy kernel ahead of the step.  Not by captured 4-byte
+    // hipMemsetAsync nodes: in this engine's city128 graph such nodes left byte patterns
+    // (0x01010101 / 0x05050505 / 0xC0C0C0C0) in the counters (profiles/r02_graph_memset_city128.log,
+    // round 1's replay fault; tools/probe/graphprobe.hip reproduces the node sequence standalone).
+    // Every list index is bounds-checked in the kernels.
+    if (!h->capturing) {
         hipLaunchKernelGGL(k_zero2, dim3(1), dim3(64), 0, s, h->d_rcount + q, h->d.defer_respawn ? h->d.resp_count : nullptr);
+        HIPCHK(hipGetLastError());
     }
-    HIPCHK(hipGetLastError());
     struct GstepScope {  // the step launch advances the graph's policy counter while capturing
         Dev& d;
         GstepScope(Dev& dd, uint64_t* g) : d(dd) { d.gstep_adv = g; }
         ~GstepScope() { d.gstep_adv = nullptr; }
     } gscope(h->d, h->capturing ? h->d_gstep : nullptr);
-    const int K = (!h->fused && !h->d.fobs && obs_dev) ? h->chunks : 1;
-    if (K > 1) {
-        if (side) HIPCHK(hipStreamWaitEvent(s, h->ev_rjoin, 0));
-        // 3) pipelined: the tick of chunk c + 1 (caller's stream) runs while the observations of chunk
-        //    c stream out on the engine's second stream; the caller's stream joins at the end
-        const int N = h->d.N;
-        for (int c = 0; c < K; c++) {
-            const int c0 = (int)((long)N * c / K) & ~63, c1 = c + 1 == K ? N : (int)((long)N * (c + 1) / K) & ~63;
-            rc = launch_tick(h, actions_dev, rewards_dev, done_dev, trunc_dev, listed_dev, reset_dev, h->d_rlist[q],
-                             h->d_rcount + q, nullptr, s, c0, c1);
-            if (rc) return rc;
-            h->d.gstep_adv = nullptr;  // advanced once per step
-            HIPCHK(hipEventRecord(h->ev_chunk[c], s));
-            HIPCHK(hipStreamWaitEvent(h->s_obs, h->ev_chunk[c], 0));
-            rc = launch_obs(h, obs_dev, nullptr, h->s_obs, c0, c1);
-            if (rc) return rc;
-        }
-        HIPCHK(hipEventRecord(h->ev_join, h->s_obs));
-        HIPCHK(hipStreamWaitEvent(s, h->ev_join, 0));
-        h->rpar = q;
-        return ZS_OK;
-    }
     rc = launch_tick(h, actions_dev, rewards_dev, done_dev, trunc_dev, listed_dev, reset_dev, h->d_rlist[q],
                      h->d_rcount + q, obs_dev, s);
     if (rc) return rc;
     h->rpar = q;
-    if (h->d.defer_respawn && h->resp_overlap && obs_dev && !h->d.fobs) {
-        // fork: k_respawn and then the observations of its envs on s_obs; the observations of every
-        // unmarked env on s after the reset join; join.  Marks are written by this step's tick only.
-        HIPCHK(hipEventRecord(h->ev_chunk[0], s));
-        HIPCHK(hipStreamWaitEvent(h->s_obs, h->ev_chunk[0], 0));
-        rc = launch_respawn(h, h->s_obs);
-        if (rc) return rc;
-        rc = launch_obs(h, obs_dev, nullptr, h->s_obs, 0, -1, 2);
-        if (rc) return rc;
-        HIPCHK(hipEventRecord(h->ev_join, h->s_obs));
-        if (side) HIPCHK(hipStreamWaitEvent(s, h->ev_rjoin, 0));
-        rc = launch_obs(h, obs_dev, nullptr, s, 0, -1, 1);
-        if (rc) return rc;
-        HIPCHK(hipStreamWaitEvent(s, h->ev_join, 0));
-        return ZS_OK;
-    }
     if (h->d.defer_respawn) {
         rc = launch_respawn(h, s);
         if (rc) return rc;
@@ -1286,10 +1186,9 @@ extern "C" int zs_step_graph(zs_handle* h, uint64_t step0, int32_t n_discrete, i
                 }
                 h->forked = 1;
             }
-            const bool zero = !h->memset_nodes;  // the step's work-list counters (k_zero2 in eager steps)
+            // the policy kernel also zeroes the step's work-list counters (k_zero2 in eager steps)
             hipLaunchKernelGGL(k_gen_actions_dev, dim3((n + 255) / 256), dim3(256), 0, cs, h->d, h->d_gstep, n_discrete,
-                               actions_dev, zero ? h->d_rcount + (1 - h->rpar) : nullptr,
-                               zero && h->d.defer_respawn ? h->d.resp_count : nullptr);
+                               actions_dev, h->d_rcount + (1 - h->rpar), h->d.defer_respawn ? h->d.resp_count : nullptr);
             rc = zs_step(h, actions_dev, obs_dev, rewards_dev, done_dev, trunc_dev, listed_dev, reset_dev, cs);
             h->forked = 0;
             hipError_t ce = hipStreamEndCapture(cs, &graph);
@@ -1341,18 +1240,33 @@ extern "C" int zs_get_state(zs_handle* h, int32_t env, int32_t* buf_host, void* 
 extern "C" int zs_set_state(zs_handle* h, int32_t env, const int32_t* buf_host, void* stream) {
     if (!h || !buf_host) return fail(ZS_EINVAL, "null argument");
     if (env < 0 || env >= h->d.N) return fail(ZS_EINVAL, "env index out of range");
-    {  // obstacle HP is kept as int16 in HBM (every reachable value fits: MAX_LIFE 200 down to the damage of
-       // one tick below zero); refuse a poke outside that range instead of wrapping it
+    {  // obstacle life is int32 in HBM; INT32_MIN is the observation kernels' absent mark (ZS_HP_FLOOR)
         const int32_t* hp = buf_host + ZS_STATE_HEADER + ZS_STATE_ENTITY_WORDS * h->d.E + h->d.E;
         for (int o = 0; o < h->d.O; o++)
-            if (hp[o] < -32768 || hp[o] > 32767) return fail(ZS_EINVAL, "obstacle life outside the int16 range");
+            if (hp[o] < ZS_HP_FLOOR) return fail(ZS_EINVAL, "obstacle life below -2147483647");
     }
     hipStream_t s = (hipStream_t)stream;
     HIPCHK(hipSetDevice(h->device));
+    HIPCHK(hipMemsetAsync(h->d_err, 0, sizeof(int), s));
     HIPCHK(hipMemcpyAsync(h->d_state, buf_host, sizeof(int32_t) * h->state_words, hipMemcpyHostToDevice, s));
-    hipLaunchKernelGGL(k_set_state, dim3(1), dim3(64), 0, s, h->d, env, h->d_state);
+    hipLaunchKernelGGL(k_set_state, dim3(1), dim3(64), 0, s, h->d, env, h->d_state, h->d_err);
     HIPCHK(hipGetLastError());
+    int err = 0;
+    HIPCHK(hipMemcpyAsync(&err, h->d_err, sizeof(int), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
+    if (err) return fail(ZS_EINVAL, "state record's needs_reset [5] differs from the engine's (pending resets are not settable)");
+    return ZS_OK;
+}
+
+extern "C" int zs_overflow(zs_handle* h, uint32_t* flags_host, int32_t clear, void* stream) {
+    if (!h || !flags_host) return fail(ZS_EINVAL, "null argument");
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(hipSetDevice(h->device));
+    uint32_t f = 0;
+    HIPCHK(hipMemcpyAsync(&f, h->d.ovf, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    if (clear) HIPCHK(hipMemsetAsync(h->d.ovf, 0, sizeof(uint32_t), s));
+    HIPCHK(hipStreamSynchronize(s));
+    *flags_host = f;
     return ZS_OK;
 }
 
@@ -1453,9 +1367,9 @@ extern "C" int zs_describe(zs_handle* h, char* buf, int32_t len) {
     snprintf(buf, (size_t)len,
              "{\"envs\": %d, \"entities\": %d, \"lanes_per_env\": %d, \"step_kernel\": \"%s\", \"step_lds\": %zu, "
              "\"step_wgs_per_cu\": %d, \"rng_window\": %d, \"obs_kernel\": \"%s\", \"reset_side_stream\": %d, "
-             "\"reset_lds\": %zu, \"respawn\": \"%s\", \"chunks\": %d}",
+             "\"reset_lds\": %zu, \"respawn\": \"%s\"}",
              d.N, d.E, h->G, h->fused ? "k_step" : "k_tick", h->lds, h->resident, d.rw_cap, obs_kernel, h->reset_side,
-             h->reset_lds, d.defer_respawn ? "k_respawn" : "tick", h->chunks);
+             h->reset_lds, d.defer_respawn ? "k_respawn" : "tick");
     return ZS_OK;
 }
 

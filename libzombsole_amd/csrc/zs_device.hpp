@@ -115,12 +115,17 @@ struct Dev {
     int32_t* scal;
     int32_t* prev_life;
     uint8_t* listed;
-    int16_t* obst_hp;  // [N][O]; int16: MAX_LIFE 200 down to one tick's damage below 0 (half the obs kernels' reads)
+    // [N][O] int32.  The reference's obstacle life is an unbounded Python int on map objects that are
+    // re-spawned at every reset with the life they had (game.py:151-155) and can be hit again before
+    // the first cleanup (core.py:72-78,168-184), so it falls without a floor across episodes.  int32
+    // holds it exactly down to ZS_HP_FLOOR (> 9 M episodes of maximal damage to one obstacle); below
+    // that the tick saturates it and raises ZS_OVF_INT32 in *ovf (zs_overflow).
+    int32_t* obst_hp;
     // [N]: bit k set once an obstacle of chunk k (obstacles k * hp_chunk .. + hp_chunk - 1) may have left
     // its MAX_LIFE (set_target_life, zs_set_state); a clean chunk's HP is hp_init's, so the observation
     // kernels read it from that shared static row (cache-resident) instead of the env's row in HBM
     uint32_t* hp_dirty;
-    const int16_t* hp_init;  // [O] Box / Wall MAX_LIFE
+    const int32_t* hp_init;  // [O] Box / Wall MAX_LIFE
     int hp_chunk;            // ceil(O / 32)
     // [N]: bit k set once a dead-body word of chunk k (words k * dead_chunk .. + dead_chunk - 1) may be
     // non-zero (tick cleanup, zs_set_state; k_reset clears it with the row): the prefetching observation
@@ -140,8 +145,29 @@ struct Dev {
     int32_t* cand;
     int* resp_list;   // envs whose respawn the tick deferred to k_respawn [N]
     int* resp_count;
-    uint8_t* resp_mark;  // [N] 1: the tick deferred this env's respawn this step (overlapped observations), or null
+    // sticky range flags of the handle (zs_overflow): ZS_OVF_INT16 once an obstacle's life went below
+    // the int16 range (int16 observations then saturate it), ZS_OVF_INT32 once one saturated at
+    // ZS_HP_FLOOR (the engine then differs from the reference's unbounded int)
+    uint32_t* ovf;
 };
+
+// lowest obstacle life the engine holds exactly; INT32_MIN itself marks an absent obstacle in the
+// observation kernels' compact images (ZS_HP_ABSENT, zs_obs.hpp)
+#define ZS_HP_FLOOR (-2147483647)
+
+// an obstacle life about to be stored: saturated at ZS_HP_FLOOR (64-bit arithmetic, no wrap), range
+// flags raised (rare path: one global atomic)
+__device__ __forceinline__ int32_t hp_store_value(const Dev& d, int64_t v) {
+    if (v < -32768) {
+        uint32_t f = ZS_OVF_INT16;
+        if (v < (int64_t)ZS_HP_FLOOR) {
+            v = ZS_HP_FLOOR;
+            f |= ZS_OVF_INT32;
+        }
+        atomicOr(d.ovf, f);
+    }
+    return (int32_t)v;
+}
 
 __device__ __forceinline__ int32_t pack_xy(int x, int y) { return (int32_t)((uint32_t)(x & 0xffff) | ((uint32_t)y << 16)); }
 __device__ __forceinline__ int unpack_x(int32_t p) { return (int)(int16_t)(p & 0xffff); }

@@ -48,16 +48,30 @@ __device__ __forceinline__ int floordiv100_i32(int a) {  // Python a // 100
     return q;
 }
 
+// A value into an observation element of type T.  Every value fits int32; only an obstacle's
+// carried-over life (and the simple code of such a cell) can leave the int16 range, and the int16
+// form saturates it (the tick raised ZS_OVF_INT16 when the life got there: zs_overflow).
+template <typename T>
+__device__ __forceinline__ T obs_val(int64_t v) {
+    if constexpr (sizeof(T) == 2) return (T)(v < -32768 ? -32768 : (v > 32767 ? 32767 : v));
+    return (T)v;
+}
+template <typename T>
+__device__ __forceinline__ T obs_val(int v) {
+    if constexpr (sizeof(T) == 2) return (T)max(-32768, min(v, 32767));  // v_med3_i32
+    return (T)v;
+}
+
 template <typename T>
 __device__ __forceinline__ void obs_store(T* o, int plane, int cell, bool ch, int code, int life, int weapon) {
     if (!ch) {
         const int adj = life < 100 ? life : 100;
         // 15 * adj // 100 (Python floor division); 32-bit fast path for every reachable life
         const int64_t f = adj >= -(1 << 26) ? (int64_t)floordiv100_i32(15 * adj) : floordiv100(15 * (int64_t)adj);
-        o[cell] = (T)(256 * (int64_t)code + 16 * (int64_t)weapon + f);
+        o[cell] = obs_val<T>(256 * (int64_t)code + 16 * (int64_t)weapon + f);
     } else {
         o[cell] = (T)code;
-        o[plane + cell] = (T)life;
+        o[plane + cell] = obs_val<T>(life);
         o[2 * plane + cell] = (T)weapon;
     }
 }
@@ -422,7 +436,7 @@ __device__ __forceinline__ void obs_prefetch(const Dev& d, int e, int ahead, zs_
         f.dead[i] = (((dirty.y >> (w / d.dead_chunk)) & 1u) ? dr : d.dead_zero)[w];
     }
     f.opres = d.obst_present[(size_t)ed * d.OW + min(lane, d.OW - 1)];
-    const int16_t* hr = d.obst_hp + (size_t)eh * d.O;
+    const int32_t* hr = d.obst_hp + (size_t)eh * d.O;
 #pragma unroll
     for (int i = 0; i < OBS_PF_H; i++) {
         const int o = min(lane + 64 * i, d.O - 1);
@@ -621,33 +635,20 @@ __device__ __forceinline__ void obs_stage_flush(const lu8* slot, T* o, int lane)
 // bits only (~5 KB at city128), so four waves per workgroup and many workgroups per CU hide the two
 // load round trips.
 // ---------------------------------------------------------------------------
-// STAGED: channels blocks go through an LDS slot per wave (in obs_stage_t, at the destination's 16-B
-// phase) and out as throttled 16-B buffer stores (obs_stage_flush, as k_obs_lds).
 // stat (uniform): the map's static tables (obs_stage_static4, 16 * DW bytes at the start of the
 // workgroup's LDS) give each window cell's static word (obstacle rank, kind, objective bit) by LDS
 // reads, so the HP loads follow the env's first load round directly (two dependent load rounds
 // instead of three).
-// lmode (uniform): 0 every env (of mask); 1 every env the tick did not mark for k_respawn
-// (d.resp_mark); 2 the envs of d.resp_list (after k_respawn, beside a lmode-1 launch).
-template <typename T, int NOBS, bool STAGED>
-__global__ void __launch_bounds__(256) k_obs_gather(Dev d, T* out, const uint8_t* mask, ObsLayout L, int stat, int lmode) {
+template <typename T, int NOBS>
+__global__ void __launch_bounds__(256) k_obs_gather(Dev d, T* out, const uint8_t* mask, ObsLayout L, int stat) {
     extern __shared__ __align__(16) uint8_t smem[];
     constexpr int WW = 21, PLANE = WW * WW, PER = (PLANE + 63) / 64;
-    typedef typename obs_stage<T>::type S;
-    constexpr int TS = (int)sizeof(T), SLOT = STAGED ? obs_stage_slot_bytes(TS) : 0;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int idx0 = xcd_remap(blockIdx.x, gridDim.x) * 4;
-    int e = idx0 + wave;
-    if (lmode == 2) {
-        const int n = min(*d.resp_count, d.N);
-        if (idx0 >= n) return;  // the whole workgroup past the list
-        e = e < n ? d.resp_list[e] : d.N;
-    }
-    const bool act = e < d.N && !(mask && !mask[e]) && !(lmode == 1 && d.resp_mark[e]);
+    const int e = xcd_remap(blockIdx.x, gridDim.x) * 4 + wave;
+    const bool act = e < d.N && !(mask && !mask[e]);
     if (!stat && !act) return;
     const lv4u* st4 = (const lv4u*)smem;
-    lu8* img = (lu8*)(smem + (stat ? 16 * d.DW : 0) + wave * (L.bytes + SLOT));
-    lu8* slot = img + L.bytes;
+    lu8* img = (lu8*)(smem + (stat ? 16 * d.DW : 0) + wave * L.bytes);
     const int N = d.N, W = d.W, H = d.H;
     if (stat) obs_stage_static4(d, (lv4u*)smem, threadIdx.x, blockDim.x);
     uint32_t hpd = 0;  // arrives with obs_build's loads, used one load round later
@@ -669,7 +670,7 @@ __global__ void __launch_bounds__(256) k_obs_gather(Dev d, T* out, const uint8_t
     const lu32* opres = (const lu32*)(img + L.off_opres);
     const bool ch = d.obs_enc == ZS_ENC_CHANNELS;
     const int C = ch ? 3 : 1;
-    const int16_t* hrow = d.obst_hp + (size_t)e * d.O;
+    const int32_t* hrow = d.obst_hp + (size_t)e * d.O;
     uint32_t sc[NOBS][PER];
     int32_t hv[NOBS][PER];
     // static words of the window cells (out-of-bounds cells read cell 0, discarded below)
@@ -733,27 +734,13 @@ __global__ void __launch_bounds__(256) k_obs_gather(Dev d, T* out, const uint8_t
             int lf = sb ? elife : (obp ? hv[a][i] : 0);
             lf = inb ? lf : 200;
             const int weapon = (inb && sb) ? ((v >> 8) & 255) : 0;
-            if (STAGED) {
-                ZS_LDS S* ot = (ZS_LDS S*)slot + (int)((uintptr_t)o & 15) / TS;
-                if (cell < PLANE) {
-                    ot[cell] = (S)code;
-                    ot[PLANE + cell] = (S)lf;
-                    ot[2 * PLANE + cell] = (S)weapon;
-                }
-            } else if (cell < PLANE) {
-                obs_store(o, PLANE, cell, ch, code, lf, weapon);
-            }
-        }
-        if (STAGED) {
-            wave_sync();
-            obs_stage_flush<T>(slot, o, lane);
-            wave_sync();
+            if (cell < PLANE) obs_store(o, PLANE, cell, ch, code, lf, weapon);
         }
     }
 }
 
 template <typename T, int NOBS>
-__global__ void __launch_bounds__(256, ZS_OBS_PIPE_WAVES) k_obs_lds(Dev d, T* out, ObsLayout L, int env0, int env1, int walk) {
+__global__ void __launch_bounds__(256, ZS_OBS_PIPE_WAVES) k_obs_lds(Dev d, T* out, ObsLayout L, int env0, int env1) {
     extern __shared__ __align__(16) uint8_t smem[];
     typedef typename obs_stage<T>::type S;
     constexpr int WW = 21, PLANE = WW * WW, PER = (PLANE + 63) / 64, TS = (int)sizeof(T);
@@ -765,21 +752,11 @@ __global__ void __launch_bounds__(256, ZS_OBS_PIPE_WAVES) k_obs_lds(Dev d, T* ou
     lv4u* st4 = (lv4u*)smem;
     obs_stage_static4(d, st4, threadIdx.x, blockDim.x);
     __syncthreads();
-    // walk 0: every wave strides over [env0, env1) by the launch's wave count, XCD-contiguous blocks of
-    // envs per round; walk 1 (grid a multiple of 8): XCD x owns the x-th eighth of the range and its
-    // workgroups walk it, so each XCD's stores stream through one region of the tensor
-    int waves = gridDim.x * 4, e, hi = env1;
-    if (walk == 1) {
-        const int x = blockIdx.x & 7, nj = gridDim.x >> 3, r = (env1 - env0 + 7) >> 3;
-        const int lo = env0 + x * r;
-        hi = min(env1, lo + r);
-        waves = nj * 4;
-        e = lo + (int)(blockIdx.x >> 3) * 4 + wave;
-    } else {
-        e = env0 + xcd_remap(blockIdx.x, gridDim.x) * 4 + wave;
-    }
-    if (e >= hi) return;
-    env1 = hi;
+    // every wave strides over [env0, env1) by the launch's wave count, XCD-contiguous blocks of envs per
+    // round (walking one region of envs per XCD instead measured no faster with the encoding on)
+    const int waves = gridDim.x * 4;
+    int e = env0 + xcd_remap(blockIdx.x, gridDim.x) * 4 + wave;
+    if (e >= env1) return;
     lu8* img = (lu8*)(smem + stat_words * 4 + wave * (L.bytes + SLOT));
     lu8* slot = img + L.bytes;  // 16-B aligned: the static tables, L.bytes and SLOT are multiples of 16
     const li32* pos = (const li32*)(img + L.off_pos);
@@ -809,7 +786,7 @@ __global__ void __launch_bounds__(256, ZS_OBS_PIPE_WAVES) k_obs_lds(Dev d, T* ou
                     obs_cell_lds(d, L, st4, img, wm, cc, ox + q, oy + r, code, lf, weapon);
                     if (cell < PLANE) {
                         ot[cell] = (S)code;
-                        ot[PLANE + cell] = (S)lf;
+                        ot[PLANE + cell] = obs_val<S>(lf);
                         ot[2 * PLANE + cell] = (S)weapon;
                     }
                 }
@@ -974,7 +951,7 @@ __global__ void __launch_bounds__(64 * (RING_ENC + RING_WRT), 1) k_obs_ring(Dev 
                 obs_cell_lds(d, L, st4, img, wm, cc, ox + q2, oy + r, code, lf, weapon);
                 if (cell < PLANE) {
                     ot[cell] = (S)code;
-                    ot[PLANE + cell] = (S)lf;
+                    ot[PLANE + cell] = obs_val<S>(lf);
                     ot[2 * PLANE + cell] = (S)weapon;
                 }
             }

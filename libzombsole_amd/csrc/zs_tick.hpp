@@ -273,13 +273,14 @@ __device__ __forceinline__ int target_life(const Dev& d, const Grp& c, int tgt) 
     if (tgt >= 0) return LL(c, tgt);
     return d.obst_hp[(size_t)c.e * d.O + (-tgt - 1)];
 }
-__device__ __forceinline__ void set_target_life(const Dev& d, Grp& c, int tgt, int v) {
-    if (tgt >= 0) {
-        LL(c, tgt) = v;
+// v = the new life (64-bit: an obstacle's carried-over life minus a hit may leave the int32 range)
+__device__ __forceinline__ void set_target_life(const Dev& d, Grp& c, int tgt, int64_t v) {
+    if (tgt >= 0) {  // Zombie / Player / Agent: 100 at most, one tick of hits below 0 at least
+        LL(c, tgt) = (int)v;
         return;
     }
     int oi = -tgt - 1;
-    d.obst_hp[(size_t)c.e * d.O + oi] = (int16_t)v;
+    d.obst_hp[(size_t)c.e * d.O + oi] = hp_store_value(d, v);
     d.hp_dirty[c.e] |= 1u << (oi / d.hp_chunk);
     uint32_t* w = &d.obst_nonpos[(size_t)c.e * d.OW + (oi >> 5)];
     uint32_t bit = 1u << (oi & 31);
@@ -520,8 +521,8 @@ __device__ __forceinline__ void decide_agent(const Dev& d, const Grp& c, int s, 
         int q = closest_in(d, c, x, y, 0, d.A + d.P, s);
         kind = K_HEAL;
         tgt = q >= 0 ? q : s;
-    } else if (ak == ZS_ACT_RAISE) {
-        kind = K_RAISE;
+    } else if (ak == ZS_ACT_RAISE && (d.flags & ZS_FLAG_DEBUG)) {
+        kind = K_RAISE;  // only a debug env re-raises (core.py:96-99); elsewhere an unknown kind idles
     }
 }
 
@@ -770,14 +771,15 @@ __device__ __forceinline__ void env_step_leader(const Dev& d, Grp& c, const int3
             int w = LW(c, s);
             if (d2(x, y, unpack_x(tp), unpack_y(tp)) <= weapon_r2(w)) {
                 int dmg = rng_int(d, c, weapon_lo(w), weapon_hi(w));
-                set_target_life(d, c, tgt, target_life(d, c, tgt) - dmg);
+                set_target_life(d, c, tgt, (int64_t)target_life(d, c, tgt) - dmg);
             }
         } else {  // thing_heal (core.py:186-202), HEALING_RANGE = 3
             int tp = target_pos(d, c, tgt);
             if (d2(x, y, unpack_x(tp), unpack_y(tp)) <= 9) {
                 int ml = target_maxlife(d, tgt);
                 int hl = rng_int(d, c, ml / 10, ml / 4);
-                set_target_life(d, c, tgt, min(ml, target_life(d, c, tgt) + hl));
+                const int64_t nl = (int64_t)target_life(d, c, tgt) + hl;
+                set_target_life(d, c, tgt, nl < ml ? nl : (int64_t)ml);
             }
         }
     }
@@ -1252,7 +1254,6 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
         if (listed_out)
             for (int a = 0; a < A; a++) listed_out[(size_t)e * A + a] = 1;
         if (reset_out) reset_out[e] = 1;
-        if (d.resp_mark) d.resp_mark[e] = 0;
         d.scal[S_NEEDRESET * N + e] = 0;
         lst[g] = 1u << 11;  // no MT refill for this env here
     }
@@ -1286,7 +1287,6 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
             const int k = atomicAdd(d.resp_count, 1);
             if ((unsigned)k < (unsigned)N) d.resp_list[k] = e;
         }
-        if (d.resp_mark) d.resp_mark[e] = c.respawn ? 1 : 0;
         if (reset_out) reset_out[e] = 0;
         MISC(c, MISC_T) = c.t;
         MISC(c, MISC_DEATHS) = c.deaths;

@@ -13,7 +13,7 @@ from . import _abi
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_build", "libzombsole_mi355x.so")
 SYMBOLS = ["zs_last_error", "zs_create", "zs_destroy", "zs_obs_shape", "zs_seed", "zs_reset", "zs_step", "zs_observe",
-           "zs_gen_actions", "zs_step_graph", "zs_state_size", "zs_get_state", "zs_set_state", "zs_get_rng", "zs_set_rng", "zs_profile", "zs_profile_read", "zs_describe",
+           "zs_gen_actions", "zs_step_graph", "zs_state_size", "zs_get_state", "zs_set_state", "zs_get_rng", "zs_set_rng", "zs_overflow", "zs_profile", "zs_profile_read", "zs_describe",
            "zs_debug_stamps", "zs_debug_lists"]
 
 _lib = None
@@ -53,12 +53,13 @@ def load_library(path=None):
     L.zs_set_state.argtypes = [vp, i32, vp, vp]
     L.zs_get_rng.argtypes = [vp, i32, vp, vp]
     L.zs_set_rng.argtypes = [vp, i32, vp, vp]
+    L.zs_overflow.argtypes = [vp, C.POINTER(C.c_uint32), i32, vp]
     L.zs_profile.argtypes = [vp, i32]
     L.zs_profile_read.argtypes = [vp, C.POINTER(C.c_double)]
     L.zs_debug_stamps.argtypes = [vp, vp, vp, i32]
     L.zs_describe.argtypes = [vp, C.c_char_p, i32]
-    # an older build selected by ZS_ENGINE_LIB for an A/B (tools/ab.sh) may lack newer diagnostics
-    optional = {"zs_debug_lists"} if os.environ.get("ZS_ENGINE_LIB") and path is None else set()
+    # an older build selected by ZS_ENGINE_LIB for an A/B (tools/ab.sh) may lack newer entry points
+    optional = {"zs_debug_lists", "zs_overflow"} if os.environ.get("ZS_ENGINE_LIB") and path is None else set()
     for s in SYMBOLS:
         if s in optional and not hasattr(L, s):
             continue
@@ -238,6 +239,23 @@ class Engine(object):
         if rc:
             _raise(self.L, rc, "zs_set_state")
 
+
+    def overflow(self, clear=False):
+        """Sticky range flags (_abi.OVF_INT16 | OVF_INT32) of every env since creation / the last clear."""
+        f = C.c_uint32(0)
+        rc = self.L.zs_overflow(self.h, C.byref(f), 1 if clear else 0, self._stream())
+        if rc:
+            _raise(self.L, rc, "zs_overflow")
+        return int(f.value)
+
+    def check_lossless(self):
+        """Raise OverflowError when an obstacle life left what this engine's outputs hold exactly: below
+        the int16 range with int16 observations, or saturated at -2**31 + 1."""
+        f = self.overflow()
+        if f & _abi.OVF_INT32:
+            raise OverflowError("an obstacle life fell below -2147483647 and saturated (reference: unbounded int)")
+        if (f & _abi.OVF_INT16) and self.obs_dtype == self.torch.int16:
+            raise OverflowError("an obstacle life fell below -32768: int16 observations saturated it")
 
     def get_rng(self, env):
         """(mt[624] uint32, index) of env's MT19937 stream, CPython getstate() form."""

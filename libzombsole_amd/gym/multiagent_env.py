@@ -60,7 +60,7 @@ class MultiagentZombsoleEnv(object):
                                         observation_surroundings_width=w,
                                         observation_position_encoding_style=observation_position_encoding_style,
                                         agent_weapons=agent_weapons, max_episode_steps=0,
-                                        obs_dtype=_abi.DTYPE_I64, autoreset=False)
+                                        obs_dtype=_abi.DTYPE_I64, autoreset=False, debug=debug)
         names = _abi.expand_weapons(agent_weapons, len(agent_ids))
         self._simple = enc == _abi.ENC_SIMPLE
         self._ids = list(agent_ids)[:len(names)]

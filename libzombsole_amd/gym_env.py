@@ -43,7 +43,7 @@ class ZombsoleGymEnv(Env):
                                          observation_scope=observation_scope,
                                          observation_position_encoding=observation_position_encoding,
                                          agent_weapon=agent_weapon, max_episode_steps=0,
-                                         obs_dtype=_abi.DTYPE_I32, autoreset=False)
+                                         obs_dtype=_abi.DTYPE_I32, autoreset=False, debug=debug)
         cfg = builder.cfg
         # a channels observation encodes 8 + int(agent_id): the reference raises that ValueError
         # whenever it builds an observation (gym/observation.py:59-60), not at construction

@@ -44,6 +44,7 @@ def load(path):
     L.zo_rng_draws.restype = C.c_uint64
     L.zo_rng_draws.argtypes = [C.c_void_p]
     L.zo_poke_life.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int]
+    L.zo_poke_obstacle.argtypes = [C.c_void_p, C.c_int, C.c_int]
     L.zo_run_batch.restype = C.c_int64
     L.zo_run_batch.argtypes = [C.c_void_p, C.c_uint64, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                                C.POINTER(C.c_uint64)]
@@ -141,6 +142,9 @@ class OracleEnv(object):
 
     def poke_life(self, which, i, life):
         return self.L.zo_poke_life(self.h, which, i, life)
+
+    def poke_obstacle(self, i, life):
+        return self.L.zo_poke_obstacle(self.h, i, life)
 
 
 def run_batch(builder, seed0, n_envs, steps, n_discrete, threads=1):

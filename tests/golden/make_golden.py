@@ -53,6 +53,9 @@ SYN = os.path.join(REPO, "libzombsole_amd", "maps")
 def map_arg(name):
     if name in ("bridge64", "city128"):
         return os.path.join(SYN, name + ".txt")
+    test_map = os.path.join(HERE, "maps", name + ".txt")  # test-only maps (absolute path, gym_env.py:55)
+    if os.path.isfile(test_map):
+        return test_map
     return name
 
 
@@ -119,6 +122,16 @@ CONFIGS = [
      dict(rules_name="extermination", player_names=["hamster", "randoman"], map_name="bridge",
           agent_ids=["0", "1", "2"], initial_zombies=10, minimum_zombies=4,
           observation_surroundings_width=11, debug=True), [23, 24], 120, 2, 60),
+    # obstacle life carried over resets without a floor (game.py:151-155, core.py:72-78,168-184): walls
+    # poked near the int16 floor are re-spawned destroyed at every reset and shot again on tick 1 by
+    # rifle agents (two of them on the centre wall when the spawn shuffle puts them either side of it);
+    # no zombies, so Extermination ends every episode after one step
+    ("multi_wallhp_carryover_a2", "multi", "fixed",
+     dict(rules_name="extermination", player_names=[], map_name="wall_hp", agent_ids=["0", "1"],
+          initial_zombies=0, minimum_zombies=0), [25, 26, 27], 80, 4, 0,
+     {"poke_obstacles": [[5, -32700], [6, -32720], [7, -32760]],
+      "actions": [{"action_type": "attack", "parameter": [1, 0]},
+                  {"action_type": "attack", "parameter": [-1, 0]}]}),
 ]
 
 

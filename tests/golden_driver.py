@@ -65,7 +65,11 @@ def obs_bytes_multi(obs, agent_ids):
 
 
 def run_config(cfg, K):
-    name, surface, stream, kw, seeds, calls, full_calls, max_steps = cfg
+    name, surface, stream, kw, seeds, calls, full_calls, max_steps = cfg[:8]
+    # extras: poke_obstacles [[i, life], ...] set on the map's Box/Wall objects before the first reset
+    # (the reference shares them across resets, game.py:151-155); stream "fixed": `actions`, one dict
+    # action per agent, every step
+    extras = cfg[8] if len(cfg) > 8 else {}
     kw = dict(kw)
     kw["map_name"] = K.map_arg(kw["map_name"])
     out = []
@@ -85,6 +89,8 @@ def run_config(cfg, K):
         game = base.game
         obstacles = [t for t in game.map.things if isinstance(t, (K.Box, K.Wall))]
         agent_ids = list(base.possible_agents) if surface == "multi" else [kw["agent_id"]]
+        for i, life in extras.get("poke_obstacles", []):
+            obstacles[i].life = life
         recs = []
         random.seed(seed)
         obs, _ = env.reset()
@@ -106,6 +112,9 @@ def run_config(cfg, K):
                         if stream == "discrete":
                             act = A.discrete_action_id(seed, call, 0, n_act)
                             rec["act"] = int(act)
+                        elif stream == "fixed":
+                            act = dict(extras["actions"][0])
+                            rec["act"] = act
                         else:
                             act = dict_act(seed, call, 0)
                             rec["act"] = act
@@ -115,6 +124,8 @@ def run_config(cfg, K):
                         if stream == "discrete":
                             act = {aid: int(A.discrete_action_id(seed, call, i, n_act))
                                    for i, aid in enumerate(agent_ids)}
+                        elif stream == "fixed":
+                            act = {aid: dict(extras["actions"][i]) for i, aid in enumerate(agent_ids)}
                         else:
                             act = {aid: dict_act(seed, call, i) for i, aid in enumerate(agent_ids)}
                         rec["act"] = [act[a] for a in agent_ids]
@@ -156,5 +167,8 @@ def run_config(cfg, K):
             rec["state"] = canonical_state(game, obstacles, K)
             recs.append(rec)
         out.append({"seed": seed, "calls": recs})
-    return {"name": name, "surface": surface, "stream": stream, "kwargs": dict(cfg[3]),
-            "max_steps": max_steps, "runs": out}
+    res = {"name": name, "surface": surface, "stream": stream, "kwargs": dict(cfg[3]),
+           "max_steps": max_steps, "runs": out}
+    if extras:
+        res["extras"] = extras
+    return res

@@ -30,24 +30,36 @@ def load_fixture(name):
         return json.load(f)
 
 
+def map_path(name):
+    """A fixture's map: the test-only maps of tests/golden/maps by path, else a bundled map name."""
+    p = os.path.join(GOLDEN, "maps", name + ".txt")
+    return p if os.path.isfile(p) else name
+
+
+def obstacle_pokes(fx):
+    """[[obstacle index, life], ...] set on the map's Box/Wall objects before the first reset."""
+    return (fx.get("extras") or {}).get("poke_obstacles", [])
+
+
 def builder_for(fx, num_envs=1, dtype=None):
     kw = dict(fx["kwargs"])
     ms = fx.get("max_steps", 0)
+    debug = bool(kw.get("debug", False))
     if fx["surface"] == "single":
         return _abi.single_env_config(
-            num_envs, kw["rules_name"], kw.get("player_names", []), kw["map_name"], kw["agent_id"],
+            num_envs, kw["rules_name"], kw.get("player_names", []), map_path(kw["map_name"]), kw["agent_id"],
             initial_zombies=kw.get("initial_zombies", 0), minimum_zombies=kw.get("minimum_zombies", 0),
             observation_scope=kw.get("observation_scope", "world"),
             observation_position_encoding=kw.get("observation_position_encoding", "simple"),
             agent_weapon=kw.get("agent_weapon", "rifle"), max_episode_steps=ms,
-            obs_dtype=_abi.DTYPE_I32 if dtype is None else dtype)
+            obs_dtype=_abi.DTYPE_I32 if dtype is None else dtype, debug=debug)
     return _abi.multi_env_config(
-        num_envs, kw["rules_name"], kw.get("player_names", []), kw["map_name"], kw["agent_ids"],
+        num_envs, kw["rules_name"], kw.get("player_names", []), map_path(kw["map_name"]), kw["agent_ids"],
         initial_zombies=kw.get("initial_zombies", 0), minimum_zombies=kw.get("minimum_zombies", 0),
         observation_surroundings_width=kw.get("observation_surroundings_width", 21),
         observation_position_encoding_style=kw.get("observation_position_encoding_style", "channels"),
         agent_weapons=kw.get("agent_weapons", "rifle"), max_episode_steps=ms,
-        obs_dtype=_abi.DTYPE_I64 if dtype is None else dtype)
+        obs_dtype=_abi.DTYPE_I64 if dtype is None else dtype, debug=debug)
 
 
 def action_triples(fx, rec, n_agents):

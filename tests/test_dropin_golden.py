@@ -19,7 +19,7 @@ class K:
 
     @staticmethod
     def map_arg(name):
-        return name
+        return G.map_path(name)
 
 
 def _cfg(fx):
@@ -27,7 +27,7 @@ def _cfg(fx):
     calls = len(runs[0]["calls"])
     full = sum(1 for r in runs[0]["calls"] if "obs" in r)
     return (fx["name"], fx["surface"], fx["stream"], fx["kwargs"], [r["seed"] for r in runs], calls, full,
-            fx["max_steps"])
+            fx["max_steps"], fx.get("extras") or {})
 
 
 # the 32-agent fort fixture is covered through the batched ABI (test_engine_golden)

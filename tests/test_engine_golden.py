@@ -25,6 +25,12 @@ def replay_engine(fx):
     eng = _engine(fx, n)
     kinds = [o[2] for o in eng.builder.map.obstacles]
     eng.seed([r["seed"] for r in runs])
+    pokes = G.obstacle_pokes(fx)
+    for k in range(n if pokes else 0):  # the map's Box/Wall life before the first reset (carried over)
+        st = eng.get_state(k)
+        for i, life in pokes:
+            st.obst_life[i] = life
+        eng.set_state(k, st)
     eng.reset()
     ncalls = len(runs[0]["calls"])
     for i in range(ncalls):

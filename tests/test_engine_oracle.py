@@ -131,7 +131,6 @@ PATHS = {
     "obs_in_step_unfused": {"ZS_FOBS": "1", "ZS_FUSED": "0"},
     "obs_k_obs": {"ZS_FOBS": "0", "ZS_OBS_PIPE": "0", "ZS_OBS_GATHER": "0"},  # one-env-per-wave k_obs
     "obs_gather": {"ZS_FOBS": "0", "ZS_OBS_PIPE": "0"},  # window-only fetches (k_obs_gather)
-    "obs_gather_lds": {"ZS_FOBS": "0", "ZS_OBS_PIPE": "0", "ZS_OBS_GATHER_LDS": "1"},  # ... with 16-B stores
     "obs_gather_scell": {"ZS_FOBS": "0", "ZS_OBS_PIPE": "0", "ZS_OBS_GATHER_STAT": "0"},  # ... global static words
     "obs_pipe_cells": {"ZS_OBS_LDS": "0"},          # k_obs_pipe's per-cell stores instead of k_obs_lds
     "obs_lds": {"ZS_OBS_LDS": "1"},                 # k_obs_lds at any env count
@@ -140,7 +139,6 @@ PATHS = {
     "obs_scan_in_step": {"ZS_OBS_WIN": "0", "ZS_FOBS": "1"},
     "obs_scell": {"ZS_OBS_STAT": "0"},              # per-cell static words instead of LDS bitmaps
     "obs_scell_in_step": {"ZS_OBS_STAT": "0", "ZS_FOBS": "1"},
-    "chunked": {"ZS_CHUNKS": "4", "ZS_FUSED": "0"},  # tick / observation pipeline over 4 env chunks
     "no_lds_budget": {"ZS_LDS_BUDGET": "0"},        # largest LDS copies instead of occupancy-first
 }
 
@@ -149,7 +147,7 @@ PATHS = {
 def test_kernel_paths(path, monkeypatch):
     for k, v in PATHS[path].items():
         monkeypatch.setenv(k, v)
-    run_parity(c2, 256 if path == "chunked" else 96, 60, check_state_every=30)
+    run_parity(c2, 96, 60, check_state_every=30)
     run_parity(lambda n: _abi.single_env_config(n, "safehouse", ["terminator"], "city_for_safehouse", "0",
                                                 initial_zombies=20, minimum_zombies=20,
                                                 observation_scope="world", observation_position_encoding="channels",
@@ -165,7 +163,6 @@ RESPAWN = {
     "leader": {"ZS_DEFER_RESPAWN": "0"},
     "deferred": {"ZS_DEFER_RESPAWN": "1"},
     "deferred_fused": {"ZS_DEFER_RESPAWN": "1", "ZS_FUSED": "1"},
-    "deferred_overlap": {"ZS_DEFER_RESPAWN": "1", "ZS_RESPAWN_OVERLAP": "1"},  # respawned envs' obs on a side stream
     "deferred_unfused_serial_reset": {"ZS_DEFER_RESPAWN": "1", "ZS_FUSED": "0", "ZS_RESET_STREAM": "0"},
 }
 
@@ -194,7 +191,6 @@ GRAPH = {
     "default": {},
     "unfused_side_stream": {"ZS_FUSED": "0"},
     "unfused_serial": {"ZS_FUSED": "0", "ZS_RESET_STREAM": "0"},
-    "respawn_overlap": {"ZS_RESPAWN_OVERLAP": "1"},
 }
 
 
@@ -222,11 +218,9 @@ def test_store_stream_every_phase(monkeypatch):
 
 
 @pytest.mark.parametrize("stat", ["0", "1"])
-@pytest.mark.parametrize("staged", ["0", "1"])
-def test_city128_gather_paths(staged, stat, monkeypatch):
-    """C4's observation kernel (k_obs_gather), per-cell stores and LDS-staged 16-B stores; static
-    words from the LDS tables (default) or one global load per window cell."""
-    monkeypatch.setenv("ZS_OBS_GATHER_LDS", staged)
+def test_city128_gather_paths(stat, monkeypatch):
+    """C4's observation kernel (k_obs_gather): static words from the LDS tables (default) or one
+    global load per window cell."""
     monkeypatch.setenv("ZS_OBS_GATHER_STAT", stat)
     run_parity(lambda n: _abi.multi_env_config(n, "safehouse", [], "city128", ["0", "1", "2", "3"],
                                                initial_zombies=50, minimum_zombies=50),

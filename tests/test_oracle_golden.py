@@ -12,6 +12,8 @@ from oracle.oracle import OracleEnv, OracleRaised
 def replay_oracle(fx, run):
     b = G.builder_for(fx)
     env = OracleEnv(b)
+    for i, life in G.obstacle_pokes(fx):
+        assert env.poke_obstacle(i, life) == 0
     env.seed(run["seed"])
     listed = None
     for i, rec in enumerate(run["calls"]):

@@ -258,6 +258,98 @@ int probe_chain2(hipStream_t s, int replays, int kernel_between, int scribble = 
     return 0;
 }
 
+// The engine's city128 step graph as it was captured with ZS_GRAPH_MEMSET=1 (round 2), node for node:
+// on the capture stream an event record (the reset fork), the policy kernel, then on a side stream
+// (waiting on that event) a one-wave kernel with dynamic LDS (k_reset), its join event; back on the
+// capture stream the two captured 4-byte memsets (the parity's pending-list counter, then the
+// deferred-respawn counter in its own allocation), the step kernel (one-wave workgroups, a by-value
+// argument block of the engine's Dev size, dynamic LDS) appending to both counters, the respawn kernel
+// (appends nothing), the wait on the join, and the observation kernel.  Two graphs (one per list
+// parity) replayed alternately; a correct replay leaves exactly `waves` in both counters.
+template <int NW>
+__global__ void k_step_like(Big<NW> b, int* c1, int* c2, int* rec, int bytes) {
+    extern __shared__ uint32_t lds[];
+    for (int i = threadIdx.x; i < bytes / 4; i += 64) lds[i] = b.w[i % NW] ^ (uint32_t)i;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int v = atomicAdd(c1, 1), w = atomicAdd(c2, 1);
+        atomicMax(&rec[0], v + 1);
+        atomicMax(&rec[1], w + 1);
+    }
+}
+
+template <int NW>
+__global__ void k_other(Big<NW> b, int bytes) {
+    extern __shared__ uint32_t lds[];
+    for (int i = threadIdx.x; i < bytes / 4; i += 64) lds[i] = b.w[i % NW];
+    __syncthreads();
+    if (threadIdx.x == 0 && lds[0] == 0xdeadbeefu) g_out[0] = 1;
+}
+
+int probe_fork(hipStream_t s, int replays, int waves) {
+    constexpr int NW = 180;  // 720 B by value, about the engine's Dev
+    Big<NW> b;
+    for (int i = 0; i < NW; i++) b.w[i] = 0x9e3779b9u * (i + 3);
+    int *cnt, *resp, *rec;
+    CHK(hipMalloc(&cnt, 16));
+    CHK(hipMalloc(&resp, 16));
+    CHK(hipMemset(cnt, 0, 16));
+    CHK(hipMemset(resp, 0, 16));
+    CHK(hipMalloc(&rec, 2 * sizeof(int)));
+    hipStream_t cs, side;
+    CHK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+    CHK(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+    hipEvent_t fork, join;
+    CHK(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
+    CHK(hipEventCreateWithFlags(&join, hipEventDisableTiming));
+    hipGraphExec_t x[2];
+    for (int q = 0; q < 2; q++) {
+        hipGraph_t g;
+        CHK(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
+        CHK(hipEventRecord(fork, cs));
+        hipLaunchKernelGGL(k_other<NW>, dim3(64), dim3(64), 0, cs, b, 0);               // policy
+        CHK(hipStreamWaitEvent(side, fork, 0));
+        hipLaunchKernelGGL(k_other<NW>, dim3(256), dim3(64), 20480, side, b, 20480);    // reset, side stream
+        CHK(hipEventRecord(join, side));
+        CHK(hipMemsetAsync(cnt + (1 - q), 0, sizeof(int), cs));                         // list counter
+        CHK(hipMemsetAsync(resp, 0, sizeof(int), cs));                                  // respawn counter
+        hipLaunchKernelGGL(k_step_like<NW>, dim3(waves), dim3(64), 24576, cs, b, cnt + (1 - q), resp, rec, 24576);
+        hipLaunchKernelGGL(k_other<NW>, dim3(512), dim3(64), 20480, cs, b, 20480);      // respawn
+        CHK(hipStreamWaitEvent(cs, join, 0));
+        hipLaunchKernelGGL(k_other<NW>, dim3(1024), dim3(256), 16384, cs, b, 16384);    // observations
+        CHK(hipStreamEndCapture(cs, &g));
+        CHK(hipGraphInstantiate(&x[q], g, nullptr, nullptr, 0));
+        CHK(hipGraphDestroy(g));
+    }
+    int bad = 0, first_bad = -1;
+    unsigned w1 = 0, w2 = 0;
+    for (int i = 0; i < replays; i++) {
+        CHK(hipMemsetAsync(rec, 0, 2 * sizeof(int), s));
+        CHK(hipGraphLaunch(x[i & 1], s));
+        int got[2] = {0, 0};
+        CHK(hipMemcpyAsync(got, rec, sizeof(got), hipMemcpyDeviceToHost, s));
+        CHK(hipStreamSynchronize(s));
+        if (got[0] != waves || got[1] != waves) {
+            bad++;
+            if (first_bad < 0) first_bad = i;
+            w1 = (unsigned)got[0] > w1 ? (unsigned)got[0] : w1;
+            w2 = (unsigned)got[1] > w2 ? (unsigned)got[1] : w2;
+        }
+    }
+    printf("engine city128 graph shape (fork/join, 2 memsets, %d-workgroup append), %d replays: %d bad (first %d, "
+           "worst counts 0x%08x 0x%08x)  %s\n",
+           waves, replays, bad, first_bad, w1, w2, bad ? "MISMATCH" : "OK");
+    for (int q = 0; q < 2; q++) CHK(hipGraphExecDestroy(x[q]));
+    CHK(hipEventDestroy(fork));
+    CHK(hipEventDestroy(join));
+    CHK(hipStreamDestroy(cs));
+    CHK(hipStreamDestroy(side));
+    CHK(hipFree(cnt));
+    CHK(hipFree(resp));
+    CHK(hipFree(rec));
+    return 0;
+}
+
 int main(int argc, char** argv) {
     hipStream_t s;
     CHK(hipStreamCreate(&s));
@@ -270,6 +362,7 @@ int main(int argc, char** argv) {
     if (probe_lds(s, 1024) || probe_lds(s, 7744) || probe_lds(s, 14304) || probe_lds(s, 32768) || probe_lds(s, 65536))
         return 1;
     if (argc < 2) return 0;  // "memset": also the captured memset (writes device memory from graph params)
+    if (argc > 2) return probe_fork(s, 400, 1) || probe_fork(s, 400, 4096);  // "memset fork": the engine's shape only
     if (probe_chain(s, 200, 1024) || probe_chain(s, 200, 14304)) return 1;
     if (probe_chain2(s, 200, 0) || probe_chain2(s, 200, 1) || probe_chain2(s, 50, 1, 1) || probe_chain2(s, 50, 1, 2))
         return 1;
