@@ -168,6 +168,47 @@ def cpu_baseline(args, builder_fn):
                           n_envs, steps, dt, rate1, steps1)}
 
 
+def env_range(rank, world, total_envs, envs_per_gpu=0):
+    """(envs on this rank, first global env, scaling, node-wide envs): a fixed count per rank (weak
+    scaling) or the node's total split into contiguous ranges (strong)."""
+    if envs_per_gpu:
+        return envs_per_gpu, rank * envs_per_gpu, "weak", envs_per_gpu * world
+    env0 = rank * total_envs // world
+    return (rank + 1) * total_envs // world - env0, env0, "strong", total_envs
+
+
+def timed_loop(one_step, steps, warmup, sync, distributed, before_timing=None):
+    """W untimed steps, then exactly K steps bracketed by sync() (the device) and a barrier on both
+    sides; returns this rank's wall time of the K steps."""
+    import torch.distributed as dist
+    for _ in range(warmup):
+        one_step()
+    sync()
+    if distributed:
+        dist.barrier()
+    if before_timing:
+        before_timing()
+    sync()
+    if distributed:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        one_step()
+    sync()
+    if distributed:
+        dist.barrier()
+    return time.perf_counter() - t0
+
+
+def max_over_ranks(elapsed, device):
+    """The slowest rank's time (every rank gets it)."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def main():
     args = parse()
     import torch
@@ -196,13 +237,7 @@ def main():
                                      minimum_zombies=args.min_zombies, max_episode_steps=args.max_episode_steps,
                                      obs_dtype=dtype, lanes_per_env=args.lanes_per_env)
 
-    if args.envs_per_gpu:
-        n_local, env0, scaling = args.envs_per_gpu, rank * args.envs_per_gpu, "weak"
-        total_envs = n_local * world
-    else:
-        total_envs, scaling = args.envs, "strong"
-        env0 = rank * total_envs // world
-        n_local = (rank + 1) * total_envs // world - env0
+    n_local, env0, scaling, total_envs = env_range(rank, world, args.envs, args.envs_per_gpu)
     eng = Engine(builder(n_local), device=dev)
     launch = eng.describe()
     launch["step_graph"] = not args.no_graph
@@ -212,8 +247,8 @@ def main():
 
     gather = None
     if args.gather and distributed:
-        # C5: every step's observation shards + (rewards, done, truncated) packed per env, all-gathered
-        # over RCCL into preallocated node-wide tensors (a centralised learner's input)
+        # C5: every step's observation shards + rewards / done / truncated, all-gathered over RCCL into
+        # node-wide tensors (a centralised learner's input) on a second stream while the next step runs
         from libzombsole_amd.vector import StepGather
         gather = StepGather(eng)
 
@@ -225,31 +260,20 @@ def main():
         # both are one replayed hipGraph whose step counter advances on the device
         nonlocal step
         step += 1
-        if use_graph:
+        if gather:
+            if use_graph:
+                gather.step(lambda out: eng.step_graph(step, 7, out=out))
+            else:
+                eng.gen_actions(step, 7)
+                gather.step(lambda out: eng.step(out=out))
+        elif use_graph:
             eng.step_graph(step, 7)
         else:
             eng.gen_actions(step, 7)
             eng.step()
-        if gather:
-            gather()
 
-    for _ in range(args.warmup):
-        one_step()
-    torch.cuda.synchronize()
-    if distributed:
-        dist.barrier()
-    if not use_graph:
-        eng.profile(True)
-    torch.cuda.synchronize()
-    if distributed:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        one_step()
-    torch.cuda.synchronize()
-    if distributed:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed = timed_loop(one_step, args.steps, args.warmup, torch.cuda.synchronize, distributed,
+                         before_timing=None if use_graph else (lambda: eng.profile(True)))
     prof_steps = args.steps
     if use_graph:
         # per-kernel HIP-event durations: the same steps launched one kernel at a time right after
@@ -276,9 +300,7 @@ def main():
     torch.cuda.synchronize()
     ends = ends.tolist()
     if distributed:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = max_over_ranks(elapsed, torch.device("cuda", local))
     value = total_envs * args.steps / elapsed
 
     # roofline of the dominant kernel (HIP-event durations on the engine's stream)
@@ -331,7 +353,8 @@ def main():
                        world, "RCCL all-gather of obs + rewards/done per step" if gather
                        else "no data-path collective"), "launch": launch,
                    "episode_ends_per_step": {"done": ends[0] / mix_steps, "truncated": ends[1] / mix_steps,
-                                             "fraction_of_envs": ends[0] / mix_steps / n_local,
+                                             # done or truncated: each is an autoreset at the next step
+                                             "fraction_of_envs": (ends[0] + ends[1]) / mix_steps / n_local,
                                              "sample": "%d untimed steps after the timed window, rank 0" % mix_steps}},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,

@@ -204,8 +204,9 @@ int zs_gen_actions(zs_handle* h, uint64_t step, int32_t n_discrete, int32_t* act
 
 /* The bench loop's step as one replayed hipGraph: zs_gen_actions for step number t, then
  * zs_step (same outputs), where t = step0 on the first call after a (re)capture and advances by
- * one per call on the device.  The launches are captured once per pending-reset-list parity and
- * recaptured when any buffer argument changes; results equal zs_gen_actions + zs_step. */
+ * one per call on the device.  The launches are captured once per pending-reset-list parity for
+ * each set of buffer arguments (the last 4 sets are kept, so double-buffered outputs replay
+ * without recapture); results equal zs_gen_actions + zs_step. */
 int zs_step_graph(zs_handle* h, uint64_t step0, int32_t n_discrete, int32_t* actions_dev, void* obs_dev,
                   double* rewards_dev, uint8_t* done_dev, uint8_t* trunc_dev, uint8_t* listed_dev,
                   uint8_t* reset_dev, void* stream);

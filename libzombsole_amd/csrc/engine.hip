@@ -277,8 +277,15 @@ struct zs_handle {
     ObsLayout obs_gl;      // its per-wave image
     // zs_step_graph: one captured hipGraph per autoreset-list parity (the step alternates the two
     // pending-reset lists), replayed on the caller's stream; keyed by the caller's buffers
-    hipGraphExec_t gexec[2] = {nullptr, nullptr};
-    const void* gkey[8] = {};
+    // a few buffer sets cached (a caller alternating double-buffered outputs, vector.StepGather)
+    struct GraphSet {
+        hipGraphExec_t g[2] = {nullptr, nullptr};  // per pending-list parity
+        const void* key[8] = {};
+        uint64_t used = 0;
+    };
+    static const int kGraphSets = 4;
+    GraphSet gsets[kGraphSets];
+    uint64_t gclock = 0;
     uint64_t* d_gstep = nullptr;  // [0] policy step counter (k_gen_actions_dev reads, the step launch advances)
     int capturing = 0;            // zs_step is being captured by zs_step_graph
     int forked = 0;               // zs_step_graph recorded ev_rfork itself (before its policy launch)
@@ -347,11 +354,12 @@ static void free_all(zs_handle* h) {
     h->ev_rfork = h->ev_rjoin = nullptr;
     if (h->s_reset) (void)hipStreamDestroy(h->s_reset);
     h->s_reset = nullptr;
-    for (hipGraphExec_t& g : h->gexec)
-        if (g) {
-            (void)hipGraphExecDestroy(g);
-            g = nullptr;
-        }
+    for (auto& gs : h->gsets)
+        for (hipGraphExec_t& g : gs.g)
+            if (g) {
+                (void)hipGraphExecDestroy(g);
+                g = nullptr;
+            }
     for (hipEvent_t ev : h->ev_pool) (void)hipEventDestroy(ev);
     h->ev_pool.clear();
 }
@@ -1148,10 +1156,17 @@ extern "C" int zs_step_graph(zs_handle* h, uint64_t step0, int32_t n_discrete, i
     HIPCHK(hipSetDevice(h->device));
     const void* key[8] = {actions_dev, obs_dev, rewards_dev, done_dev, trunc_dev, listed_dev, reset_dev,
                           (const void*)(intptr_t)n_discrete};
-    bool same = h->gexec[0] && h->gexec[1];
-    for (int k = 0; k < 8 && same; k++) same = key[k] == h->gkey[k];
-    if (!same) {
-        for (hipGraphExec_t& g : h->gexec)
+    zs_handle::GraphSet* set = nullptr;
+    for (auto& gs : h->gsets) {
+        bool same = gs.g[0] && gs.g[1];
+        for (int k = 0; k < 8 && same; k++) same = key[k] == gs.key[k];
+        if (same) set = &gs;
+    }
+    if (!set) {  // capture into the least recently used set
+        set = &h->gsets[0];
+        for (auto& gs : h->gsets)
+            if (gs.used < set->used) set = &gs;
+        for (hipGraphExec_t& g : set->g)
             if (g) {
                 HIPCHK(hipGraphExecDestroy(g));
                 g = nullptr;
@@ -1194,7 +1209,7 @@ extern "C" int zs_step_graph(zs_handle* h, uint64_t step0, int32_t n_discrete, i
             hipError_t ce = hipStreamEndCapture(cs, &graph);
             if (rc == ZS_OK && ce != hipSuccess) rc = fail(ZS_EHIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(ce));
             if (rc == ZS_OK) {
-                hipError_t ie = hipGraphInstantiate(&h->gexec[(p0 + g) & 1], graph, nullptr, nullptr, 0);
+                hipError_t ie = hipGraphInstantiate(&set->g[(p0 + g) & 1], graph, nullptr, nullptr, 0);
                 if (ie != hipSuccess) rc = fail(ZS_EHIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(ie));
             }
             if (graph) (void)hipGraphDestroy(graph);
@@ -1204,17 +1219,18 @@ extern "C" int zs_step_graph(zs_handle* h, uint64_t step0, int32_t n_discrete, i
         h->capturing = 0;
         (void)hipStreamDestroy(cs);
         if (rc != ZS_OK) {
-            for (hipGraphExec_t& g : h->gexec)
+            for (hipGraphExec_t& g : set->g)
                 if (g) {
                     (void)hipGraphExecDestroy(g);
                     g = nullptr;
                 }
             return rc;
         }
-        for (int k = 0; k < 8; k++) h->gkey[k] = key[k];
+        for (int k = 0; k < 8; k++) set->key[k] = key[k];
     }
-    // gexec[p] drains list p (the parity of this step) and fills list 1 - p
-    HIPCHK(hipGraphLaunch(h->gexec[h->rpar], s));
+    set->used = ++h->gclock;
+    // g[p] drains list p (the parity of this step) and fills list 1 - p
+    HIPCHK(hipGraphLaunch(set->g[h->rpar], s));
     h->rpar = 1 - h->rpar;
     return ZS_OK;
 }

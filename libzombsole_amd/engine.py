@@ -117,12 +117,9 @@ class Engine(object):
         dt = {_abi.DTYPE_I32: torch.int32, _abi.DTYPE_I64: torch.int64, _abi.DTYPE_I16: torch.int16}
         self.obs_dtype = dt[builder.cfg.obs_dtype]
         kw = dict(device=self.device)
-        self.obs = torch.zeros((self.N,) + self.obs_shape, dtype=self.obs_dtype, **kw)
-        self.rewards = torch.zeros((self.N, self.A if self.multi else 1), dtype=torch.float64, **kw)
-        self.done = torch.zeros(self.N, dtype=torch.uint8, **kw)
-        self.trunc = torch.zeros(self.N, dtype=torch.uint8, **kw)
-        self.listed = torch.zeros((self.N, self.A), dtype=torch.uint8, **kw)
-        self.was_reset = torch.zeros(self.N, dtype=torch.uint8, **kw)
+        self.out = self.outputs()
+        self.obs, self.rewards, self.done, self.trunc = self.out.obs, self.out.rewards, self.out.done, self.out.trunc
+        self.listed, self.was_reset = self.out.listed, self.out.was_reset
         self.actions = torch.zeros((self.N, self.A, 3), dtype=torch.int32, **kw)
         n = C.c_int32()
         self.L.zs_state_size(self.h, C.byref(n))
@@ -155,24 +152,32 @@ class Engine(object):
             _raise(self.L, rc, "zs_reset")
         return self.obs
 
-    def step(self, actions=None):
-        """One tick for all envs; `actions` int32 [N, A, 3] device tensor (default: self.actions)."""
+    def outputs(self, rows=None):
+        """A set of step output buffers (StepOutputs) with `rows` >= N rows; the engine writes the
+        first N.  Steps may alternate between sets (double-buffered outputs, vector.StepGather)."""
+        return StepOutputs(self, self.N if rows is None else max(int(rows), self.N))
+
+    def step(self, actions=None, out=None):
+        """One tick for all envs; `actions` int32 [N, A, 3] device tensor (default: self.actions);
+        outputs into `out` (default: self.out)."""
         a = self.actions if actions is None else actions
-        rc = self.L.zs_step(self.h, _ptr(a), _ptr(self.obs), _ptr(self.rewards), _ptr(self.done),
-                            _ptr(self.trunc), _ptr(self.listed), _ptr(self.was_reset), self._stream())
+        o = self.out if out is None else out
+        rc = self.L.zs_step(self.h, _ptr(a), _ptr(o.obs), _ptr(o.rewards), _ptr(o.done),
+                            _ptr(o.trunc), _ptr(o.listed), _ptr(o.was_reset), self._stream())
         if rc:
             _raise(self.L, rc, "zs_step")
-        return self.obs, self.rewards, self.done, self.trunc
+        return o.obs[:self.N], o.rewards[:self.N], o.done[:self.N], o.trunc[:self.N]
 
-    def step_graph(self, step0, n_discrete):
+    def step_graph(self, step0, n_discrete, out=None):
         """gen_actions(t, n_discrete) + step() as one replayed hipGraph (t = step0 on the first call,
         then advancing by one per call on the device)."""
-        rc = self.L.zs_step_graph(self.h, int(step0), int(n_discrete), _ptr(self.actions), _ptr(self.obs),
-                                  _ptr(self.rewards), _ptr(self.done), _ptr(self.trunc), _ptr(self.listed),
-                                  _ptr(self.was_reset), self._stream())
+        o = self.out if out is None else out
+        rc = self.L.zs_step_graph(self.h, int(step0), int(n_discrete), _ptr(self.actions), _ptr(o.obs),
+                                  _ptr(o.rewards), _ptr(o.done), _ptr(o.trunc), _ptr(o.listed),
+                                  _ptr(o.was_reset), self._stream())
         if rc:
             _raise(self.L, rc, "zs_step_graph")
-        return self.obs, self.rewards, self.done, self.trunc
+        return o.obs[:self.N], o.rewards[:self.N], o.done[:self.N], o.trunc[:self.N]
 
     def observe(self, mask=None):
         """Re-encode observations from the current state (after pokes)."""
@@ -283,6 +288,26 @@ class Engine(object):
         buf = self.get_rng(env)
         r = rnd or _random
         r.setstate((3, tuple(int(v) for v in buf), None))
+
+
+class StepOutputs(object):
+    """One set of zs_step output buffers, `rows` >= N rows (rows past N are padding the engine never
+    writes: equal-sized shards for a collective).  Rewards, done and truncated live in one flat byte
+    tensor (`flat`: float64 rewards [rows][R], then done [rows], then truncated [rows]) so a per-step
+    exchange moves them in one collective."""
+
+    def __init__(self, eng, rows):
+        torch = eng.torch
+        kw = dict(device=eng.device)
+        R = eng.A if eng.multi else 1
+        self.rows = rows
+        self.obs = torch.zeros((rows,) + eng.obs_shape, dtype=eng.obs_dtype, **kw)
+        self.flat = torch.zeros(rows * (8 * R + 2), dtype=torch.uint8, **kw)
+        self.rewards = self.flat[:8 * R * rows].view(torch.float64).view(rows, R)
+        self.done = self.flat[8 * R * rows:(8 * R + 1) * rows]
+        self.trunc = self.flat[(8 * R + 1) * rows:]
+        self.listed = torch.zeros((rows, eng.A), dtype=torch.uint8, **kw)
+        self.was_reset = torch.zeros(rows, dtype=torch.uint8, **kw)
 
 
 class StateView(object):

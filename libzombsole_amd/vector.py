@@ -116,17 +116,21 @@ def _all_gather_rows(out, x, group):
     dist.all_gather_into_tensor(out, x, group=group)
 
 
-def gather_observations(obs, group=None):
+def gather_observations(obs, group=None, sizes=None):
     """All-gather every rank's observation shard into one [sum(N_r), ...] tensor in global env
     order.
 
-    Shards from `shard_range` differ by at most one env: the per-rank sizes are exchanged first and
-    short shards padded to the longest, so every rank issues one equal-sized collective.  Over RCCL
-    on MI355X it is one all_gather_into_tensor; with gloo (CPU tests) the same call on host tensors."""
+    Shards from `shard_range` differ by at most one env: short shards are padded to the longest, so
+    every rank issues one equal-sized collective.  `sizes` (every rank's shard size, e.g. from
+    shard_range) saves a size exchange and its host sync per call; per-step callers should use
+    StepGather, which also overlaps the exchange with the next step.  Over RCCL on MI355X it is one
+    all_gather_into_tensor; with gloo (CPU tests) the same call on host tensors."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
-    sizes = _gather_sizes(obs.shape[0], obs.device, group)
+    if sizes is None:
+        sizes = _gather_sizes(obs.shape[0], obs.device, group)
+    sizes = [int(v) for v in sizes]
     m = max(sizes)
     x = obs.contiguous()
     if x.shape[0] < m:
@@ -139,15 +143,24 @@ def gather_observations(obs, group=None):
 
 
 class StepGather(object):
-    """C5's per-step exchange for a centralised learner: every rank's observation
-    shard plus its rewards / done / truncated, all-gathered into preallocated node-wide tensors.
+    """C5's per-step exchange for a centralised learner, overlapped with the next
+    step's compute.
 
-    Rewards (float64 [N, A] as bytes), done and truncated are packed into one uint8 row per env so
-    the exchange is two collectives per step.  The shard sizes are exchanged once, at construction;
-    short shards (sizes differ by one when the total does not divide) are padded, and `obs()` /
-    `rewards()` / `done()` / `truncated()` return the node-wide tensors in global env order."""
+    Every rank's observation shard plus its rewards / done / truncated are all-gathered into node-wide
+    tensors.  The engine writes each step into one of `depth` output sets (Engine.outputs), padded to
+    the longest shard, so the exchange copies nothing: the observations are one collective and
+    rewards / done / truncated (one flat byte tensor per set, engine.StepOutputs) a second.  Step t
+    writes set t % depth on the caller's stream; its collectives are issued on a communication stream
+    that waits for that step only, so they run while step t + 1 computes into the next set; before a
+    set is written again the caller's stream waits for the collectives that read it.  With gloo (CPU
+    tensors) everything is synchronous.
 
-    def __init__(self, engine, group=None):
+        g = StepGather(eng)
+        g.step(lambda out: eng.step_graph(t, 7, out=out))   # per step
+        g.obs(), g.rewards(), g.done(), g.truncated()      # the last step's node-wide tensors
+    """
+
+    def __init__(self, engine, group=None, depth=2):
         import torch
         import torch.distributed as dist
         self.torch = torch
@@ -155,42 +168,76 @@ class StepGather(object):
         self.group = group
         self.world = dist.get_world_size(group)
         self.n = engine.N
-        self.sizes = _gather_sizes(self.n, engine.device, group)
+        self.sizes = _gather_sizes(self.n, engine.device, group)  # once: shards keep their size
         self.m = max(self.sizes)
-        self.R = engine.rewards.shape[1]
+        self.R = engine.A if engine.multi else 1
+        self.depth = int(depth)
+        self.sets = [engine.outputs(rows=self.m) for _ in range(self.depth)]
+        shape = tuple(self.sets[0].obs.shape[1:])
         dev = engine.device
-        shape = tuple(engine.obs.shape[1:])
-        self.pad = None if self.n == self.m else torch.zeros((self.m,) + shape, dtype=engine.obs.dtype, device=dev)
-        self.pack = torch.zeros((self.m, 8 * self.R + 2), dtype=torch.uint8, device=dev)
-        self.g_obs = torch.empty((self.world * self.m,) + shape, dtype=engine.obs.dtype, device=dev)
-        self.g_pack = torch.empty((self.world * self.m, 8 * self.R + 2), dtype=torch.uint8, device=dev)
+        self.g_obs = [torch.empty((self.world * self.m,) + shape, dtype=self.sets[0].obs.dtype, device=dev)
+                      for _ in range(self.depth)]
+        self.g_flat = [torch.empty(self.world * self.sets[0].flat.numel(), dtype=torch.uint8, device=dev)
+                       for _ in range(self.depth)]
+        cuda = dev.type == "cuda"
+        self.comm = torch.cuda.Stream(device=dev) if cuda else None
+        self.pending = [None] * self.depth  # per set: event after the collectives that read it
+        self.t = 0
+        self.last = None
 
-    def __call__(self):
-        e, n, R = self.eng, self.n, self.R
-        self.pack[:n, :8 * R].copy_(e.rewards.view(self.torch.uint8).view(n, 8 * R))
-        self.pack[:n, 8 * R] = e.done
-        self.pack[:n, 8 * R + 1] = e.trunc
-        src = e.obs
-        if self.pad is not None:
-            self.pad[:n].copy_(e.obs)
-            src = self.pad
-        _all_gather_rows(self.g_obs, src, self.group)
-        _all_gather_rows(self.g_pack, self.pack, self.group)
+    def step(self, run):
+        """run(out) issues one engine step into output set `out` on the current stream; the step's
+        exchange follows on the communication stream.  Returns the set used."""
+        torch = self.torch
+        k = self.t % self.depth
+        out = self.sets[k]
+        if self.pending[k] is not None:
+            torch.cuda.current_stream(self.eng.device).wait_event(self.pending[k])
+        run(out)
+        if self.comm is not None:
+            done = torch.cuda.Event()
+            done.record(torch.cuda.current_stream(self.eng.device))
+            self.comm.wait_event(done)
+            with torch.cuda.stream(self.comm):
+                _all_gather_rows(self.g_obs[k], out.obs, self.group)
+                _all_gather_rows(self.g_flat[k], out.flat, self.group)
+                ev = torch.cuda.Event()
+                ev.record(self.comm)
+            self.pending[k] = ev
+        else:
+            _all_gather_rows(self.g_obs[k], out.obs, self.group)
+            _all_gather_rows(self.g_flat[k], out.flat, self.group)
+        self.last = k
+        self.t += 1
+        return out
+
+    def wait(self):
+        """Make the current stream wait for the last step's exchange (before reading its results)."""
+        if self.last is not None and self.pending[self.last] is not None:
+            self.torch.cuda.current_stream(self.eng.device).wait_event(self.pending[self.last])
 
     def _rows(self, t):
         if all(s == self.m for s in self.sizes):
             return t
         return self.torch.cat([t[r * self.m:r * self.m + s] for r, s in enumerate(self.sizes)], dim=0)
 
+    def _flat(self, lo, hi):
+        """Rows [lo, hi) of every rank's flat buffer segment (units: bytes per row), ranks in order."""
+        self.wait()
+        f = self.g_flat[self.last].view(self.world, -1)
+        m = self.m
+        return self.torch.cat([f[r, lo * m:hi * m].view(m, hi - lo)[:s] for r, s in enumerate(self.sizes)], dim=0)
+
     def obs(self):
-        return self._rows(self.g_obs)
+        self.wait()
+        return self._rows(self.g_obs[self.last])
 
     def rewards(self):
         R = self.R
-        return self._rows(self.g_pack[:, :8 * R]).contiguous().view(self.torch.float64).view(-1, R)
+        return self._flat(0, 8 * R).contiguous().view(self.torch.float64).view(-1, R)
 
     def done(self):
-        return self._rows(self.g_pack[:, 8 * self.R])
+        return self._flat(8 * self.R, 8 * self.R + 1).view(-1)
 
     def truncated(self):
-        return self._rows(self.g_pack[:, 8 * self.R + 1])
+        return self._flat(8 * self.R + 1, 8 * self.R + 2).view(-1)

@@ -5,7 +5,8 @@ how envs are split over ranks: each rank runs its `shard_range` of the bench wor
 through the C oracle (test infrastructure) and the all-reduced checksum must equal the
 single-rank run.  The optional observation gather (`gather_observations`) is checked with
 rank-tagged tensors, on shards of unequal size (25 envs over 2 ranks: 13 + 12), and C5's
-per-step `StepGather` (rewards / done / truncated packed beside the observations) likewise.
+per-step, double-buffered `StepGather` (rewards / done / truncated in one flat byte buffer beside the
+observations, padded output sets) over several steps, each step's gathered values checked.
 """
 import os
 import socket
@@ -45,20 +46,39 @@ def _worker(rank, world, port, q):
         cnt, csum = run_batch(_builder(), e0, n, STEPS, 7, threads=1)
         parts = [None] * world
         dist.all_gather_object(parts, (cnt, csum))
+        from libzombsole_amd.engine import StepOutputs
         from libzombsole_amd.vector import StepGather
         obs = torch.full((n, 2, 3, 5, 5), rank, dtype=torch.int32)
         g = gather_observations(obs)
-        # a stand-in engine (CPU tensors) for the per-step exchange
+        g2 = gather_observations(obs, sizes=[shard_range(TOTAL, r, world)[1] for r in range(world)])
+        # a stand-in engine (CPU tensors) for the per-step exchange: its step writes step-tagged values
         gl = torch.arange(e0, e0 + n)
-        fake = type("E", (), dict(N=n, device=torch.device("cpu"), obs=obs + 10 * gl.view(-1, 1, 1, 1, 1).int(),
-                                  rewards=(gl.double() / 4).view(-1, 1).repeat(1, 2),
-                                  done=(gl % 2).to(torch.uint8), trunc=(gl % 3 == 0).to(torch.uint8)))
-        sg = StepGather(fake)
-        sg()
-        ok = (torch.equal(sg.obs()[:, 0, 0, 0, 0], torch.arange(TOTAL).int() * 10 + (torch.arange(TOTAL) >= 13).int())
-              and torch.equal(sg.rewards()[:, 1], torch.arange(TOTAL).double() / 4)
-              and torch.equal(sg.done(), (torch.arange(TOTAL) % 2).to(torch.uint8))
-              and torch.equal(sg.truncated(), (torch.arange(TOTAL) % 3 == 0).to(torch.uint8)))
+
+        class Fake(object):
+            N, A, multi, obs_shape, obs_dtype, device, torch = n, 2, True, (2, 3, 5, 5), torch.int32, \
+                torch.device("cpu"), torch
+
+            def outputs(self, rows=None):
+                return StepOutputs(self, max(rows or n, n))
+
+        def run(t):
+            def fill(out):
+                out.obs[:n] = 10 * gl.view(-1, 1, 1, 1, 1).int() + 1000 * t
+                out.rewards[:n] = ((gl.double() / 4) + t).view(-1, 1).repeat(1, 2)
+                out.done[:n] = ((gl + t) % 2).to(torch.uint8)
+                out.trunc[:n] = ((gl + t) % 3 == 0).to(torch.uint8)
+            return fill
+
+        sg = StepGather(Fake())
+        ok = torch.equal(g, g2) and len(sg.sets) == 2 and all(s.obs.shape[0] == 13 for s in sg.sets)
+        ga = torch.arange(TOTAL)
+        for t in range(5):
+            used = sg.step(run(t))
+            ok = ok and used is sg.sets[t % 2]
+            ok = ok and (torch.equal(sg.obs()[:, 0, 0, 0, 0], ga.int() * 10 + 1000 * t)
+                         and torch.equal(sg.rewards()[:, 1], ga.double() / 4 + t)
+                         and torch.equal(sg.done(), ((ga + t) % 2).to(torch.uint8))
+                         and torch.equal(sg.truncated(), ((ga + t) % 3 == 0).to(torch.uint8)))
         if rank == 0:
             q.put((sum(c for c, _ in parts), sum(s for _, s in parts) % (1 << 64), g[:, 0, 0, 0, 0].tolist(), ok))
     finally:

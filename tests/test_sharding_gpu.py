@@ -79,15 +79,22 @@ def test_rccl_world1_gather():
         eng.seed(list(range(2048)))
         eng.reset()
         g = StepGather(eng)
-        for t in range(1, 6):
-            eng.step_graph(t, 7)
-            g()
+        ref = Engine(_c5(2048))  # the same envs stepped without the exchange, default outputs
+        ref.seed(list(range(2048)))
+        ref.reset()
+        for t in range(1, 9):
+            out = g.step(lambda o: eng.step_graph(t, 7, out=o))
+            assert out is g.sets[(t - 1) % 2]  # double-buffered outputs, graphs cached per set
+            ref.step_graph(t, 7)
             torch.cuda.synchronize()
-            assert torch.equal(g.obs(), eng.obs)
-            assert torch.equal(g.rewards(), eng.rewards)
-            assert torch.equal(g.done(), eng.done)
-            assert torch.equal(g.truncated(), eng.trunc)
-            assert torch.equal(gather_observations(eng.obs), eng.obs)
+            assert torch.equal(g.obs(), ref.obs)
+            assert torch.equal(out.obs, ref.obs)
+            assert torch.equal(g.rewards(), ref.rewards)
+            assert torch.equal(g.done(), ref.done)
+            assert torch.equal(g.truncated(), ref.trunc)
+            assert torch.equal(gather_observations(ref.obs), ref.obs)
+            assert torch.equal(gather_observations(ref.obs, sizes=[2048]), ref.obs)
+        ref.close()
         eng.close()
     finally:
         dist.destroy_process_group()
