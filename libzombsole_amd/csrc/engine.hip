@@ -415,7 +415,11 @@ static int validate(const zs_config* c) {
 // workgroups (at most 32 one-wave workgroups per CU), then the largest optional LDS copies (RNG
 // window beyond 64 words, spawn candidates, spawn lists).  A fused launch (reset work + tick in
 // one) allocates max(tick image, reset image) for every workgroup.
-static const int kResetWGs = 256;  // reset-work workgroups of a fused step launch
+// reset-work workgroups of a fused step launch (ZS_RESET_WGS overrides)
+static int reset_wgs() {
+    static const int n = getenv("ZS_RESET_WGS") ? std::max(1, atoi(getenv("ZS_RESET_WGS"))) : 256;
+    return n;
+}
 
 static bool getenv_off(const char* name) {
     const char* f = getenv(name);
@@ -444,7 +448,7 @@ static int choose_layout(zs_handle* h, int want_g, bool fused, int obs_bytes) {
     int lists = (d.nps + d.nzs <= 4096) ? d.nps + d.nzs : 0;
     for (int G = g0; G <= 64; G *= 2) {
         int ne = 64 / G;
-        int wgs = (d.N + ne - 1) / ne + (fused ? std::min(d.N, kResetWGs) : 0);
+        int wgs = (d.N + ne - 1) / ne + (fused ? std::min(d.N, reset_wgs()) : 0);
         int want = getenv_off("ZS_LDS_BUDGET") ? 1 : std::min(32, std::max(1, (wgs + 255) / 256));
         int best_res = -1;
         for (int pass = 0; pass < 2 && best_res < 0; pass++)  // windows below the need only if nothing else fits
@@ -976,7 +980,7 @@ static int launch_tick(zs_handle* h, const int32_t* actions, double* rew, uint8_
     const int p = h->rpar;
     // fused: the first n_reset workgroups rebuild the envs of the pending list (ended at the previous
     // call) while the others tick every other env; the two sets of envs are disjoint
-    const int n_reset = std::min(d.N, kResetWGs);
+    const int n_reset = std::min(d.N, reset_wgs());
     if (h->prof) HIPCHK(hipEventRecord(prof_event(h, &i0), s));
 #define ZS_TICK(GG)                                                                                                   \
     if (h->fused)                                                                                                     \

@@ -179,6 +179,70 @@ __device__ __forceinline__ void obs_cell_lds(const Dev& d, const ObsLayout& L, c
     weapon = (inb && sb) ? ((ev.x >> 8) & 255) : 0;
 }
 
+// One agent's 21 x 21 channels block into an LDS staging slot (`ot`, elements of S): this lane's
+// cells lane + 64 i.  The lookups of obs_cell_lds are issued level by level for a group of GRP cells
+// (window-map byte, static word and dead-body word of every cell of the group; then their entity pairs
+// and obstacle HP; then the selects and the slot writes), so the LDS round trips of the group overlap.
+// Cell by cell, each cell's slot writes sit between its reads and the next cell's, and (LDS addresses
+// the compiler cannot tell apart) every read waits for them: four dependent LDS waits per cell.
+#ifndef ZS_OBS_GRP
+#define ZS_OBS_GRP 1  // measured on one MI355X (2 runs each): C5 k_obs_lds 241 / 243 us at 1, 286 / 291 at 4
+#endif
+template <typename S, int GRP = ZS_OBS_GRP>
+__device__ __forceinline__ void obs_encode_block(const Dev& d, const ObsLayout& L, const lv4u* st4, const lu8* img,
+                                                 const lu8* wm, int ox, int oy, ZS_LDS S* ot, int lane) {
+    constexpr int WW = 21, PLANE = WW * WW, PER = (PLANE + 63) / 64;
+    const lv2i* ent = (const lv2i*)(img + L.off_life);
+    const lu32* dead = (const lu32*)(img + L.off_dead);
+    const li32* hpx = (const li32*)(img + L.off_hp);
+#pragma unroll
+    for (int i0 = 0; i0 < PER; i0 += GRP) {
+        constexpr int G2 = GRP;
+        int sb[G2];
+        zs_v4u sw[G2];
+        uint32_t dw[G2], bit[G2];
+        bool inb[G2];
+#pragma unroll
+        for (int k = 0; k < G2; k++) {
+            const int i = i0 + k < PER ? i0 + k : PER - 1;
+            const int cc = min(lane + 64 * i, PLANE - 1), r = cc / WW, q = cc - r * WW;
+            const int x = ox + q, y = oy + r;
+            inb[k] = (unsigned)x < (unsigned)d.W && (unsigned)y < (unsigned)d.H;
+            const int c = inb[k] ? y * d.W + x : 0;
+            bit[k] = 1u << (c & 31);
+            sb[k] = wm[cc];
+            sw[k] = st4[c >> 5];
+            dw[k] = dead[c >> 5];
+        }
+        zs_v2i ev[G2];
+        int ohp[G2];
+#pragma unroll
+        for (int k = 0; k < G2; k++) {
+            ev[k] = ent[sb[k] ? sb[k] - 1 : 0];
+            const bool isob = (sw[k].x & bit[k]) != 0u;
+            ohp[k] = hpx[isob ? (int)sw[k].w + __popc(sw[k].x & (bit[k] - 1u)) : 0];
+        }
+#pragma unroll
+        for (int k = 0; k < G2; k++) {
+            const int cell = lane + 64 * (i0 + k);
+            const bool isob = (sw[k].x & bit[k]) != 0u;
+            const bool obp = isob && ohp[k] != ZS_HP_ABSENT;
+            int code = (dw[k] & bit[k]) ? ZS_THING_DEADBODY : (sw[k].z & bit[k]) ? ZS_THING_OBJECTIVE : ZS_THING_NONE;
+            code = obp ? ((sw[k].y & bit[k]) ? ZS_THING_BOX : ZS_THING_WALL) : code;
+            code = sb[k] ? (ev[k].x & 255) : code;
+            code = inb[k] ? code : ZS_THING_WALL;
+            int lf = sb[k] ? ev[k].y : (obp ? ohp[k] : 0);
+            lf = inb[k] ? lf : 200;
+            const int weapon = (inb[k] && sb[k]) ? ((ev[k].x >> 8) & 255) : 0;
+            if (i0 + k < PER && cell < PLANE) {
+                ot[cell] = (S)code;
+                ot[PLANE + cell] = obs_val<S>(lf);
+                ot[2 * PLANE + cell] = (S)weapon;
+            }
+        }
+    }
+}
+
 // Stream env e's observations from its image: lane handles cells lane, lane + 64, ... of every
 // observation.  out = the base of the [N][nobs][C][h][w] tensor.
 //
@@ -596,7 +660,12 @@ __device__ __forceinline__ void obs_store_throttle() {
 // Stream one staged block to o: slot element k + mis / sizeof(T) holds output element k, so the
 // 16-B chunk q of the destination (counted from the 16-B boundary at or below o) reads the aligned
 // slot elements [q * VPC, (q + 1) * VPC).  The partial chunks at the two ends are element stores.
-template <typename T, int NBLK = 1, int THR = ZS_OBS_THR>
+// narrow (int16 / int32) blocks: C5's int16 stream moves a quarter of C3's bytes per cell and is not
+// write-bound, so its flush need not hold stores back
+#ifndef ZS_OBS_THR_NARROW
+#define ZS_OBS_THR_NARROW ZS_OBS_THR
+#endif
+template <typename T, int NBLK = 1, int THR = (sizeof(T) == 8 ? ZS_OBS_THR : ZS_OBS_THR_NARROW)>
 __device__ __forceinline__ void obs_stage_flush(const lu8* slot, T* o, int lane) {
     typedef typename obs_stage<T>::type S;
     constexpr int TS = (int)sizeof(T), VPC = 16 / TS, NB = NBLK * 3 * 441 * TS;
@@ -777,20 +846,8 @@ __global__ void __launch_bounds__(256, ZS_OBS_PIPE_WAVES) k_obs_lds(Dev d, T* ou
             const lu8* wm = img + a * PLANE;
             T* o = out + ((size_t)e * NOBS + a) * 3 * PLANE;
             ZS_LDS S* ot = (ZS_LDS S*)slot + (int)((uintptr_t)o & 15) / TS;
-            if (!(ZS_OBS_DIAG & 16)) {  // diagnostic builds: 16 skips the encoding, 8 the stores
-#pragma unroll
-                for (int i = 0; i < PER; i++) {
-                    const int cell = lane + 64 * i;
-                    const int cc = cell < PLANE ? cell : PLANE - 1, r = cc / WW, q = cc - r * WW;
-                    int code, lf, weapon;
-                    obs_cell_lds(d, L, st4, img, wm, cc, ox + q, oy + r, code, lf, weapon);
-                    if (cell < PLANE) {
-                        ot[cell] = (S)code;
-                        ot[PLANE + cell] = obs_val<S>(lf);
-                        ot[2 * PLANE + cell] = (S)weapon;
-                    }
-                }
-            }
+            if (!(ZS_OBS_DIAG & 16))  // diagnostic builds: 16 skips the encoding, 8 the stores
+                obs_encode_block<S>(d, L, st4, img, wm, ox, oy, ot, lane);
             wave_sync();
             if (!(ZS_OBS_DIAG & 8)) obs_stage_flush(slot, o, lane);
             wave_sync();
@@ -942,19 +999,7 @@ __global__ void __launch_bounds__(64 * (RING_ENC + RING_WRT), 1) k_obs_ring(Dev 
             const int32_t ap = pos[a];
             const int ox = unpack_x(ap) - WW / 2, oy = unpack_y(ap) - WW / 2;
             const lu8* wm = img + a * PLANE;
-            ZS_LDS S* ot = ot0 + a * 3 * PLANE;
-#pragma unroll
-            for (int i = 0; i < PER; i++) {
-                const int cell = lane + 64 * i;
-                const int cc = cell < PLANE ? cell : PLANE - 1, r = cc / WW, q2 = cc - r * WW;
-                int code, lf, weapon;
-                obs_cell_lds(d, L, st4, img, wm, cc, ox + q2, oy + r, code, lf, weapon);
-                if (cell < PLANE) {
-                    ot[cell] = (S)code;
-                    ot[PLANE + cell] = obs_val<S>(lf);
-                    ot[2 * PLANE + cell] = (S)weapon;
-                }
-            }
+            obs_encode_block<S>(d, L, st4, img, wm, ox, oy, ot0 + a * 3 * PLANE, lane);
         }
         ring_state_store(&state[PAIR * q + h], 2 * u + 1);
     }

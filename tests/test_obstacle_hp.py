@@ -124,7 +124,7 @@ def test_int32_floor_saturates_and_flags():
     from libzombsole_amd.engine import Engine, EngineError
     eng = Engine(_builder(8))
     eng.seed(list(range(8)))
-    _poke_all(eng, [(5, -2147483600), (6, -2147483600), (7, -2147483600)])
+    _poke_all(eng, [(5, -2147483630), (6, -2147483630), (7, -2147483630)])  # any hit (>= 25) passes the floor
     eng.reset()
     assert eng.overflow(clear=True) == _abi.OVF_INT16  # the poke itself left the int16 range
     eng.actions.copy_(torch.from_numpy(np.broadcast_to(FIXED, (8, 2, 3)).copy()))
@@ -134,7 +134,7 @@ def test_int32_floor_saturates_and_flags():
     assert eng.overflow() == _abi.OVF_INT16 | _abi.OVF_INT32
     for k in range(8):
         st = eng.get_state(k)
-        hit = [int(st.obst_life[i]) for i in (5, 6, 7) if int(st.obst_life[i]) != -2147483600]
+        hit = [int(st.obst_life[i]) for i in (5, 6, 7) if int(st.obst_life[i]) != -2147483630]
         assert hit and all(v == -2147483647 for v in hit), (k, list(st.obst_life[5:8]))
     with pytest.raises(OverflowError):
         eng.check_lossless()

@@ -12,3 +12,7 @@ if [ -n "$STAMPS" ]; then
   N_ENVS=8192 GS=16 timeout -k 10 120 python tools/stamps.py > gpurun_out/stamps_8192.log 2>&1 || exit 1
   N_ENVS=65536 GS=8 timeout -k 10 120 python tools/stamps.py > gpurun_out/stamps_65536.log 2>&1 || exit 1
 fi
+if [ -n "$AB_LIBS" ]; then
+  CFGS="${AB_CFGS:-c5 c3}" LIBS="$AB_LIBS" STEPS=100 bash tools/ab.sh > gpurun_out/ab.log 2>&1 || { tail -5 gpurun_out/ab.log; exit 1; }
+  cat gpurun_out/ab.log
+fi
