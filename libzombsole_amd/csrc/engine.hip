@@ -32,7 +32,6 @@ __global__ void __launch_bounds__(64, ZS_STEP_WAVES) k_step(Dev d, int n_reset, 
                                              uint8_t* done_out, uint8_t* trunc_out, uint8_t* listed_out,
                                              uint8_t* reset_out, int* reset_list, int* reset_count,
                                              const int* cur_list, const int* cur_count, int* err_out, void* obs_out) {
-    if (d.gstep_adv && blockIdx.x == 0 && threadIdx.x == 0) *d.gstep_adv += 1;
     if ((int)blockIdx.x < n_reset)
         reset_role(d, 1, cur_list, cur_count, nullptr, err_out, blockIdx.x, n_reset, d.fobs ? obs_out : nullptr);
     else
@@ -81,54 +80,34 @@ __global__ void k_seed(Dev d, int env0, int n, const uint64_t* seeds) {
 }
 
 // ---------------------------------------------------------------------------
-// bench / parity action stream (libzombsole_amd/actions.py)
+// bench / parity action stream (libzombsole_amd/actions.py; policy_action in zs_device.hpp)
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
-    uint64_t z = x + 0x9E3779B97F4A7C15ull;
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    return z ^ (z >> 31);
-}
-
-__constant__ int32_t c_discrete[7][3] = {{ZS_ACT_MOVE, 0, 1},  {ZS_ACT_MOVE, -1, 0},       {ZS_ACT_MOVE, 0, -1},
-                                         {ZS_ACT_MOVE, 1, 0},  {ZS_ACT_ATTACK_CLOSEST, 0, 0}, {ZS_ACT_HEAL, 0, 0},
-                                         {ZS_ACT_HEAL_CLOSEST, 0, 0}};
-
+// one thread per (env, agent): its triple
 __global__ void k_gen_actions(Dev d, uint64_t step, int n_discrete, int32_t* act) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= d.N * d.A) return;
-    int e = i / d.A, a = i - e * d.A;
-    uint64_t h = splitmix64(splitmix64(splitmix64(d.seeds[e]) ^ step) ^ (uint64_t)a);
-    int id = (int)(h % (uint64_t)n_discrete);
+    const int e = i / d.A;
+    const int id = policy_id(d.seeds[e], step, n_discrete, i - e * d.A);
     act[(size_t)i * 3 + 0] = c_discrete[id][0];
     act[(size_t)i * 3 + 1] = c_discrete[id][1];
     act[(size_t)i * 3 + 2] = c_discrete[id][2];
 }
 
-// The work-list counters a step appends to (eager zs_step; inside zs_step_graph's graph
-// k_gen_actions_dev zeroes them).
-__global__ void k_zero2(int* a, int* b) {
-    if (threadIdx.x == 0 && a) *a = 0;
-    if (threadIdx.x == 1 && b) *b = 0;
+// The same policy for the step number in device memory (zs_step_graph with the reset work on a side
+// stream: launched after the reset fork, it gives the reset work a head start on the tick)
+__global__ void k_gen_actions_ctr(Dev d, const uint64_t* ctr, int n_discrete, int32_t* act) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= d.N * d.A) return;
+    const int e = i / d.A;
+    const int id = policy_id(d.seeds[e], ctr[0], n_discrete, i - e * d.A);
+    act[(size_t)i * 3 + 0] = c_discrete[id][0];
+    act[(size_t)i * 3 + 1] = c_discrete[id][1];
+    act[(size_t)i * 3 + 2] = c_discrete[id][2];
 }
 
-// The same policy with the step read from device memory (zs_step_graph; the step launch advances
-// it, Dev::gstep_adv).  Its first workgroup also zeroes the work-list counters the step appends to
-// (k_zero2's job in eager steps): one launch fewer ahead of the tick.
-__global__ void __launch_bounds__(256) k_gen_actions_dev(Dev d, const uint64_t* ctr, int n_discrete, int32_t* act,
-                                                         int* z0, int* z1) {
-    const uint64_t step = ctr[0];
-    if (blockIdx.x == 0 && threadIdx.x == 0 && z0) *z0 = 0;
-    if (blockIdx.x == 0 && threadIdx.x == 1 && z1) *z1 = 0;
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < d.N * d.A) {
-        int e = i / d.A, a = i - e * d.A;
-        uint64_t h = splitmix64(splitmix64(splitmix64(d.seeds[e]) ^ step) ^ (uint64_t)a);
-        int id = (int)(h % (uint64_t)n_discrete);
-        act[(size_t)i * 3 + 0] = c_discrete[id][0];
-        act[(size_t)i * 3 + 1] = c_discrete[id][1];
-        act[(size_t)i * 3 + 2] = c_discrete[id][2];
-    }
+// the step's tail when no observation launch ends the step (observations written by the step launch)
+__global__ void k_tail(Dev d) {
+    if (threadIdx.x == 0) step_tail(d);
 }
 
 // ---------------------------------------------------------------------------
@@ -286,9 +265,8 @@ struct zs_handle {
     static const int kGraphSets = 4;
     GraphSet gsets[kGraphSets];
     uint64_t gclock = 0;
-    uint64_t* d_gstep = nullptr;  // [0] policy step counter (k_gen_actions_dev reads, the step launch advances)
-    int capturing = 0;            // zs_step is being captured by zs_step_graph
-    int forked = 0;               // zs_step_graph recorded ev_rfork itself (before its policy launch)
+    uint64_t* d_gstep = nullptr;  // [0] policy step counter (the step's policy reads it, the step's tail advances it)
+    int graph_pol = 0;            // zs_step_graph is capturing a step with this policy (n_discrete), else 0
     int obs_pipe_wgs = 8;  // k_obs_pipe / k_obs_lds workgroups per CU
     // next-step reset work on a side stream, concurrent with the tick (the two touch disjoint envs);
     // the caller's stream joins it before the observations
@@ -1061,6 +1039,8 @@ extern "C" int zs_reset(zs_handle* h, const uint8_t* env_mask_dev, void* obs_dev
                                (const int*)h->d_rlist[p], (const int*)(h->d_rcount + p), h->d_rlist[q],
                                h->d_rcount + q, env_mask_dev, h->d.N);
             HIPCHK(hipGetLastError());
+            // the list the next step appends to (list[p] now) starts empty (zs_step's counter protocol)
+            HIPCHK(hipMemsetAsync(h->d_rcount + p, 0, sizeof(int), s));
             h->rpar = q;
         }
     }
@@ -1096,31 +1076,43 @@ extern "C" int zs_step(zs_handle* h, const int32_t* actions_dev, void* obs_dev, 
         side = h->reset_side != 0;
         hipStream_t rs = s;
         if (side) {  // fork: the reset work sees everything the caller queued before this call
-            // (zs_step_graph records the fork ahead of its policy launch: the actions are not an input)
-            if (!h->forked) HIPCHK(hipEventRecord(h->ev_rfork, s));
+            HIPCHK(hipEventRecord(h->ev_rfork, s));
             HIPCHK(hipStreamWaitEvent(h->s_reset, h->ev_rfork, 0));
             rs = h->s_reset;
+        }
+        // zs_step_graph's policy: with the reset work beside the tick, its own launch on the caller's
+        // stream right after the fork and ahead of the reset launch (captured in that order, the graph
+        // starts the policy first: C3 173 M env-steps/s, against 167 with the reset launch captured first
+        // and 169 with the policy inside the step launch); otherwise inside the step launch (no launch,
+        // no gap: 8 192 envs 110 -> 117 M env-steps/s)
+        if (h->graph_pol && side) {
+            const int n = h->d.N * h->d.A;
+            hipLaunchKernelGGL(k_gen_actions_ctr, dim3((n + 255) / 256), dim3(256), 0, s, h->d,
+                               (const uint64_t*)h->d_gstep, h->graph_pol, (int32_t*)actions_dev);
+            HIPCHK(hipGetLastError());
         }
         rc = launch_reset(h, 1, nullptr, h->d.fobs ? obs_dev : nullptr, rs);
         if (rc) return rc;
         if (side) HIPCHK(hipEventRecord(h->ev_rjoin, h->s_reset));
     }
-    // 2) tick every other env; envs that end now are queued on list[q] for the next call.
-    // The work-list counters this call appends to are zeroed by k_zero2 (eager steps) or, inside
-    // zs_step_graph's graph, by the policy kernel ahead of the step.  Not by captured 4-byte
-    // hipMemsetAsync nodes: in this engine's city128 graph such nodes left byte patterns
-    // (0x01010101 / 0x05050505 / 0xC0C0C0C0) in the counters (profiles/r02_graph_memset_city128.log,
-    // round 1's replay fault; tools/probe/graphprobe.hip reproduces the node sequence standalone).
-    // Every list index is bounds-checked in the kernels.
-    if (!h->capturing) {
-        hipLaunchKernelGGL(k_zero2, dim3(1), dim3(64), 0, s, h->d_rcount + q, h->d.defer_respawn ? h->d.resp_count : nullptr);
-        HIPCHK(hipGetLastError());
-    }
-    struct GstepScope {  // the step launch advances the graph's policy counter while capturing
+    struct PolScope {
         Dev& d;
-        GstepScope(Dev& dd, uint64_t* g) : d(dd) { d.gstep_adv = g; }
-        ~GstepScope() { d.gstep_adv = nullptr; }
-    } gscope(h->d, h->capturing ? h->d_gstep : nullptr);
+        PolScope(Dev& dd, int n, const uint64_t* st) : d(dd) {
+            d.pol_n = n;
+            d.pol_step = st;
+        }
+        ~PolScope() { d.pol_n = 0, d.pol_step = nullptr; }
+    } pol(h->d, side ? 0 : h->graph_pol, side ? nullptr : h->d_gstep);
+    // 2) tick every other env; envs that end now are queued on list[q] for the next call.
+    // Work-list counters: between calls the list the next step appends to (list[1 - rpar]) and the
+    // deferred-respawn list are empty.  This step appends to list[q] and resp_list, drains list[p] and
+    // resp_list, and its last launch (the observation kernel, else k_tail) empties list[p] and resp_list
+    // again (Dev::tail_*), so no launch ahead of the tick is needed.  (Not by captured 4-byte
+    // hipMemsetAsync nodes: in this engine's round-2 city128 graph such nodes left byte patterns in the
+    // counters, profiles/r02_graph_memset_city128.log; tools/probe/graphprobe.hip replays that node
+    // sequence standalone without a fault, profiles/r03_graphprobe_fork.log.)  Every list index is
+    // bounds-checked in the kernels.
+    const int p = h->rpar;
     rc = launch_tick(h, actions_dev, rewards_dev, done_dev, trunc_dev, listed_dev, reset_dev, h->d_rlist[q],
                      h->d_rcount + q, obs_dev, s);
     if (rc) return rc;
@@ -1130,9 +1122,22 @@ extern "C" int zs_step(zs_handle* h, const int32_t* actions_dev, void* obs_dev, 
         if (rc) return rc;
     }
     // join the reset work, then 3) observations of every env (already written by the step launch
-    // when fobs)
+    // when fobs), carrying the step's tail
     if (side) HIPCHK(hipStreamWaitEvent(s, h->ev_rjoin, 0));
-    if (h->d.fobs) return ZS_OK;
+    struct TailScope {
+        Dev& d;
+        TailScope(Dev& dd, int* c0, int* c1, uint64_t* st) : d(dd) {
+            d.tail_cnt0 = c0;
+            d.tail_cnt1 = c1;
+            d.tail_step = st;
+        }
+        ~TailScope() { d.tail_cnt0 = d.tail_cnt1 = nullptr, d.tail_step = nullptr; }
+    } tail(h->d, h->d_rcount + p, h->d.defer_respawn ? h->d.resp_count : nullptr, h->graph_pol ? h->d_gstep : nullptr);
+    if (h->d.fobs || !obs_dev) {
+        hipLaunchKernelGGL(k_tail, dim3(1), dim3(64), 0, s, h->d);
+        HIPCHK(hipGetLastError());
+        return ZS_OK;
+    }
     return launch_obs(h, obs_dev, nullptr, s);
 }
 
@@ -1186,7 +1191,6 @@ extern "C" int zs_step_graph(zs_handle* h, uint64_t step0, int32_t n_discrete, i
         HIPCHK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
         const int prof = h->prof;
         h->prof = 0;  // no timing events inside a graph
-        h->capturing = 1;
         const int p0 = h->rpar;
         int rc = ZS_OK;
         for (int g = 0; g < 2 && rc == ZS_OK; g++) {  // parity p0, then 1 - p0 (zs_step flips rpar)
@@ -1195,21 +1199,11 @@ extern "C" int zs_step_graph(zs_handle* h, uint64_t step0, int32_t n_discrete, i
                 rc = fail(ZS_EHIP, "hipStreamBeginCapture failed");
                 break;
             }
-            const int n = h->d.N * h->d.A;
-            if (!h->fused && h->reset_side) {  // the reset work does not wait for the policy
-                if (hipEventRecord(h->ev_rfork, cs) != hipSuccess) {
-                    (void)hipStreamEndCapture(cs, &graph);
-                    if (graph) (void)hipGraphDestroy(graph);
-                    rc = fail(ZS_EHIP, "hipEventRecord (reset fork) failed");
-                    break;
-                }
-                h->forked = 1;
-            }
-            // the policy kernel also zeroes the step's work-list counters (k_zero2 in eager steps)
-            hipLaunchKernelGGL(k_gen_actions_dev, dim3((n + 255) / 256), dim3(256), 0, cs, h->d, h->d_gstep, n_discrete,
-                               actions_dev, h->d_rcount + (1 - h->rpar), h->d.defer_respawn ? h->d.resp_count : nullptr);
+            // the step's policy reads the step number *d_gstep (zs_step: its own launch, or inside the
+            // step launch), the step's tail advances it
+            h->graph_pol = n_discrete;
             rc = zs_step(h, actions_dev, obs_dev, rewards_dev, done_dev, trunc_dev, listed_dev, reset_dev, cs);
-            h->forked = 0;
+            h->graph_pol = 0;
             hipError_t ce = hipStreamEndCapture(cs, &graph);
             if (rc == ZS_OK && ce != hipSuccess) rc = fail(ZS_EHIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(ce));
             if (rc == ZS_OK) {
@@ -1218,9 +1212,8 @@ extern "C" int zs_step_graph(zs_handle* h, uint64_t step0, int32_t n_discrete, i
             }
             if (graph) (void)hipGraphDestroy(graph);
         }
-        h->rpar = p0;  // capturing ran no work: the lists are where they were
+        h->rpar = p0;  // a capture runs no work: the lists are where they were
         h->prof = prof;
-        h->capturing = 0;
         (void)hipStreamDestroy(cs);
         if (rc != ZS_OK) {
             for (hipGraphExec_t& g : set->g)

@@ -138,9 +138,16 @@ struct Dev {
     uint32_t* dead;
     uint32_t* ring;
     uint32_t* rngst;
-    // inside zs_step_graph's graph: the policy's step counter, advanced by the step launch's first
-    // workgroup (k_gen_actions_dev, earlier in the same stream, has read it); null otherwise
-    uint64_t* gstep_adv;
+    // zs_step_graph: the bench policy (zs_gen_actions) is generated by the step launch itself for step
+    // *pol_step with pol_n discrete actions (0: actions read from the caller's buffer)
+    const uint64_t* pol_step;
+    int pol_n;
+    // the step's tail (zs_step), done by the last launch of the step (the observation kernel, or
+    // k_tail): zero the pending-list counter this step drained and the deferred-respawn counter (the
+    // next step appends to them), advance the policy step counter; null fields = nothing to do
+    int* tail_cnt0;
+    int* tail_cnt1;
+    uint64_t* tail_step;
     uint64_t* seeds;
     int32_t* cand;
     int* resp_list;   // envs whose respawn the tick deferred to k_respawn [N]
@@ -167,6 +174,36 @@ __device__ __forceinline__ int32_t hp_store_value(const Dev& d, int64_t v) {
         atomicOr(d.ovf, f);
     }
     return (int32_t)v;
+}
+
+// the step's tail (see Dev::tail_*), by one thread of the last launch of a zs_step
+__device__ __forceinline__ void step_tail(const Dev& d) {
+    if (d.tail_cnt0) *d.tail_cnt0 = 0;
+    if (d.tail_cnt1) *d.tail_cnt1 = 0;
+    if (d.tail_step) *d.tail_step += 1;
+}
+
+// bench / parity action stream (libzombsole_amd/actions.py): agent a of env e at step t takes
+// DISCRETE[splitmix64(splitmix64(splitmix64(seed_e) ^ t) ^ a) % n]
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__constant__ int32_t c_discrete[7][3] = {{ZS_ACT_MOVE, 0, 1},  {ZS_ACT_MOVE, -1, 0},       {ZS_ACT_MOVE, 0, -1},
+                                         {ZS_ACT_MOVE, 1, 0},  {ZS_ACT_ATTACK_CLOSEST, 0, 0}, {ZS_ACT_HEAL, 0, 0},
+                                         {ZS_ACT_HEAL_CLOSEST, 0, 0}};
+
+// the policy's discrete action id for agent a of the env seeded `seed`
+__device__ __forceinline__ int policy_id(uint64_t seed, uint64_t step, int n, int a) {
+    return (int)(splitmix64(splitmix64(splitmix64(seed) ^ step) ^ (uint64_t)a) % (uint64_t)n);
+}
+// component k (0..3A) of an env's action triples under the policy
+__device__ __forceinline__ int32_t policy_action(uint64_t seed, uint64_t step, int n, int k) {
+    const int a = k / 3;
+    return c_discrete[policy_id(seed, step, n, a)][k - 3 * a];
 }
 
 __device__ __forceinline__ int32_t pack_xy(int x, int y) { return (int32_t)((uint32_t)(x & 0xffff) | ((uint32_t)y << 16)); }

@@ -429,6 +429,7 @@ __device__ __forceinline__ void obs_stream_any(const Dev& d, const ObsLayout& L,
 // workgroup's static tables (stat_words = 4 * DW, or 0).
 template <typename T>
 __global__ void __launch_bounds__(256) k_obs(Dev d, T* out, const uint8_t* mask, ObsLayout L, int stat_words) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) step_tail(d);  // a zs_step's tail (Dev::tail_*)
     extern __shared__ __align__(16) uint8_t smem[];
     const int wave = threadIdx.x >> 6, wpg = blockDim.x >> 6;
     lu32* st = (lu32*)smem;
@@ -551,6 +552,7 @@ __device__ __forceinline__ void obs_window_compact(const Dev& d, const ObsLayout
 
 template <typename T, int NOBS>
 __global__ void __launch_bounds__(256, ZS_OBS_PIPE_WAVES) k_obs_pipe(Dev d, T* out, ObsLayout L, int env0, int env1) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) step_tail(d);  // a zs_step's tail (Dev::tail_*)
     extern __shared__ __align__(16) uint8_t smem[];
     constexpr int WW = 21, PLANE = WW * WW, PER = (PLANE + 63) / 64;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -710,6 +712,7 @@ __device__ __forceinline__ void obs_stage_flush(const lu8* slot, T* o, int lane)
 // instead of three).
 template <typename T, int NOBS>
 __global__ void __launch_bounds__(256) k_obs_gather(Dev d, T* out, const uint8_t* mask, ObsLayout L, int stat) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) step_tail(d);  // a zs_step's tail (Dev::tail_*)
     extern __shared__ __align__(16) uint8_t smem[];
     constexpr int WW = 21, PLANE = WW * WW, PER = (PLANE + 63) / 64;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -810,9 +813,10 @@ __global__ void __launch_bounds__(256) k_obs_gather(Dev d, T* out, const uint8_t
 
 template <typename T, int NOBS>
 __global__ void __launch_bounds__(256, ZS_OBS_PIPE_WAVES) k_obs_lds(Dev d, T* out, ObsLayout L, int env0, int env1) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) step_tail(d);  // a zs_step's tail (Dev::tail_*)
     extern __shared__ __align__(16) uint8_t smem[];
     typedef typename obs_stage<T>::type S;
-    constexpr int WW = 21, PLANE = WW * WW, PER = (PLANE + 63) / 64, TS = (int)sizeof(T);
+    constexpr int WW = 21, PLANE = WW * WW, TS = (int)sizeof(T);
     constexpr int SLOT = obs_stage_slot_bytes(TS);
     // the wave index (hence the env and every block address) is wave-uniform: scalar registers, and
     // the buffer resources of the flush need no waterfall loop
@@ -936,9 +940,10 @@ __device__ __forceinline__ void ring_wait(const ZS_LDS int* p, int v) {
 
 template <typename T, int NOBS>
 __global__ void __launch_bounds__(64 * (RING_ENC + RING_WRT), 1) k_obs_ring(Dev d, T* out, ObsLayout L, int env0, int env1) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) step_tail(d);  // a zs_step's tail (Dev::tail_*)
     extern __shared__ __align__(16) uint8_t smem[];
     typedef typename obs_stage<T>::type S;
-    constexpr int WW = 21, PLANE = WW * WW, PER = (PLANE + 63) / 64, TS = (int)sizeof(T);
+    constexpr int WW = 21, PLANE = WW * WW, TS = (int)sizeof(T);
     constexpr int PAIR = ring_pair(TS, NOBS), US = RING_SLOTS / PAIR;  // envs per unit, unit slots
     constexpr int SLOT = obs_stage_slot_bytes(TS, NOBS * PAIR), BLK = NOBS * 3 * PLANE;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;

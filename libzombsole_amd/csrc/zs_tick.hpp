@@ -1060,9 +1060,15 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
     uint8_t vw[4], vr[4], vo[4];
     int mval = 0, av = 0;
     uint32_t bmv[8], opw = 0u;
+    uint64_t pseed = 0, pstep = 0;  // the fused policy's inputs (zs_step_graph)
     const int nmisc = MISC_N + 2 * A;
     if (active) {
-        if (A) av = actions[(size_t)e * A * 3 + min(j, 3 * A - 1)];
+        if (d.pol_n) {
+            pseed = d.seeds[e];
+            pstep = *d.pol_step;
+        } else if (A) {
+            av = actions[(size_t)e * A * 3 + min(j, 3 * A - 1)];
+        }
         needs_reset = d.scal[S_NEEDRESET * N + e];
         n_order = d.scal[S_NORDER * N + e];
         st = d.rngst[e];
@@ -1093,6 +1099,15 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
         opw = d.obst_present[(size_t)e * d.OW + min(j, d.OW - 1)];
     }
     stepping = active && needs_reset == 0;
+    if (active && d.pol_n) {
+        // zs_step_graph: the policy's actions for this step (zs_gen_actions' stream), written out to the
+        // caller's action buffer as the policy kernel would (envs reset by this call included)
+        for (int k = j; k < 3 * A; k += G) {
+            const int32_t v = policy_action(pseed, pstep, d.pol_n, k);
+            ((int32_t*)actions)[(size_t)e * A * 3 + k] = v;
+            if (stepping) LACT(c, k) = v;
+        }
+    }
     if (stepping) {
 #pragma unroll
         for (int u = 0; u < 4; u++) {
@@ -1106,8 +1121,10 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
             }
         }
         if (j < nmisc) MISC(c, j) = mval;
-        if (j < 3 * A) LACT(c, j) = av;
-        for (int k = j + G; k < 3 * A; k += G) LACT(c, k) = actions[(size_t)e * A * 3 + k];
+        if (!d.pol_n) {
+            if (j < 3 * A) LACT(c, j) = av;
+            for (int k = j + G; k < 3 * A; k += G) LACT(c, k) = actions[(size_t)e * A * 3 + k];
+        }
 #pragma unroll
         for (int u = 0; u < 8; u++)
             if (j + u * G < d.DW) c.bm[IX(c, j + u * G)] = bmv[u];
@@ -1356,7 +1373,6 @@ template <int G>
 __global__ void __launch_bounds__(64, ZS_STEP_WAVES) k_tick(Dev d, const int32_t* actions, double* rew, uint8_t* done_out,
                                              uint8_t* trunc_out, uint8_t* listed_out, uint8_t* reset_out,
                                              int* reset_list, int* reset_count, void* obs_out, int env0, int env1) {
-    if (d.gstep_adv && blockIdx.x == 0 && threadIdx.x == 0) *d.gstep_adv += 1;
     tick_wg<G>(d, xcd_remap(blockIdx.x, gridDim.x), actions, rew, done_out, trunc_out, listed_out, reset_out, reset_list,
                reset_count, obs_out, env0, env1);
 }
