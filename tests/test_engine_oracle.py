@@ -164,6 +164,7 @@ RESPAWN = {
     "deferred": {"ZS_DEFER_RESPAWN": "1"},
     "deferred_fused": {"ZS_DEFER_RESPAWN": "1", "ZS_FUSED": "1"},
     "deferred_unfused_serial_reset": {"ZS_DEFER_RESPAWN": "1", "ZS_FUSED": "0", "ZS_RESET_STREAM": "0"},
+    "deferred_unfused_side_reset": {"ZS_DEFER_RESPAWN": "1", "ZS_FUSED": "0"},
 }
 
 
@@ -236,3 +237,64 @@ def test_rng_window_reload(monkeypatch):
                                                initial_zombies=50, minimum_zombies=50),
                24, 30, check_state_every=15)
     run_parity(c2, 128, 60, check_state_every=30, graph=True)
+
+
+@pytest.mark.parametrize("fused", ["0", "1"])
+def test_masked_reset_of_pending_envs(fused, monkeypatch):
+    """Next-step autoreset, reset work on the side stream (unfused) or inside the step launch: between
+    calls a pending env still shows its terminal world (state records against the oracle's, which resets
+    only at the next call); a masked zs_reset of pending and running envs alike resets each once (the
+    oracle's env.reset() draws) and takes the pending ones off the list, and the unmasked pending envs
+    still autoreset at the next step."""
+    import torch
+    from libzombsole_amd.engine import Engine
+    from oracle.oracle import OracleEnv
+    monkeypatch.setenv("ZS_FUSED", fused)
+
+    def b(n):
+        return _abi.multi_env_config(n, "extermination", [], "bridge64", ["0", "1"], initial_zombies=10,
+                                     minimum_zombies=0, max_episode_steps=6)
+    n, steps = 256, 30
+    eng = Engine(b(n))
+    assert eng.describe()["reset_side_stream"] == (fused == "0")
+    kinds = [o[2] for o in eng.builder.map.obstacles]
+    eng.seed([700 + i for i in range(n)])
+    eng.reset()
+    refs = []
+    for k in range(n):
+        o = OracleEnv(b(1))
+        o.seed(700 + k)
+        o.reset()
+        refs.append(o)
+    need = [False] * n
+    masked_pending = 0
+    for t in range(1, steps + 1):
+        if t in (7, 9, 20):  # masked reset of every other env, pending ones included
+            mask = (torch.arange(n, device=eng.device) % 2 == 0).to(torch.uint8)
+            obs = eng.reset(mask).cpu().numpy()
+            for k in range(0, n, 2):
+                assert np.array_equal(obs[k], refs[k].reset()), ("masked reset obs", k, t)
+                masked_pending += need[k]
+                need[k] = False
+        eng.gen_actions(t, 7)
+        acts = eng.actions.cpu().numpy()
+        eng.step()
+        torch.cuda.synchronize()
+        obs = eng.obs.cpu().numpy()
+        rew = eng.rewards.cpu().numpy()
+        was_reset = eng.was_reset.cpu().numpy()
+        for k, o in enumerate(refs):
+            if need[k]:
+                assert was_reset[k], (k, t)
+                exp = o.reset()
+                need[k] = False
+            else:
+                assert not was_reset[k], (k, t)
+                exp, r, d, tr, lb = o.step(acts[k])
+                assert np.array_equal(rew[k][lb], r[:2][lb]), ("rew", k, t)
+                need[k] = d or tr
+            assert np.array_equal(obs[k], exp), ("obs", k, t)
+        for k in range(0, n, 17):  # pending envs included: the terminal world until the next call
+            assert eng.get_state(k).canonical(kinds) == refs[k].state(), ("state", k, t)
+    assert masked_pending > 0  # the masked resets met envs whose autoreset was pending
+    eng.close()

@@ -157,7 +157,7 @@ def test_set_state_refuses_pending_flag_change():
     eng.actions.copy_(torch.from_numpy(np.broadcast_to(FIXED, (4, 2, 3)).copy()))
     eng.step()  # every episode ends: all four envs are pending reset now
     st = eng.get_state(2)
-    assert int(st.buf[5]) == 1
+    assert int(st.buf[5]) in (1, 2)  # pending: rebuilt by the next call, or already into its shadow record
     before = st.buf.copy()
     st.buf[5] = 0
     st.buf[0] = 777
