@@ -323,17 +323,36 @@ def main():
     else:
         dom, dom_ms, dom_b = launch["obs_kernel"], obs_ms, obs_b
     achieved = dom_b * n_local / (dom_ms * 1e-3) / 1e9
+    # profiled workload key: the preset, or "n8" for C3's 8 192-env shard (the 8-GPU headline's per-GPU run)
+    wkey = "n8" if (args.config == "c3" and n_local == 8192) else args.config
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc):
         try:
             with open(pmc) as f:
-                wl = json.load(f).get("workloads", {}).get(args.config)
+                wls = json.load(f).get("workloads", {})
+            wl = wls.get(wkey) or wls.get(args.config)
             # profiled bytes per launch, scaled to this run's envs per GPU (per-env work is fixed)
             t = wl["kernels"].get(dom, {}).get("hbm_bytes_per_launch") if wl else None
             traffic = t * n_local / wl["envs_per_gpu"] if t is not None else None
         except Exception:
             traffic = None
+    # issue figures of the dominant and the step kernel from the SQ / GRBM counter passes (SURVEY.md §8(d):
+    # the path is latency / issue bound; tools/pmc_sq.py defines them)
+    issue = None
+    sqp = os.path.join(ROOT, "profiles", "pmc_sq.json")
+    if os.path.exists(sqp):
+        try:
+            with open(sqp) as f:
+                wl = json.load(f).get("workloads", {}).get(wkey)
+            if wl:
+                keep = ("valu_busy", "waves_per_cu", "wait_frac", "stall_frac", "active_frac", "valu_per_wave")
+                issue = {"profile": wl["profile"], "source": "profiles/pmc_sq.json"}
+                for k in {dom, step_name, launch["obs_kernel"]}:
+                    if k in wl["kernels"]:
+                        issue[k] = {n: round(v, 4) for n, v in wl["kernels"][k].items() if n in keep}
+        except Exception:
+            issue = None
     out = {
         "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True,
@@ -365,7 +384,8 @@ def main():
                      "step_launch_ms": tick_ms, "k_obs_ms": obs_ms,
                      "k_reset_ms": reset_ms, "k_respawn_ms": prof["respawn_ms"] / prof_steps,
                      "step_launch_writes_obs": bool(fobs),
-                     "step_launch_resets": bool(fused)},
+                     "step_launch_resets": bool(fused),
+                     "issue": issue},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

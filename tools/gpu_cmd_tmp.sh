@@ -1,1 +1,6 @@
-bash tools/sweep.sh 'c3g256;ZS_RESET_GRID=256;--config c3' 'c3g512;ZS_RESET_GRID=512;--config c3' 'c3g128;ZS_RESET_GRID=128;--config c3' 'c3d0;ZS_DEFER_RESET=0;--config c3' 'c5g256;ZS_RESET_GRID=256;--config c5' 'c5d0;ZS_DEFER_RESET=0;--config c5' 'c4g256;ZS_RESET_GRID=256;--config c4' 'c4d0;ZS_DEFER_RESET=0;--config c4'
+cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
+for cfg in "c3:--config c3:k_gen_actions_ctr" "n8:--envs 8192:k_step" "c5:--config c5:k_gen_actions_ctr"; do n=${cfg%%:*}; r=${cfg#*:}; a=${r%%:*}; k=${r#*:}
+timeout -k 10 300 rocprofv3 --kernel-trace -T --output-format csv -d $PWD/gpurun_out/trace_$n -o run -- python3 bench.py $a --steps 60 --warmup 10 --no-cpu-baseline > gpurun_out/trace_$n.log 2>&1 || exit 1
+python3 tools/trace_steps.py gpurun_out/trace_$n $k 30 > gpurun_out/trace_$n.txt 2>&1
+done
+tail -12 gpurun_out/trace_*.txt
