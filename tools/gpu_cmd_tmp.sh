@@ -1,6 +1,16 @@
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
-for cfg in "c3:--config c3:k_gen_actions_ctr" "n8:--envs 8192:k_step" "c5:--config c5:k_gen_actions_ctr"; do n=${cfg%%:*}; r=${cfg#*:}; a=${r%%:*}; k=${r#*:}
-timeout -k 10 300 rocprofv3 --kernel-trace -T --output-format csv -d $PWD/gpurun_out/trace_$n -o run -- python3 bench.py $a --steps 60 --warmup 10 --no-cpu-baseline > gpurun_out/trace_$n.log 2>&1 || exit 1
-python3 tools/trace_steps.py gpurun_out/trace_$n $k 30 > gpurun_out/trace_$n.txt 2>&1
+for c in FETCH_SIZE WRITE_SIZE; do
+timeout -s KILL 120 rocprofv3 --pmc $c -T --output-format csv -d $PWD/gpurun_out/tickio_$c -o run -- ./tools/probe/tickio > gpurun_out/tickio_$c.log 2>&1 || exit 1
 done
-tail -12 gpurun_out/trace_*.txt
+python3 - <<'PY'
+import csv, glob
+for c in ("FETCH_SIZE", "WRITE_SIZE"):
+    vals = {}
+    for f in glob.glob("gpurun_out/tickio_%s/**/*counter_collection.csv" % c, recursive=True):
+        for row in csv.DictReader(open(f)):
+            if "k_tick_io" in row["Kernel_Name"]:
+                vals.setdefault(row["Dispatch_Id"], 0.0)
+                vals[row["Dispatch_Id"]] += float(row["Counter_Value"])
+    print(c, [round(v) for k, v in sorted(vals.items(), key=lambda kv: int(kv[0]))])
+PY
+head -3 gpurun_out/tickio_FETCH_SIZE.log | tail -1; grep "k_tick_io read" gpurun_out/tickio_*.log
