@@ -28,7 +28,7 @@
 // An env is either pending (reset work only; the tick reports it as reset without touching its
 // state) or stepping (tick only), so the two roles never share an env.
 template <int G>
-__global__ void __launch_bounds__(64, ZS_STEP_WAVES) k_step(Dev d, int n_reset, const int32_t* actions, double* rew,
+__global__ void __launch_bounds__(64, ZS_FUSED_WAVES) k_step(Dev d, int n_reset, const int32_t* actions, double* rew,
                                              uint8_t* done_out, uint8_t* trunc_out, uint8_t* listed_out,
                                              uint8_t* reset_out, int* reset_list, int* reset_count,
                                              const int* cur_list, const int* cur_count, int* err_out, void* obs_out) {
@@ -412,7 +412,8 @@ static int choose_layout(zs_handle* h, int want_g, bool fused, int obs_bytes) {
     // the latency of one workgroup.  Measured on one MI355X: G = 8 beats 16 when G = 16 needs more
     // than two rounds (C3, 65536 envs, E = 12: 121 vs 140 us), G = 16 beats 8 at 8192 and 16384 envs
     // and at C5 (E = 24); G = 32 beats 16 at C4 (E = 54: the decisions spread over more lanes).
-    const int wave_cap = 4 * ZS_STEP_WAVES;  // one-wave workgroups per CU the register budget admits
+    // one-wave workgroups per CU the register budget admits (k_step's or k_tick's)
+    const int wave_cap = 4 * (fused ? ZS_FUSED_WAVES : ZS_STEP_WAVES);
     int g0 = want_g > 0 ? want_g : (d.E > 32 ? 32 : 16);
     if (want_g <= 0 && d.E <= 16 && (long)d.N > 2L * wave_cap * 256 * (64 / 16)) g0 = 8;
     int cand_full = (d.W * d.H <= 65535) ? d.ncand : 0;

@@ -26,6 +26,16 @@
 #ifndef ZS_STEP_WAVES
 #define ZS_STEP_WAVES 6
 #endif
+// The fused step launch (k_step) is chosen only when the whole launch is resident at once (at most
+// 4 * ZS_FUSED_WAVES one-wave workgroups per CU), and k_reset runs a few waves per CU beside the tick
+// (3.8 measured at C3): neither needs k_tick's occupancy, and at 6 waves both spill (k_step 244,
+// k_reset 292 bytes of scratch per lane, on their serial chains).  3 waves: 147 / 151 VGPRs, none.
+#ifndef ZS_FUSED_WAVES
+#define ZS_FUSED_WAVES 3
+#endif
+#ifndef ZS_RESET_WAVES
+#define ZS_RESET_WAVES 3
+#endif
 
 #define ZS_MT_N 624
 #define ZS_MT_M 397

@@ -292,7 +292,7 @@ __device__ __forceinline__ void reset_role(const Dev& d, int list_mode, const in
     }
 }
 
-__global__ void __launch_bounds__(64, ZS_STEP_WAVES) k_reset(Dev d, int list_mode, const int* list, const int* count,
+__global__ void __launch_bounds__(64, ZS_RESET_WAVES) k_reset(Dev d, int list_mode, const int* list, const int* count,
                                               const uint8_t* mask, int* err_out, void* obs_out) {
     reset_role(d, list_mode, list, count, mask, err_out, blockIdx.x, gridDim.x, obs_out);
 }
