@@ -248,6 +248,9 @@ int zs_debug_lists(zs_handle* h, int32_t out[4], void* stream);
 /* Diagnostic builds compiled with -DZS_STAMPS only (the product .so returns ZS_ESTATE):
  * per-phase k_tick cycle sums / maxima over all workgroup launches since the last call. */
 int zs_debug_stamps(zs_handle* h, uint64_t* sum_out, uint64_t* max_out, int32_t n);
+/* Diagnostic builds only: out[2w], out[2w + 1] = start / end s_memrealtime (100 MHz) of workgroup w
+ * of the last fused step launch (k_step), w < n. */
+int zs_debug_timeline(zs_handle* h, uint64_t* out, int32_t n);
 
 /* Flat state record, int32 words:
  *   [0]  t (World.t)          [1] deaths            [2] zombie_deaths

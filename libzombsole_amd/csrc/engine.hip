@@ -32,11 +32,13 @@ __global__ void __launch_bounds__(64, ZS_FUSED_WAVES) k_step(Dev d, int n_reset,
                                              uint8_t* done_out, uint8_t* trunc_out, uint8_t* listed_out,
                                              uint8_t* reset_out, int* reset_list, int* reset_count,
                                              const int* cur_list, const int* cur_count, int* err_out, void* obs_out) {
+    TL(0);
     if ((int)blockIdx.x < n_reset)
         reset_role(d, 1, cur_list, cur_count, nullptr, err_out, blockIdx.x, n_reset, d.fobs ? obs_out : nullptr);
     else
         tick_wg<G>(d, xcd_remap(blockIdx.x - n_reset, gridDim.x - n_reset), actions, rew, done_out, trunc_out,
                    listed_out, reset_out, reset_list, reset_count, obs_out, 0, d.N);
+    TL(1);
 }
 
 // ---------------------------------------------------------------------------
@@ -1408,6 +1410,20 @@ extern "C" int zs_debug_lists(zs_handle* h, int32_t* out, void* stream) {
 // ---------------------------------------------------------------------------
 // diagnostic build (-DZS_STAMPS): per-phase k_tick cycle sums since the last read
 // ---------------------------------------------------------------------------
+// diagnostic build (-DZS_STAMPS): start / end s_memrealtime of the first n workgroups of the last step launch
+extern "C" int zs_debug_timeline(zs_handle* h, uint64_t* out, int32_t n) {
+#ifdef ZS_STAMPS
+    if (!h || !out || n < 0 || n > ZS_STAMP_WGS) return fail(ZS_EINVAL, "bad argument");
+    HIPCHK(hipSetDevice(h->device));
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamp_tl), (size_t)n * 2 * sizeof(unsigned long long)));
+    return ZS_OK;
+#else
+    (void)h; (void)out; (void)n;
+    return fail(ZS_ESTATE, "not a ZS_STAMPS diagnostic build");
+#endif
+}
+
 extern "C" int zs_debug_stamps(zs_handle* h, uint64_t* sum_out, uint64_t* max_out, int32_t n) {
 #ifdef ZS_STAMPS
     if (!h || !sum_out || n > ZS_NPHASE) return fail(ZS_EINVAL, "bad argument");

@@ -42,6 +42,30 @@ __device__ __forceinline__ int xcd_remap(int b, int nb) {
     return x * q + (x < r ? x : r) + k;
 }
 
+// Units (envs, or env pairs) of a persistent store-stream kernel dealt so that the chip writes a
+// narrow address range at a time: XCD x (workgroups b = x mod 8) owns a contiguous region of the
+// units, in proportion to its workgroups; round k of the XCD's gx workgroups covers gx * W consecutive
+// units of it, W consecutive ones per workgroup (one per writer wave).  Measured with
+// tools/probe/storeceil.hip: whole 21 168-B blocks per wave, consecutive waves of an XCD on consecutive
+// blocks ("xcd waveenv") 5.78 TB/s; one block per wave strided over the chip ("chunk 21168") 5.06.
+#ifndef ZS_RING_DEAL
+#define ZS_RING_DEAL 1
+#endif
+struct XcdDeal {
+    int base, span, off, w, ucount;
+    __device__ XcdDeal(int b, int nb, int n_units, int W) : w(W) {
+        const int q = nb >> 3, r = nb & 7, x = b & 7, j = b >> 3;
+        const int gs = x * q + (x < r ? x : r), gx = q + (x < r);  // XCD x: workgroups [gs, gs + gx)
+        const int r0 = (int)((long long)n_units * gs / nb), r1 = (int)((long long)n_units * (gs + gx) / nb);
+        base = r0;
+        span = gx * W;
+        off = j * W;
+        const int m = r1 - r0 - off;
+        ucount = m <= 0 ? 0 : (m / span) * W + min(m % span, W);
+    }
+    __device__ int unit(int u) const { return base + (u / w) * span + off + u % w; }
+};
+
 __device__ __forceinline__ int floordiv100_i32(int a) {  // Python a // 100
     int q = a / 100;
     if (q * 100 != a && a < 0) q -= 1;
@@ -483,7 +507,7 @@ __device__ __forceinline__ zs_v2u obs_dirty(const Dev& d, int e) { return zs_v2u
 // dirty = obs_dirty(d, e), loaded by an earlier prefetch (its `ahead` env): an obstacle of a clean HP
 // chunk reads hp_init instead of the env's row, a clean dead-body chunk reads dead_zero, and the address
 // selects wait on nothing in flight.
-__device__ __forceinline__ void obs_prefetch(const Dev& d, int e, int ahead, zs_v2u dirty, ObsPrefetch& f) {
+__device__ __forceinline__ void obs_prefetch_env(const Dev& d, int e, zs_v2u dirty, ObsPrefetch& f) {
     const int lane = threadIdx.x & 63, N = d.N;
     const int s = lane < d.E ? lane : d.E - 1;
 #ifndef ZS_OBS_DIAG
@@ -507,6 +531,9 @@ __device__ __forceinline__ void obs_prefetch(const Dev& d, int e, int ahead, zs_
         const int o = min(lane + 64 * i, d.O - 1);
         f.hp[i] = (((dirty.x >> (o / d.hp_chunk)) & 1u) ? hr : d.hp_init)[o];
     }
+}
+__device__ __forceinline__ void obs_prefetch(const Dev& d, int e, int ahead, zs_v2u dirty, ObsPrefetch& f) {
+    obs_prefetch_env(d, e, dirty, f);
     f.dirty_ahead = obs_dirty(d, ahead);
 }
 
@@ -912,6 +939,9 @@ __global__ void __launch_bounds__(256, ZS_OBS_PIPE_WAVES) k_obs_lds(Dev d, T* ou
 #ifndef RING_THR
 #define RING_THR 16
 #endif
+#ifndef ZS_RING_PF
+#define ZS_RING_PF 2  // encoder prefetch depth (items)
+#endif
 // Envs per ring unit: two when one env's block ends off a 16-B boundary and two end on one (C5's
 // int16 10 584-B envs): a unit is then one aligned, contiguous stream, with no partial 16-B chunk
 // shared by two writers.
@@ -957,12 +987,19 @@ __global__ void __launch_bounds__(64 * (RING_ENC + RING_WRT), 1) k_obs_ring(Dev 
     __syncthreads();
     // unit g covers envs env0 + PAIR * g + h (h < PAIR, below env1); this workgroup's units are
     // g_first, g_first + G, ...; its items (envs) t = PAIR * u + h, the last one possibly absent
-    const int G = gridDim.x;
-    const int g_first = xcd_remap(blockIdx.x, G), n_units = (env1 - env0 + PAIR - 1) / PAIR;
+    const int G = gridDim.x, n_units = (env1 - env0 + PAIR - 1) / PAIR;
+#if ZS_RING_DEAL
+    const XcdDeal deal(blockIdx.x, G, n_units, RING_WRT);
+    const int ucount = deal.ucount;
+    auto unit_of = [&](int u) { return deal.unit(u); };
+#else
+    const int g_first = xcd_remap(blockIdx.x, G);
     const int ucount = g_first < n_units ? (n_units - g_first + G - 1) / G : 0;
-    const int count = ucount ? min(PAIR * ucount, env1 - env0 - PAIR * (g_first + (ucount - 1) * G) + PAIR * (ucount - 1))
-                             : 0;
-    auto unit_env = [&](int u) { return env0 + PAIR * (g_first + u * G); };
+    auto unit_of = [&](int u) { return g_first + u * G; };
+#endif
+    // items in the last unit: PAIR, or fewer for the run's last unit
+    const int count = ucount ? PAIR * (ucount - 1) + min(PAIR, env1 - env0 - PAIR * unit_of(ucount - 1)) : 0;
+    auto unit_env = [&](int u) { return env0 + PAIR * unit_of(u); };
     if (wave >= RING_ENC) {  // writer
         for (int u = wave - RING_ENC; u < ucount; u += RING_WRT) {
             const int q = u % US, e = unit_env(u);
@@ -984,14 +1021,20 @@ __global__ void __launch_bounds__(64 * (RING_ENC + RING_WRT), 1) k_obs_ring(Dev 
     auto item_env = [&](int t) { return unit_env(t / PAIR) + t % PAIR; };
     int t = wave;
     if (t >= count) return;
-    ObsPrefetch f;
-    obs_prefetch(d, item_env(t), t + RING_ENC < count ? item_env(t + RING_ENC) : item_env(t), obs_dirty(d, item_env(t)), f);
-    for (; t < count; t += RING_ENC) {
+    // encode item t: its image from f, then (before any LDS work) the loads of the item `ahead`
+    // iterations later into f, with that item's dirty masks dq (loaded two iterations earlier), and
+    // dq reloaded for the item two iterations after that
+    auto encode = [&](int t, ObsPrefetch& f, zs_v2u& dq, int ahead) {
         const int u = t / PAIR, h = t % PAIR, e = item_env(t);
         obs_build_compact(d, L, img, f, code_s, lane);
-        if (t + RING_ENC < count) {
-            const int en = item_env(t + RING_ENC);
-            obs_prefetch(d, en, t + 2 * RING_ENC < count ? item_env(t + 2 * RING_ENC) : en, f.dirty_ahead, f);
+        const int tn = t + ahead * RING_ENC, tq = t + (ahead + 2) * RING_ENC;
+        if (ahead == 1) {
+            if (tn < count) obs_prefetch(d, item_env(tn), tn + RING_ENC < count ? item_env(tn + RING_ENC) : item_env(tn), f.dirty_ahead, f);
+        } else {
+            // every load unconditional (an item past the wave's last reads the wave's first env again),
+            // so the waits for the older prefetch count the younger one's loads exactly
+            obs_prefetch_env(d, item_env(tn < count ? tn : wave), dq, f);
+            dq = obs_dirty(d, item_env(tq < count ? tq : wave));
         }
         wave_sync();
         obs_window_compact<NOBS>(d, L, img, lane);
@@ -1007,5 +1050,25 @@ __global__ void __launch_bounds__(64 * (RING_ENC + RING_WRT), 1) k_obs_ring(Dev 
             obs_encode_block<S>(d, L, st4, img, wm, ox, oy, ot0 + a * 3 * PLANE, lane);
         }
         ring_state_store(&state[PAIR * q + h], 2 * u + 1);
+    };
+    auto envc = [&](int tt) { return item_env(tt < count ? tt : wave); };
+#if ZS_RING_PF == 2
+    // two items of register prefetch: a load round trip under the saturated store stream outlasts the
+    // encoding of one env
+    ObsPrefetch fa, fb;
+    zs_v2u qa, qb;
+    obs_prefetch_env(d, envc(t), obs_dirty(d, envc(t)), fa);
+    obs_prefetch_env(d, envc(t + RING_ENC), obs_dirty(d, envc(t + RING_ENC)), fb);
+    qa = obs_dirty(d, envc(t + 2 * RING_ENC));
+    qb = obs_dirty(d, envc(t + 3 * RING_ENC));
+    for (; t < count; t += 2 * RING_ENC) {
+        encode(t, fa, qa, 2);
+        if (t + RING_ENC < count) encode(t + RING_ENC, fb, qb, 2);
     }
+#else
+    ObsPrefetch f;
+    zs_v2u q0 = {0u, 0u};
+    obs_prefetch(d, envc(t), envc(t + RING_ENC), obs_dirty(d, envc(t)), f);
+    for (; t < count; t += RING_ENC) encode(t, f, q0, 1);
+#endif
 }

@@ -57,7 +57,17 @@ __device__ unsigned long long g_stamp_wg[ZS_STAMP_WGS * ZS_NPHASE];
             g_stamp_wg[blockIdx.x * ZS_NPHASE + 12 + (k)-1] += _t - _r_prev;              \
         _r_prev = _t;                                                                     \
     } while (0)
+// workgroup timeline of the last launch: s_memrealtime (100 MHz, one clock for the whole chip) at
+// the workgroup's start and end, g_stamp_tl[block][0 / 1]
+__device__ unsigned long long g_stamp_tl[ZS_STAMP_WGS * 2];
+#define TL(k)                                                                             \
+    do {                                                                                  \
+        unsigned long long _t;                                                            \
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");  \
+        if (threadIdx.x == 0 && blockIdx.x < ZS_STAMP_WGS) g_stamp_tl[blockIdx.x * 2 + (k)] = _t; \
+    } while (0)
 #else
+#define TL(k)
 #define STAMP_DECL
 #define STAMP(k)
 #define SUB_DECL

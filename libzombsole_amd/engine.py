@@ -14,7 +14,7 @@ from . import _abi
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_build", "libzombsole_mi355x.so")
 SYMBOLS = ["zs_last_error", "zs_create", "zs_destroy", "zs_obs_shape", "zs_seed", "zs_reset", "zs_step", "zs_observe",
            "zs_gen_actions", "zs_step_graph", "zs_state_size", "zs_get_state", "zs_set_state", "zs_get_rng", "zs_set_rng", "zs_overflow", "zs_profile", "zs_profile_read", "zs_describe",
-           "zs_debug_stamps", "zs_debug_lists"]
+           "zs_debug_stamps", "zs_debug_timeline", "zs_debug_lists"]
 
 _lib = None
 
@@ -59,12 +59,14 @@ def load_library(path=None):
     L.zs_debug_stamps.argtypes = [vp, vp, vp, i32]
     L.zs_describe.argtypes = [vp, C.c_char_p, i32]
     # an older build selected by ZS_ENGINE_LIB for an A/B (tools/ab.sh) may lack newer entry points
-    optional = {"zs_debug_lists", "zs_overflow"} if os.environ.get("ZS_ENGINE_LIB") and path is None else set()
+    optional = {"zs_debug_lists", "zs_overflow", "zs_debug_timeline"} if os.environ.get("ZS_ENGINE_LIB") and path is None else set()
     for s in SYMBOLS:
         if s in optional and not hasattr(L, s):
             continue
         if s == "zs_debug_lists":
             L.zs_debug_lists.argtypes = [vp, C.POINTER(i32), vp]
+        if s == "zs_debug_timeline":
+            L.zs_debug_timeline.argtypes = [vp, vp, i32]
         if s != "zs_last_error":
             getattr(L, s).restype = C.c_int
     if path is None:
@@ -223,6 +225,15 @@ class Engine(object):
         if rc:
             _raise(self.L, rc, "zs_debug_stamps")
         return ssum, smax
+
+    def debug_timeline(self, n):
+        """Start / end s_memrealtime (100 MHz) of the first n workgroups of the last fused step launch,
+        shape [n, 2] (diagnostic -DZS_STAMPS build only)."""
+        out = np.zeros((n, 2), dtype=np.uint64)
+        rc = self.L.zs_debug_timeline(self.h, C.c_void_p(out.ctypes.data), n)
+        if rc:
+            _raise(self.L, rc, "zs_debug_timeline")
+        return out
 
     def debug_lists(self):
         """(pending-reset count of list 0, of list 1, deferred-respawn count, parity drained next)."""

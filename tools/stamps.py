@@ -62,6 +62,25 @@ def main():
                 print("   %-10s per-reset %9.0f cyc" % (name, ssum[k] / max(1, nres)))
             else:
                 print("   %-10s mean %9.0f cyc   max %9d cyc" % (name, ssum[k] / (wgs * steps), smax[k]))
+        desc = eng.describe()
+        if desc.get("step_kernel") == "k_step":
+            # workgroup timeline of one more fused step launch (s_memrealtime, 10 ns)
+            import numpy as np
+            n_reset = min(n_envs, int(os.environ.get("ZS_RESET_WGS", "256")))
+            eng.gen_actions(31 + steps, 7)
+            eng.step()
+            torch.cuda.synchronize()
+            tl = eng.debug_timeline(n_reset + wgs).astype(np.int64)
+            t0 = tl[:, 0].min()
+            st, en = (tl[:, 0] - t0) / 100.0, (tl[:, 1] - t0) / 100.0  # us
+            dur = en - st
+            q = lambda a: " ".join("p%d %.1f" % (p, np.percentile(a, p)) for p in (10, 50, 90, 99, 100))
+            print("   timeline (us from the first workgroup start): launch span %.1f" % en.max())
+            print("     tick wg start  %s" % q(st[n_reset:]))
+            print("     tick wg end    %s" % q(en[n_reset:]))
+            print("     tick wg life   %s" % q(dur[n_reset:]))
+            if n_reset:
+                print("     reset wg end   %s" % q(en[:n_reset]))
         eng.close()
 
 
