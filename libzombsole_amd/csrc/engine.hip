@@ -245,6 +245,7 @@ struct zs_handle {
     int device;
     Dev d;
     int G;          // lanes per env in k_tick
+    int tick_waves = ZS_STEP_WAVES;  // k_tick's register budget (waves per SIMD it is compiled for)
     size_t lds;     // k_tick dynamic LDS bytes
     ObsLayout obs_l;  // k_obs per-wave LDS image
     int obs_wpg;      // k_obs waves (envs) per workgroup
@@ -753,7 +754,22 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
         TRY(choose_layout(h, cfg->lanes_per_env, true, obs_b));
         const char* fz = getenv("ZS_FUSED");
         h->fused = fz ? atoi(fz) != 0 : h->resident >= h->want;
-        if (!h->fused) TRY(choose_layout(h, cfg->lanes_per_env, false, obs_b));
+        if (!h->fused) {
+            TRY(choose_layout(h, cfg->lanes_per_env, false, obs_b));
+            // k_tick's register budget: 5 waves per SIMD (96 VGPRs, 20 B of scratch per lane) unless 6 (80
+            // VGPRs, 52 B of scratch on the leader's paths) saves a round of resident workgroups.  Measured
+            // on one MI355X: C3 tick 95.6 -> 91.9 us and C4 185 -> 179 us at 5; C5 (16 384 workgroups:
+            // 2.7 rounds at 6 waves, 3.2 at 5) 167 -> 178 us.  ZS_TICK_WAVES=5/6 forces either.
+            const int wgs = (d.N + 64 / h->G - 1) / (64 / h->G);
+            const int lres = std::max(1, 160 * 1024 / (int)h->lds);
+            auto rounds = [&](int w) {
+                const int r = std::min(lres, 4 * w);
+                return (wgs + 256 * r - 1) / (256 * r);
+            };
+            h->tick_waves = rounds(5) <= rounds(6) ? 5 : 6;
+            if (getenv("ZS_TICK_WAVES") && atoi(getenv("ZS_TICK_WAVES")) > 0) h->tick_waves = atoi(getenv("ZS_TICK_WAVES")) == 5 ? 5 : 6;
+            h->resident = std::min(h->resident, 4 * h->tick_waves);
+        }
         // the reset launch stages the static spawn lists whenever they fit (no serial global loads in
         // its candidate filters); a fused launch shares the tick's choice
         d.rlists_cap = d.lists_cap;
@@ -968,8 +984,11 @@ static int launch_tick(zs_handle* h, const int32_t* actions, double* rew, uint8_
         hipLaunchKernelGGL(k_step<GG>, dim3(grid + n_reset), dim3(64), h->lds, s, d, n_reset, actions, rew, done,    \
                            trunc, listed, reset_out, rlist, rcount, (const int*)h->d_rlist[p],                        \
                            (const int*)(h->d_rcount + p), h->d_err, obs);                                             \
+    else if (h->tick_waves == 5)                                                                                      \
+        hipLaunchKernelGGL((k_tick<GG, 5>), dim3(grid), dim3(64), h->lds, s, d, actions, rew, done, trunc, listed,   \
+                           reset_out, rlist, rcount, obs, env0, env1);                                                \
     else                                                                                                              \
-        hipLaunchKernelGGL(k_tick<GG>, dim3(grid), dim3(64), h->lds, s, d, actions, rew, done, trunc, listed,        \
+        hipLaunchKernelGGL((k_tick<GG, 6>), dim3(grid), dim3(64), h->lds, s, d, actions, rew, done, trunc, listed,   \
                            reset_out, rlist, rcount, obs, env0, env1)
     switch (h->G) {
     case 1: ZS_TICK(1); break;
@@ -1383,9 +1402,9 @@ extern "C" int zs_describe(zs_handle* h, char* buf, int32_t len) {
     snprintf(buf, (size_t)len,
              "{\"envs\": %d, \"entities\": %d, \"lanes_per_env\": %d, \"step_kernel\": \"%s\", \"step_lds\": %zu, "
              "\"step_wgs_per_cu\": %d, \"rng_window\": %d, \"obs_kernel\": \"%s\", \"reset_side_stream\": %d, "
-             "\"reset_lds\": %zu, \"respawn\": \"%s\"}",
+             "\"reset_lds\": %zu, \"respawn\": \"%s\", \"tick_waves\": %d}",
              d.N, d.E, h->G, h->fused ? "k_step" : "k_tick", h->lds, h->resident, d.rw_cap, obs_kernel, h->reset_side,
-             h->reset_lds, d.defer_respawn ? "k_respawn" : "tick");
+             h->reset_lds, d.defer_respawn ? "k_respawn" : "tick", h->fused ? ZS_FUSED_WAVES : h->tick_waves);
     return ZS_OK;
 }
 

@@ -48,6 +48,14 @@ __device__ unsigned long long g_stamp_wg[ZS_STAMP_WGS * ZS_NPHASE];
             g_stamp_wg[blockIdx.x * ZS_NPHASE + 6 + (k)-1] += _t - _sub_prev;             \
         _sub_prev = _t;                                                                   \
     } while (0)
+// stage-in splits: SX(1) after the first load round, SX(2) after the RNG window (slots 10, 11)
+#define SX(k)                                                                             \
+    do {                                                                                  \
+        unsigned long long _t;                                                            \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");      \
+        if (threadIdx.x == 0 && blockIdx.x < ZS_STAMP_WGS)                                \
+            g_stamp_wg[blockIdx.x * ZS_NPHASE + 9 + (k)] += _t - _st_prev;                \
+    } while (0)
 #define RST_DECL unsigned long long _r_prev;
 #define RST(k)                                                                            \
     do {                                                                                  \
@@ -68,6 +76,7 @@ __device__ unsigned long long g_stamp_tl[ZS_STAMP_WGS * 2];
     } while (0)
 #else
 #define TL(k)
+#define SX(k)
 #define STAMP_DECL
 #define STAMP(k)
 #define SUB_DECL
@@ -1138,6 +1147,7 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
 #pragma unroll
         for (int u = 0; u < 8; u++)
             if (j + u * G < d.DW) c.bm[IX(c, j + u * G)] = bmv[u];
+        SX(1);
         // the rest of the entity table (E > 4G) (SoA [slot][N]: this env's column)
         {
             auto ix = [&](int s) { return IX(c, s); };
@@ -1208,6 +1218,7 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
                 if (b + u * G < wlen) c.rw[IX(c, b + u * G)] = mt_temper(v[u]);
         }
         st0 = st_pack(off, slot, ready);
+        SX(2);
     }
     wave_sync();
     if (stepping) {
@@ -1379,8 +1390,8 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
     STAMP(6);
 }
 
-template <int G>
-__global__ void __launch_bounds__(64, ZS_STEP_WAVES) k_tick(Dev d, const int32_t* actions, double* rew, uint8_t* done_out,
+template <int G, int W = ZS_STEP_WAVES>
+__global__ void __launch_bounds__(64, W) k_tick(Dev d, const int32_t* actions, double* rew, uint8_t* done_out,
                                              uint8_t* trunc_out, uint8_t* listed_out, uint8_t* reset_out,
                                              int* reset_list, int* reset_count, void* obs_out, int env0, int env1) {
     tick_wg<G>(d, xcd_remap(blockIdx.x, gridDim.x), actions, rew, done_out, trunc_out, listed_out, reset_out, reset_list,

@@ -6,6 +6,7 @@
 //   hipcc --offload-arch=gfx950 -O3 -o envstore tools/probe/envstore.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
+#include <cstdlib>
 
 #define CHK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); return 1; } } while (0)
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
@@ -87,39 +88,78 @@ __global__ void __launch_bounds__(64 * NW) k_pair(v4u* o, int n) {
     }
 }
 
-int main() {
+int main(int argc, char** argv) {
     const int n = 65536;
     const size_t bytes = (size_t)n * 21168;
-    v4u* d;
-    CHK(hipMalloc(&d, bytes + 4096));
     hipEvent_t a, b;
     CHK(hipEventCreate(&a));
     CHK(hipEventCreate(&b));
-    auto run = [&](const char* name, int grid, auto launch) -> int {
+    auto run = [&](const char* name, v4u* d, int grid, auto launch) -> int {
         for (int rep = 0; rep < 2; rep++) {
             CHK(hipEventRecord(a));
-            for (int it = 0; it < 20; it++) launch(grid);
+            for (int it = 0; it < 20; it++) launch(d, grid);
             CHK(hipGetLastError());
             CHK(hipEventRecord(b));
             CHK(hipEventSynchronize(b));
             float ms;
             CHK(hipEventElapsedTime(&ms, a, b));
-            if (rep) printf("%-26s grid %5d %8.1f us/pass  %6.2f TB/s\n", name, grid, ms * 1e3 / 20, bytes / (ms / 20 * 1e-3) / 1e12);
+            if (rep) printf("%-26s %p grid %5d %8.1f us/pass  %6.2f TB/s\n", name, (void*)d, grid, ms * 1e3 / 20, bytes / (ms / 20 * 1e-3) / 1e12);
         }
         return 0;
     };
+    if (argc > 1) {
+        // placement: the same pattern into several separately allocated buffers
+        // argv[2]: 0 hipMalloc, 1 hipExtMallocWithFlags(hipDeviceMallocContiguous), 2 VMM (hipMemCreate of
+        // the whole size, mapped at a reserved range), 3 hipMalloc of 4 GiB
+        const int nb = atoi(argv[1]), mode = argc > 2 ? atoi(argv[2]) : 0;
+        v4u* bufs[16];
+        for (int i = 0; i < nb && i < 16; i++) {
+            if (mode == 1) {
+                CHK(hipExtMallocWithFlags((void**)&bufs[i], bytes + 4096, hipDeviceMallocContiguous));
+            } else if (mode == 2) {
+                hipMemAllocationProp prop = {};
+                prop.type = hipMemAllocationTypePinned;
+                prop.location.type = hipMemLocationTypeDevice;
+                prop.location.id = 0;
+                size_t gran = 0;
+                CHK(hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended));
+                const size_t sz = (bytes + 4096 + gran - 1) / gran * gran;
+                if (i == 0) printf("VMM granularity %zu\n", gran);
+                hipMemGenericAllocationHandle_t hdl;
+                void* va = nullptr;
+                CHK(hipMemAddressReserve(&va, sz, 0, nullptr, 0));
+                CHK(hipMemCreate(&hdl, sz, &prop, 0));
+                CHK(hipMemMap(va, sz, 0, hdl, 0));
+                hipMemAccessDesc acc = {};
+                acc.location = prop.location;
+                acc.flags = hipMemAccessFlagsProtReadWrite;
+                CHK(hipMemSetAccess(va, sz, &acc, 1));
+                bufs[i] = (v4u*)va;
+            } else if (mode == 3) {
+                CHK(hipMalloc(&bufs[i], 4ull << 30));
+            } else {
+                CHK(hipMalloc(&bufs[i], bytes + 4096));
+            }
+            CHK(hipMemset(bufs[i], 0, bytes));
+        }
+        for (int i = 0; i < nb && i < 16; i++) {
+            run("own 4 waves xcd", bufs[i], 256, [&](v4u* d, int gr) { hipLaunchKernelGGL((k_own<4, 1>), dim3(gr), dim3(256), 0, 0, d, n); });
+            run("flat4k-like coop quarters", bufs[i], 256, [&](v4u* d, int gr) { hipLaunchKernelGGL((k_coop<4, 1>), dim3(gr), dim3(256), 0, 0, d, n); });
+        }
+        return 0;
+    }
+    v4u* d;
+    CHK(hipMalloc(&d, bytes + 4096));
     for (int g : {256, 512}) {
-        run("own 1 wave  chip", g, [&](int gr) { hipLaunchKernelGGL((k_own<1, 0>), dim3(gr), dim3(64), 0, 0, d, n); });
-        run("own 1 wave  xcd", g, [&](int gr) { hipLaunchKernelGGL((k_own<1, 1>), dim3(gr), dim3(64), 0, 0, d, n); });
-        run("own 2 waves xcd", g, [&](int gr) { hipLaunchKernelGGL((k_own<2, 1>), dim3(gr), dim3(128), 0, 0, d, n); });
-        run("own 4 waves chip", g, [&](int gr) { hipLaunchKernelGGL((k_own<4, 0>), dim3(gr), dim3(256), 0, 0, d, n); });
-        run("own 4 waves xcd", g, [&](int gr) { hipLaunchKernelGGL((k_own<4, 1>), dim3(gr), dim3(256), 0, 0, d, n); });
-        run("own 8 waves xcd", g, [&](int gr) { hipLaunchKernelGGL((k_own<8, 1>), dim3(gr), dim3(512), 0, 0, d, n); });
-        run("coop 4 rr1k", g, [&](int gr) { hipLaunchKernelGGL((k_coop<4, 0>), dim3(gr), dim3(256), 0, 0, d, n); });
-        run("coop 4 quarters", g, [&](int gr) { hipLaunchKernelGGL((k_coop<4, 1>), dim3(gr), dim3(256), 0, 0, d, n); });
-        run("coop 8 rr1k", g, [&](int gr) { hipLaunchKernelGGL((k_coop<8, 0>), dim3(gr), dim3(512), 0, 0, d, n); });
-        run("coop 2 rr1k", g, [&](int gr) { hipLaunchKernelGGL((k_coop<2, 0>), dim3(gr), dim3(128), 0, 0, d, n); });
-        run("pair 4 rr1k", g, [&](int gr) { hipLaunchKernelGGL((k_pair<4>), dim3(gr), dim3(256), 0, 0, d, n); });
+        run("own 1 wave  chip", d, g, [&](v4u* d, int gr) { hipLaunchKernelGGL((k_own<1, 0>), dim3(gr), dim3(64), 0, 0, d, n); });
+        run("own 1 wave  xcd", d, g, [&](v4u* d, int gr) { hipLaunchKernelGGL((k_own<1, 1>), dim3(gr), dim3(64), 0, 0, d, n); });
+        run("own 2 waves xcd", d, g, [&](v4u* d, int gr) { hipLaunchKernelGGL((k_own<2, 1>), dim3(gr), dim3(128), 0, 0, d, n); });
+        run("own 4 waves chip", d, g, [&](v4u* d, int gr) { hipLaunchKernelGGL((k_own<4, 0>), dim3(gr), dim3(256), 0, 0, d, n); });
+        run("own 4 waves xcd", d, g, [&](v4u* d, int gr) { hipLaunchKernelGGL((k_own<4, 1>), dim3(gr), dim3(256), 0, 0, d, n); });
+        run("own 8 waves xcd", d, g, [&](v4u* d, int gr) { hipLaunchKernelGGL((k_own<8, 1>), dim3(gr), dim3(512), 0, 0, d, n); });
+        run("coop 4 rr1k", d, g, [&](v4u* d, int gr) { hipLaunchKernelGGL((k_coop<4, 0>), dim3(gr), dim3(256), 0, 0, d, n); });
+        run("coop 4 quarters", d, g, [&](v4u* d, int gr) { hipLaunchKernelGGL((k_coop<4, 1>), dim3(gr), dim3(256), 0, 0, d, n); });
+        run("pair 4 rr1k", d, g, [&](v4u* d, int gr) { hipLaunchKernelGGL((k_pair<4>), dim3(gr), dim3(256), 0, 0, d, n); });
     }
     return 0;
 }
