@@ -254,6 +254,9 @@ struct zs_handle {
     int obs_ring = 0;      // k_obs_ring: encoder and writer waves through an LDS ring (ZS_OBS_RING)
     size_t obs_ring_bytes = 0;
     size_t obs_lds_bytes = 0;
+    int obs_patch = 0;     // k_obs_lds's walk with the padded-table encoder (k_obs_patch, ZS_OBS_PATCH)
+    size_t obs_patch_bytes = 0;
+    int obs_patch_wgs = 2;  // its workgroups (PATCH_WPG waves) per CU
     int obs_gather = 0;    // else k_obs_gather<NOBS> usable (NOBS = 1, 2, 4), else 0 (k_obs)
     int obs_gather_stat = 0;    // k_obs_gather reads the static words from LDS tables (ZS_OBS_GATHER_STAT)
     ObsLayout obs_gl;      // its per-wave image
@@ -588,6 +591,43 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
     TRY(dupload(h, &p_aw, aw));
     TRY(dupload(h, &p_ac, ac));
     TRY(dupload(h, &p_bt, bt));
+    {
+        // k_obs_patch's tables (zs_obs.hpp): the map padded by half a registered window (21) on every
+        // side, each cell the code / life it shows with no thing on it, no body, every obstacle present
+        // at MAX_LIFE (out of bounds: Wall 200, gym/observation.py:69-76); per obstacle x | y << 12 |
+        // box << 24 | objective-under << 25
+        const int half = 10, pw = d.W + 2 * half, ph = d.H + 2 * half;
+        std::vector<uint16_t> pad((((size_t)pw * ph + 7) / 8) * 8, 0);
+        for (int y = -half; y < d.H + half; y++)
+            for (int x = -half; x < d.W + half; x++) {
+                uint16_t v = (uint16_t)(ZS_THING_WALL | (200 << 8));
+                if (x >= 0 && y >= 0 && x < d.W && y < d.H) {
+                    const int c = y * d.W + x;
+                    const bool obj = (objbits[c >> 5] >> (c & 31)) & 1u;
+                    const int oi = cellmap[c];
+                    if (oi >= 0)
+                        v = okind[oi] == ZS_THING_BOX ? (uint16_t)(ZS_THING_BOX | (10 << 8)) : (uint16_t)(ZS_THING_WALL | (200 << 8));
+                    else
+                        v = obj ? ZS_THING_OBJECTIVE : ZS_THING_NONE;
+                    if (oi >= 0 && obj) v |= OPAD_OBJ;
+                }
+                pad[(size_t)(y + half) * pw + x + half] = v;
+            }
+        std::vector<uint32_t> opk(std::max(d.O, 1), 0u);
+        for (int i = 0; i < d.O; i++) {
+            const int x = m.obstacle_xy[2 * i], y = m.obstacle_xy[2 * i + 1], c = y * d.W + x;
+            opk[i] = (uint32_t)(x & 0xfff) | ((uint32_t)(y & 0xfff) << 12) | ((okind[i] == ZS_THING_BOX ? 1u : 0u) << 24) |
+                     (((objbits[c >> 5] >> (c & 31)) & 1u) << 25);
+        }
+        uint16_t* p_pad;
+        uint32_t* p_opk;
+        TRY(dupload(h, &p_pad, pad));
+        TRY(dupload(h, &p_opk, opk));
+        d.opad = p_pad;
+        d.opad_w = pw;
+        d.opad_n = pw * ph;
+        d.opk = p_opk;
+    }
     d.cellmap = p_cellmap;
     d.objbits = p_objbits;
     d.obstbits = p_obstbits;
@@ -698,6 +738,30 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
                 h->obs_lds = 1;
                 h->obs_lds_bytes = lb;
                 h->obs_pipe_wgs = wgs;
+            }
+        }
+        // k_obs_patch: k_obs_lds with the padded-table encoder (maps up to 4095 x 4095, rows of the
+        // padded table in the workgroup's LDS).  ZS_OBS_PATCH=0/1 forces either.
+        if (h->obs_lds && d.OW <= 64 && (long)(d.W + 20) * 21 < 65536 && d.H < 4096) {
+            const int ts = d.obs_dtype == ZS_DTYPE_I64 ? 8 : d.obs_dtype == ZS_DTYPE_I32 ? 4 : 2;
+            const size_t pb = (size_t)patch_static_bytes(d.opad_n, d.O) +
+                              PATCH_WPG * (size_t)patch_wave_bytes(d.DW, d.O, obs_stage_slot_bytes(ts));
+            const char* pz = getenv("ZS_OBS_PATCH");
+            const void* fn = nullptr;
+            const int nobs = obs_count(d.obs_scope, d.reward_mode, d.A);
+#define ZS_PATCH_FN(TT)                                                                             \
+    fn = nobs == 1 ? (const void*)k_obs_patch<TT, 1> : nobs == 2 ? (const void*)k_obs_patch<TT, 2> \
+                                                                 : (const void*)k_obs_patch<TT, 4>
+            if (ts == 8) ZS_PATCH_FN(int64_t);
+            else if (ts == 4) ZS_PATCH_FN(int32_t);
+            else ZS_PATCH_FN(int16_t);
+#undef ZS_PATCH_FN
+            if (pb <= 160 * 1024 && (pz ? atoi(pz) != 0 : true) &&
+                hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pb) == hipSuccess) {
+                h->obs_patch = 1;
+                h->obs_patch_bytes = pb;
+                h->obs_patch_wgs = std::max(1, (int)(160 * 1024 / pb));
+                if (getenv("ZS_OBS_WGS")) h->obs_patch_wgs = std::max(1, std::min(32, atoi(getenv("ZS_OBS_WGS"))));
             }
         }
         // k_obs_ring (zs_obs.hpp): the k_obs_lds shape with dedicated writer waves.  Measured on one
@@ -887,6 +951,29 @@ static int launch_obs(zs_handle* h, void* obs, const uint8_t* mask, hipStream_t 
         }
 #undef ZS_RING_T
 #undef ZS_RING
+        HIPCHK(hipGetLastError());
+        if (h->prof) {
+            HIPCHK(hipEventRecord(prof_event(h, &i1), s));
+            h->ev_obs.push_back({i0, i1});
+        }
+        return ZS_OK;
+    }
+    if (!mask && h->obs_patch) {  // every env of [env0, env1): the padded-table encoder's store stream
+        const unsigned g = (unsigned)std::min((env1 - env0 + PATCH_WPG - 1) / PATCH_WPG, 256 * h->obs_patch_wgs);
+        const size_t lds = h->obs_patch_bytes;
+#define ZS_PATCH(TT)                                                                                                   \
+    do {                                                                                                               \
+        if (h->obs_pipe == 1)                                                                                          \
+            hipLaunchKernelGGL((k_obs_patch<TT, 1>), dim3(g), dim3(64 * PATCH_WPG), lds, s, d, (TT*)obs, env0, env1);  \
+        else if (h->obs_pipe == 2)                                                                                     \
+            hipLaunchKernelGGL((k_obs_patch<TT, 2>), dim3(g), dim3(64 * PATCH_WPG), lds, s, d, (TT*)obs, env0, env1);  \
+        else                                                                                                           \
+            hipLaunchKernelGGL((k_obs_patch<TT, 4>), dim3(g), dim3(64 * PATCH_WPG), lds, s, d, (TT*)obs, env0, env1);  \
+    } while (0)
+        if (d.obs_dtype == ZS_DTYPE_I64) ZS_PATCH(int64_t);
+        else if (d.obs_dtype == ZS_DTYPE_I32) ZS_PATCH(int32_t);
+        else ZS_PATCH(int16_t);
+#undef ZS_PATCH
         HIPCHK(hipGetLastError());
         if (h->prof) {
             HIPCHK(hipEventRecord(prof_event(h, &i1), s));
@@ -1397,7 +1484,7 @@ extern "C" int zs_describe(zs_handle* h, char* buf, int32_t len) {
     if (!h || !buf || len <= 0) return fail(ZS_EINVAL, "null argument");
     const Dev& d = h->d;
     const char* obs_kernel = d.fobs ? "step launch"
-                             : h->obs_pipe ? (h->obs_ring ? "k_obs_ring" : h->obs_lds ? "k_obs_lds" : "k_obs_pipe")
+                             : h->obs_pipe ? (h->obs_ring ? "k_obs_ring" : h->obs_patch ? "k_obs_patch" : h->obs_lds ? "k_obs_lds" : "k_obs_pipe")
                              : h->obs_gather ? "k_obs_gather" : "k_obs";
     snprintf(buf, (size_t)len,
              "{\"envs\": %d, \"entities\": %d, \"lanes_per_env\": %d, \"step_kernel\": \"%s\", \"step_lds\": %zu, "

@@ -108,6 +108,11 @@ struct Dev {
     const int32_t* scell;      // static: per-cell obstacle index + 1 | code << 16 | objective << 20 (zs_obs.hpp)
     const uint32_t* boxbits;   // static: cell holds a Box [DW]
     const int32_t* oprefix;    // static: obstacles in cells < 32*w (obstacle index = cell rank) [DW]
+    // static, k_obs_patch (zs_obs.hpp): the map padded by half a window on every side, one u16 per
+    // padded cell (opad_w x opad_n / opad_w), and per obstacle its packed cell and kind (opk)
+    const uint16_t* opad;
+    int opad_w, opad_n;
+    const uint32_t* opk;
     const int32_t* obst_xy;  // packed x | y << 16
     const uint8_t* obst_kind;
     const int32_t* pspawn;   // packed

@@ -912,6 +912,236 @@ __global__ void __launch_bounds__(256, ZS_OBS_PIPE_WAVES) k_obs_lds(Dev d, T* ou
 }
 
 // ---------------------------------------------------------------------------
+// k_obs_patch: k_obs_lds's walk, prefetch and 16-B flush, with a cheaper encoder.  A window cell's
+// value is first taken from a padded static table of the map (one LDS read: the code and life the
+// cell shows when no thing stands on it, every obstacle is present at its MAX_LIFE and no body lies
+// there; out-of-bounds cells are Wall(200) entries of the padding), then the few cells whose value
+// differs are patched in place, in rising precedence (gym/observation.py:57-90: thing > present
+// obstacle > dead body > objective > empty):
+//   * obstacles whose life left MAX_LIFE or that were cleaned up (core.py:121-138): a per-env list in
+//     LDS, compacted once per env, each entry the cell and the value it shows;
+//   * dead bodies on cells without a map obstacle, from the env's dead-body words in registers;
+//   * the present things, one per lane (slot s on lane s).
+// Per cell that is one LDS read and three slot writes instead of k_obs_lds's five dependent lookups and
+// select chain (C5: ~51 VALU instructions per cell, the kernel VALU-issue-bound at 63 % busy).
+// ---------------------------------------------------------------------------
+// padded table entry (engine.hip: opad): bits 0..2 the code, bit 3 objective under a map obstacle,
+// bits 8..15 the life; opk (per obstacle): x | y << 12 | box << 24 | objective-under << 25
+#define OPAD_OBJ 8u
+__host__ __device__ constexpr int patch_list_bytes(int O) { return ((O * 8 + 15) / 16) * 16; }
+// static LDS of a workgroup: the padded table and the obstacles' packed cells
+__host__ __device__ constexpr int patch_static_bytes(int opad_n, int O) {
+    return ((opad_n * 2 + 15) / 16) * 16 + ((O * 4 + 15) / 16) * 16 + 256;
+}
+__host__ __device__ constexpr int patch_wave_bytes(int DW, int O, int slot) {
+    return ((DW * 4 + 15) / 16) * 16 + 256 + patch_list_bytes(O) + slot;  // dead words, present words, list, slot
+}
+
+// the env a wave encodes, held in registers (lane s: entity slot s; lane w: dead-body words w, w + 64)
+struct PatchEnv {
+    int32_t pos, life;
+    int wp, pr;
+    int nchg;        // entries of the obstacle list (wave-uniform)
+    bool any_dead;   // some dead-body word is non-zero (wave-uniform)
+};
+
+// waves per workgroup: eight share one copy of the static tables (16 KB at bridge64), two workgroups
+// per CU
+#define PATCH_WPG 8
+template <typename T, int NOBS>
+__global__ void __launch_bounds__(64 * PATCH_WPG, ZS_OBS_PIPE_WAVES) k_obs_patch(Dev d, T* out, int env0, int env1) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) step_tail(d);  // a zs_step's tail (Dev::tail_*)
+    extern __shared__ __align__(16) uint8_t smem[];
+    typedef typename obs_stage<T>::type S;
+    constexpr int WW = 21, HALF = WW / 2, PLANE = WW * WW, PER = (PLANE + 63) / 64, TS = (int)sizeof(T);
+    constexpr int SLOT = obs_stage_slot_bytes(TS);
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int PW = d.opad_w, padb = ((d.opad_n * 2 + 15) / 16) * 16, okb = ((d.O * 4 + 15) / 16) * 16 + 256;
+    // the padded static table (16 B per lane-load) and the obstacles' packed cells
+    {
+        const zs_v4u* src = (const zs_v4u*)d.opad;
+        lv4u* dst = (lv4u*)smem;
+        for (int k = threadIdx.x; k < padb / 16; k += blockDim.x) dst[k] = src[k];
+        lu32* ok = (lu32*)(smem + padb);
+        for (int k = threadIdx.x; k < d.O; k += blockDim.x) ok[k] = d.opk[k];
+    }
+    __syncthreads();
+    const lu16* pad = (const lu16*)smem;
+    const lu32* okl = (const lu32*)(smem + padb);
+    // per lane: bit i set when obstacle lane + 64 i is a Box (MAX_LIFE 10, else a Wall's 200); read
+    // back per env rather than held (a loop-invariant register set the compiler would spill)
+    lu32* boxl = (lu32*)(smem + padb + okb - 256);
+    if (threadIdx.x < 64) {
+        uint32_t m = 0u;
+        for (int i = 0; i < OBS_PF_H; i++) m |= ((okl[min((int)threadIdx.x + 64 * i, d.O - 1)] >> 24) & 1u) << i;
+        boxl[threadIdx.x] = m;
+    }
+    __syncthreads();
+    const int waves = gridDim.x * PATCH_WPG;
+    int e = env0 + xcd_remap(blockIdx.x, gridDim.x) * PATCH_WPG + wave;
+    if (e >= env1) return;
+    lu8* wbase = (lu8*)(smem + padb + okb + wave * patch_wave_bytes(d.DW, d.O, SLOT));
+    lu32* deadl = (lu32*)wbase;
+    lu32* presl = (lu32*)(wbase + ((d.DW * 4 + 15) / 16) * 16);  // obstacle-present words (OW <= 64)
+    ZS_LDS zs_v2i* lst = (ZS_LDS zs_v2i*)(wbase + ((d.DW * 4 + 15) / 16) * 16 + 256);
+    lu8* slot = wbase + ((d.DW * 4 + 15) / 16) * 16 + 256 + patch_list_bytes(d.O);  // 16-B aligned
+    const int code_s = lane < d.A ? d.agent_codes[lane < d.A ? lane : 0] : (lane < d.A + d.P ? ZS_THING_PLAYER : ZS_THING_ZOMBIE);
+    // per lane, for the whole walk: its window cells' offsets in the padded table from a window's
+    // corner, two 16-bit offsets per register (engine.hip admits the kernel when 21 rows < 65536)
+    uint32_t offp[(PER + 1) / 2];
+#pragma unroll
+    for (int i = 0; i < PER; i++) {
+        const int cc = min(lane + 64 * i, PLANE - 1), r = cc / WW;
+        const uint32_t v = (uint32_t)(r * PW + (cc - r * WW));
+        if (i % 2 == 0) offp[i / 2] = v;
+        else offp[i / 2] |= v << 16;
+    }
+    const int W = d.W;
+    PatchEnv cur;
+    // registers of a prefetched env -> cur, its dead-body words and obstacle list -> LDS
+    auto build = [&](const ObsPrefetch& f) __attribute__((always_inline)) {
+        cur.pos = f.pos;
+        cur.life = f.life;
+        cur.wp = f.wp;
+        cur.pr = f.pr;
+        bool nz = false;
+#pragma unroll
+        for (int i = 0; i < OBS_PF_D; i++)
+            if (lane + 64 * i < d.DW) {
+                deadl[lane + 64 * i] = f.dead[i];
+                nz |= f.dead[i] != 0u;
+            }
+        cur.any_dead = __ballot(nz) != 0ull;
+        // obstacles away from the table's value: life off MAX_LIFE, or cleaned up
+        const int ow = min(lane, d.OW - 1), nb = min(32, d.O - 32 * ow);
+        const uint32_t full = nb == 32 ? 0xffffffffu : ((1u << nb) - 1u);
+        bool odd = lane < d.OW && f.opres != full;
+        const uint32_t boxm = boxl[lane];
+#pragma unroll
+        for (int i = 0; i < OBS_PF_H; i++)
+            odd |= lane + 64 * i < d.O && f.hp[i] != (((boxm >> i) & 1u) ? 10 : 200);
+        cur.nchg = 0;
+        if (__ballot(odd) == 0ull) return;
+        if (lane < d.OW) presl[lane] = f.opres;
+        wave_sync();  // the dead-body and present words before the lookups below
+        int n = 0;
+#pragma unroll
+        for (int i = 0; i < OBS_PF_H; i++) {
+            const uint32_t pw = presl[(lane >> 5) + 2 * i];  // past OW: unused (chg needs o < O)
+            const bool pres = (pw >> (lane & 31)) & 1u;
+            const uint32_t k = okl[lane + 64 * i];  // past O: another region's word, unused
+            const bool box = (k >> 24) & 1u;
+            const bool chg = lane + 64 * i < d.O && (!pres || f.hp[i] != (box ? 10 : 200));
+            const unsigned long long m = __ballot(chg);
+            if (chg) {
+                const int x = (int)(k & 0xfffu), y = (int)((k >> 12) & 0xfffu), c = y * W + x;
+                int code = ((k >> 25) & 1u) ? ZS_THING_OBJECTIVE : ZS_THING_NONE;
+                code = ((deadl[c >> 5] >> (c & 31)) & 1u) ? ZS_THING_DEADBODY : code;
+                code = pres ? (box ? ZS_THING_BOX : ZS_THING_WALL) : code;
+                lst[n + __popcll(m & ((1ull << lane) - 1ull))] = zs_v2i{(int)(k & 0xffffffu) | (code << 24), pres ? f.hp[i] : 0};
+            }
+            n += __popcll(m);
+        }
+        cur.nchg = n;
+    };
+    // agent a's block of env e into the slot, then streamed out
+    auto encode = [&](int e, int a) __attribute__((always_inline)) {
+        const int32_t ap = __builtin_amdgcn_readlane(cur.pos, a);
+        const int ax = unpack_x(ap), ay = unpack_y(ap);
+        T* o = out + ((size_t)e * NOBS + a) * 3 * PLANE;
+        ZS_LDS S* ot = (ZS_LDS S*)slot + (int)((uintptr_t)o & 15) / TS;
+        const int pbase = ay * PW + ax;  // padded cell of the window's corner (ax - HALF, ay - HALF)
+#pragma unroll
+        for (int i = 0; i < ((ZS_OBS_DIAG & 16) ? 0 : PER); i++) {  // diagnostic builds: 16 skips the encoding
+            const int cell = lane + 64 * i;
+            if (i + 1 < PER || cell < PLANE) {
+                const uint32_t v = pad[pbase + (int)((offp[i / 2] >> (16 * (i % 2))) & 0xffffu)];
+                ot[cell] = (S)(v & 7u);
+                ot[PLANE + cell] = (S)(v >> 8);
+                ot[2 * PLANE + cell] = (S)0;
+            }
+        }
+        // obstacles off the table's value
+        for (int k = lane; k < cur.nchg; k += 64) {
+            const zs_v2i en = lst[k];
+            const int dx = (en.x & 0xfff) - ax + HALF, dy = ((en.x >> 12) & 0xfff) - ay + HALF;
+            if ((unsigned)dx < (unsigned)WW && (unsigned)dy < (unsigned)WW) {
+                const int cc = dy * WW + dx;
+                ot[cc] = (S)((en.x >> 24) & 7);
+                ot[PLANE + cc] = obs_val<S>(en.y);
+            }
+        }
+        // dead bodies on cells without a map obstacle (a map obstacle's cell is the list's business)
+        if (cur.any_dead) {
+            const int c_lo = (ay - HALF) * W, c_hi = (ay + HALF + 1) * W;  // the window's rows
+#pragma unroll
+            for (int i = 0; i < OBS_PF_D; i++) {
+                const int w = lane + 64 * i;
+                uint32_t bits = w < d.DW ? deadl[w] : 0u;
+                if (32 * w + 31 < c_lo || 32 * w >= c_hi) bits = 0u;
+                while (bits) {
+                    const int c = 32 * w + __ffs(bits) - 1;
+                    bits &= bits - 1u;
+                    const int y = c / W, x = c - y * W;
+                    const int dx = x - ax + HALF, dy = y - ay + HALF;
+                    if ((unsigned)dx < (unsigned)WW && (unsigned)dy < (unsigned)WW) {
+                        const uint32_t sc = pad[(y + HALF) * PW + x + HALF] & 7u;
+                        if (sc != ZS_THING_BOX && sc != ZS_THING_WALL) {
+                            const int cc = dy * WW + dx;
+                            ot[cc] = (S)ZS_THING_DEADBODY;
+                            ot[PLANE + cc] = (S)0;
+                        }
+                    }
+                }
+            }
+        }
+        // the present things
+        if (lane < d.E && cur.pr) {
+            const int dx = unpack_x(cur.pos) - ax + HALF, dy = unpack_y(cur.pos) - ay + HALF;
+            if ((unsigned)dx < (unsigned)WW && (unsigned)dy < (unsigned)WW) {
+                const int cc = dy * WW + dx;
+                ot[cc] = (S)code_s;
+                ot[PLANE + cc] = obs_val<S>(cur.life);
+                ot[2 * PLANE + cc] = (S)cur.wp;
+            }
+        }
+        wave_sync();
+        if (!(ZS_OBS_DIAG & 8)) obs_stage_flush(slot, o, lane);
+        wave_sync();
+    };
+    auto process = [&](int e) __attribute__((always_inline)) {
+#pragma unroll
+        for (int a = 0; a < NOBS; a++) encode(e, a);
+    };
+    // two envs of register prefetch in flight, as k_obs_lds
+    ObsPrefetch fa, fb;
+    {
+        const int e1 = min(e + waves, env1 - 1);
+        obs_prefetch(d, e, min(e + 2 * waves, env1 - 1), obs_dirty(d, e), fa);
+        obs_prefetch(d, e1, min(e1 + 2 * waves, env1 - 1), obs_dirty(d, e1), fb);
+    }
+    build(fa);
+    for (;;) {
+        {
+            const int en = min(e + 2 * waves, env1 - 1);
+            obs_prefetch(d, en, min(en + 2 * waves, env1 - 1), fa.dirty_ahead, fa);
+        }
+        process(e);
+        e += waves;
+        if (e >= env1) break;
+        build(fb);
+        {
+            const int en = min(e + 2 * waves, env1 - 1);
+            obs_prefetch(d, en, min(en + 2 * waves, env1 - 1), fb.dirty_ahead, fb);
+        }
+        process(e);
+        e += waves;
+        if (e >= env1) break;
+        build(fa);
+    }
+}
+
+// ---------------------------------------------------------------------------
 // k_obs_ring: k_obs_lds with the encoding and the store stream on different waves.  A workgroup of
 // RING_ENC encoder waves and RING_WRT writer waves walks envs b, b + G, ... (b = its XCD-contiguous
 // index, G = the grid); encoder waves build an env's image from prefetched registers and encode every

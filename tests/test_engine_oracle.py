@@ -133,7 +133,8 @@ PATHS = {
     "obs_gather": {"ZS_FOBS": "0", "ZS_OBS_PIPE": "0"},  # window-only fetches (k_obs_gather)
     "obs_gather_scell": {"ZS_FOBS": "0", "ZS_OBS_PIPE": "0", "ZS_OBS_GATHER_STAT": "0"},  # ... global static words
     "obs_pipe_cells": {"ZS_OBS_LDS": "0"},          # k_obs_pipe's per-cell stores instead of k_obs_lds
-    "obs_lds": {"ZS_OBS_LDS": "1"},                 # k_obs_lds at any env count
+    "obs_lds": {"ZS_OBS_LDS": "1"},                 # the LDS-staged store stream at any env count (k_obs_patch)
+    "obs_lds_select": {"ZS_OBS_LDS": "1", "ZS_OBS_PATCH": "0"},  # ... k_obs_lds's per-cell select chain
     "obs_ring": {"ZS_OBS_LDS": "1", "ZS_OBS_RING": "1"},  # encoder / writer waves through an LDS ring
     "obs_scan": {"ZS_OBS_WIN": "0"},                # per-cell entity scan instead of the window map
     "obs_scan_in_step": {"ZS_OBS_WIN": "0", "ZS_FOBS": "1"},
@@ -205,10 +206,12 @@ def test_step_graph(path, monkeypatch):
                16, 30, check_state_every=15, graph=True)
 
 
-def test_store_stream_every_phase(monkeypatch):
-    """k_obs_lds writes each observation block from an LDS slot kept at the destination's 16-B
-    phase: int16 blocks of 4 agents (2646 B: every even phase), int32 single-agent blocks (5292 B)."""
+@pytest.mark.parametrize("patch", ["0", "1"])
+def test_store_stream_every_phase(patch, monkeypatch):
+    """k_obs_patch / k_obs_lds write each observation block from an LDS slot kept at the destination's
+    16-B phase: int16 blocks of 4 agents (2646 B: every even phase), int32 single-agent blocks (5292 B)."""
     monkeypatch.setenv("ZS_OBS_LDS", "1")
+    monkeypatch.setenv("ZS_OBS_PATCH", patch)
     run_parity(lambda n: _abi.multi_env_config(n, "extermination", [], "bridge64", ["0", "1", "2", "3"],
                                                initial_zombies=20, obs_dtype=_abi.DTYPE_I16, max_episode_steps=200),
                64, 60, check_state_every=30)

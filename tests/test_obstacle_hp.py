@@ -56,12 +56,21 @@ def _poke_all(eng, pokes):
         eng.set_state(k, st)
 
 
+# observation kernels: the engine's pick for the size (int16 / int32: k_obs_patch), the store stream
+# forced at 64 envs (int64 too: k_obs_patch), and k_obs_lds's per-cell select chain
+OBS_PATHS = {"default": {}, "patch": {"ZS_OBS_LDS": "1"}, "lds_select": {"ZS_OBS_LDS": "1", "ZS_OBS_PATCH": "0"}}
+
+
 @pytest.mark.gpu
+@pytest.mark.parametrize("path", sorted(OBS_PATHS))
 @pytest.mark.parametrize("dtype", [_abi.DTYPE_I64, _abi.DTYPE_I32, _abi.DTYPE_I16])
-def test_engine_matches_oracle_across_resets(dtype):
+def test_engine_matches_oracle_across_resets(dtype, path, monkeypatch):
     """64 envs x 160 calls (80 episodes), every call's obs / rewards / flags and the obstacle state
     against the oracle; int16 observations saturate like the oracle's int16 form and raise
-    ZS_OVF_INT16, never ZS_OVF_INT32."""
+    ZS_OVF_INT16, never ZS_OVF_INT32.  The 5 x 4 map puts most of every 21 x 21 window out of bounds,
+    and the walls the agents shoot are damaged, destroyed and re-spawned at negative life."""
+    for k, v in OBS_PATHS[path].items():
+        monkeypatch.setenv(k, v)
     import torch
     from libzombsole_amd.engine import Engine
     from oracle.oracle import OracleEnv
