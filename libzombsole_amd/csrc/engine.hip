@@ -769,19 +769,29 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
         // Default for int64 blocks; ZS_OBS_RING=0/1 forces either.
         if (h->obs_lds && d.obs_enc == ZS_ENC_CHANNELS) {
             const int ts = d.obs_dtype == ZS_DTYPE_I64 ? 8 : d.obs_dtype == ZS_DTYPE_I32 ? 4 : 2;
-            const size_t rb = (size_t)ring_lds_bytes(16 * d.DW, L.bytes, ts, nobs);
+            // the ring's encoders are k_obs_patch's when its tables fit (ZS_OBS_RING_PATCH=0/1 forces either)
+            const char* rp = getenv("ZS_OBS_RING_PATCH");
+            const bool patched = h->obs_patch && (rp ? atoi(rp) != 0 : true);
+            const size_t rb = patched ? (size_t)ring_lds_bytes(patch_static_bytes(d.opad_n, d.O), patch_enc_bytes(d.DW, d.O), ts, nobs)
+                                      : (size_t)ring_lds_bytes(16 * d.DW, L.bytes, ts, nobs);
             const char* rg = getenv("ZS_OBS_RING");
             if (rb <= 160 * 1024 && (rg ? atoi(rg) != 0 : ts == 8)) {
                 const void* fn = nullptr;
-#define ZS_RING_FN(TT)                                                             \
-    fn = nobs == 1 ? (const void*)k_obs_ring<TT, 1> : nobs == 2 ? (const void*)k_obs_ring<TT, 2> \
-                                                                : (const void*)k_obs_ring<TT, 4>
-                if (ts == 8) ZS_RING_FN(int64_t);
-                else if (ts == 4) ZS_RING_FN(int32_t);
-                else ZS_RING_FN(int16_t);
+#define ZS_RING_FN(TT, P)                                                                      \
+    fn = nobs == 1 ? (const void*)k_obs_ring<TT, 1, P> : nobs == 2 ? (const void*)k_obs_ring<TT, 2, P> \
+                                                                   : (const void*)k_obs_ring<TT, 4, P>
+                if (patched) {
+                    if (ts == 8) ZS_RING_FN(int64_t, true);
+                    else if (ts == 4) ZS_RING_FN(int32_t, true);
+                    else ZS_RING_FN(int16_t, true);
+                } else {
+                    if (ts == 8) ZS_RING_FN(int64_t, false);
+                    else if (ts == 4) ZS_RING_FN(int32_t, false);
+                    else ZS_RING_FN(int16_t, false);
+                }
 #undef ZS_RING_FN
                 if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)rb) == hipSuccess) {
-                    h->obs_ring = 1;
+                    h->obs_ring = patched ? 2 : 1;
                     h->obs_ring_bytes = rb;
                 }
             }
@@ -936,8 +946,15 @@ static int launch_obs(zs_handle* h, void* obs, const uint8_t* mask, hipStream_t 
         const int pair = ring_pair(ts, h->obs_pipe);
         const unsigned g = (unsigned)std::min((env1 - env0 + pair - 1) / pair, 256);
         const size_t lds = h->obs_ring_bytes;
-#define ZS_RING(TT, NB) hipLaunchKernelGGL((k_obs_ring<TT, NB>), dim3(g), dim3(64 * (RING_ENC + RING_WRT)), lds, s, d, \
-                                           (TT*)obs, h->obs_l, env0, env1)
+#define ZS_RING(TT, NB)                                                                                          \
+    do {                                                                                                         \
+        if (h->obs_ring == 2)                                                                                    \
+            hipLaunchKernelGGL((k_obs_ring<TT, NB, true>), dim3(g), dim3(64 * (RING_ENC + RING_WRT)), lds, s, d, \
+                               (TT*)obs, h->obs_l, env0, env1);                                                  \
+        else                                                                                                     \
+            hipLaunchKernelGGL((k_obs_ring<TT, NB, false>), dim3(g), dim3(64 * (RING_ENC + RING_WRT)), lds, s, d, \
+                               (TT*)obs, h->obs_l, env0, env1);                                                  \
+    } while (0)
 #define ZS_RING_T(TT)                   \
     if (h->obs_pipe == 1) ZS_RING(TT, 1); \
     else if (h->obs_pipe == 2) ZS_RING(TT, 2); \

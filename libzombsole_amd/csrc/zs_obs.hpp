@@ -933,77 +933,76 @@ __host__ __device__ constexpr int patch_list_bytes(int O) { return ((O * 8 + 15)
 __host__ __device__ constexpr int patch_static_bytes(int opad_n, int O) {
     return ((opad_n * 2 + 15) / 16) * 16 + ((O * 4 + 15) / 16) * 16 + 256;
 }
-__host__ __device__ constexpr int patch_wave_bytes(int DW, int O, int slot) {
-    return ((DW * 4 + 15) / 16) * 16 + 256 + patch_list_bytes(O) + slot;  // dead words, present words, list, slot
+
+__host__ __device__ constexpr int patch_enc_bytes(int DW, int O) {  // dead words, present words, list
+    return ((DW * 4 + 15) / 16) * 16 + 256 + patch_list_bytes(O);
 }
+__host__ __device__ constexpr int patch_wave_bytes(int DW, int O, int slot) { return patch_enc_bytes(DW, O) + slot; }
 
-// the env a wave encodes, held in registers (lane s: entity slot s; lane w: dead-body words w, w + 64)
-struct PatchEnv {
-    int32_t pos, life;
-    int wp, pr;
-    int nchg;        // entries of the obstacle list (wave-uniform)
-    bool any_dead;   // some dead-body word is non-zero (wave-uniform)
-};
-
-// waves per workgroup: eight share one copy of the static tables (16 KB at bridge64), two workgroups
-// per CU
-#define PATCH_WPG 8
-template <typename T, int NOBS>
-__global__ void __launch_bounds__(64 * PATCH_WPG, ZS_OBS_PIPE_WAVES) k_obs_patch(Dev d, T* out, int env0, int env1) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) step_tail(d);  // a zs_step's tail (Dev::tail_*)
-    extern __shared__ __align__(16) uint8_t smem[];
-    typedef typename obs_stage<T>::type S;
-    constexpr int WW = 21, HALF = WW / 2, PLANE = WW * WW, PER = (PLANE + 63) / 64, TS = (int)sizeof(T);
-    constexpr int SLOT = obs_stage_slot_bytes(TS);
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const int PW = d.opad_w, padb = ((d.opad_n * 2 + 15) / 16) * 16, okb = ((d.O * 4 + 15) / 16) * 16 + 256;
-    // the padded static table (16 B per lane-load) and the obstacles' packed cells
-    {
-        const zs_v4u* src = (const zs_v4u*)d.opad;
-        lv4u* dst = (lv4u*)smem;
-        for (int k = threadIdx.x; k < padb / 16; k += blockDim.x) dst[k] = src[k];
-        lu32* ok = (lu32*)(smem + padb);
-        for (int k = threadIdx.x; k < d.O; k += blockDim.x) ok[k] = d.opk[k];
-    }
+// Stage the static tables into the workgroup's LDS (all threads, then a barrier): the padded table,
+// the obstacles' packed cells, and per lane the Box bits of its obstacles lane + 64 i.
+__device__ __forceinline__ void patch_stage_static(const Dev& d, uint8_t* smem) {
+    const int padb = ((d.opad_n * 2 + 15) / 16) * 16, okb = ((d.O * 4 + 15) / 16) * 16;
+    const zs_v4u* src = (const zs_v4u*)d.opad;
+    lv4u* dst = (lv4u*)smem;
+    for (int k = threadIdx.x; k < padb / 16; k += blockDim.x) dst[k] = src[k];
+    lu32* ok = (lu32*)(smem + padb);
+    for (int k = threadIdx.x; k < d.O; k += blockDim.x) ok[k] = d.opk[k];
     __syncthreads();
-    const lu16* pad = (const lu16*)smem;
-    const lu32* okl = (const lu32*)(smem + padb);
-    // per lane: bit i set when obstacle lane + 64 i is a Box (MAX_LIFE 10, else a Wall's 200); read
-    // back per env rather than held (a loop-invariant register set the compiler would spill)
-    lu32* boxl = (lu32*)(smem + padb + okb - 256);
     if (threadIdx.x < 64) {
         uint32_t m = 0u;
-        for (int i = 0; i < OBS_PF_H; i++) m |= ((okl[min((int)threadIdx.x + 64 * i, d.O - 1)] >> 24) & 1u) << i;
-        boxl[threadIdx.x] = m;
+        for (int i = 0; i < OBS_PF_H; i++) m |= ((d.opk[min((int)threadIdx.x + 64 * i, d.O - 1)] >> 24) & 1u) << i;
+        ((lu32*)(smem + padb + okb))[threadIdx.x] = m;
     }
     __syncthreads();
-    const int waves = gridDim.x * PATCH_WPG;
-    int e = env0 + xcd_remap(blockIdx.x, gridDim.x) * PATCH_WPG + wave;
-    if (e >= env1) return;
-    lu8* wbase = (lu8*)(smem + padb + okb + wave * patch_wave_bytes(d.DW, d.O, SLOT));
-    lu32* deadl = (lu32*)wbase;
-    lu32* presl = (lu32*)(wbase + ((d.DW * 4 + 15) / 16) * 16);  // obstacle-present words (OW <= 64)
-    ZS_LDS zs_v2i* lst = (ZS_LDS zs_v2i*)(wbase + ((d.DW * 4 + 15) / 16) * 16 + 256);
-    lu8* slot = wbase + ((d.DW * 4 + 15) / 16) * 16 + 256 + patch_list_bytes(d.O);  // 16-B aligned
-    const int code_s = lane < d.A ? d.agent_codes[lane < d.A ? lane : 0] : (lane < d.A + d.P ? ZS_THING_PLAYER : ZS_THING_ZOMBIE);
+}
+
+// One wave's encoder: the env it encodes held in registers (lane s: entity slot s), its dead-body
+// words, obstacle-present words and obstacle list in the wave's LDS region `wb` (patch_enc_bytes).
+template <typename S>
+struct PatchEnc {
+    static constexpr int WW = 21, HALF = WW / 2, PLANE = WW * WW, PER = (PLANE + 63) / 64;
+    const lu16* pad;
+    const lu32* okl;
+    const lu32* boxl;
+    lu32* deadl;
+    lu32* presl;
+    ZS_LDS zs_v2i* lst;
+    int lane, PW, W, code_s;
     // per lane, for the whole walk: its window cells' offsets in the padded table from a window's
     // corner, two 16-bit offsets per register (engine.hip admits the kernel when 21 rows < 65536)
     uint32_t offp[(PER + 1) / 2];
+    int32_t pos, life;
+    int wp, pr;
+    int nchg;       // entries of the obstacle list (wave-uniform)
+    bool any_dead;  // some dead-body word is non-zero (wave-uniform)
+
+    __device__ __forceinline__ PatchEnc(const Dev& d, uint8_t* smem, lu8* wb, int lane_) : lane(lane_) {
+        const int padb = ((d.opad_n * 2 + 15) / 16) * 16, okb = ((d.O * 4 + 15) / 16) * 16;
+        pad = (const lu16*)smem;
+        okl = (const lu32*)(smem + padb);
+        boxl = (const lu32*)(smem + padb + okb);
+        deadl = (lu32*)wb;
+        presl = (lu32*)(wb + ((d.DW * 4 + 15) / 16) * 16);  // OW <= 64
+        lst = (ZS_LDS zs_v2i*)(wb + ((d.DW * 4 + 15) / 16) * 16 + 256);
+        PW = d.opad_w;
+        W = d.W;
+        code_s = lane < d.A ? d.agent_codes[lane < d.A ? lane : 0] : (lane < d.A + d.P ? ZS_THING_PLAYER : ZS_THING_ZOMBIE);
 #pragma unroll
-    for (int i = 0; i < PER; i++) {
-        const int cc = min(lane + 64 * i, PLANE - 1), r = cc / WW;
-        const uint32_t v = (uint32_t)(r * PW + (cc - r * WW));
-        if (i % 2 == 0) offp[i / 2] = v;
-        else offp[i / 2] |= v << 16;
+        for (int i = 0; i < PER; i++) {
+            const int cc = min(lane + 64 * i, PLANE - 1), r = cc / WW;
+            const uint32_t v = (uint32_t)(r * PW + (cc - r * WW));
+            if (i % 2 == 0) offp[i / 2] = v;
+            else offp[i / 2] |= v << 16;
+        }
     }
-    const int W = d.W;
-    PatchEnv cur;
-    // registers of a prefetched env -> cur, its dead-body words and obstacle list -> LDS
-    auto build = [&](const ObsPrefetch& f) __attribute__((always_inline)) {
-        cur.pos = f.pos;
-        cur.life = f.life;
-        cur.wp = f.wp;
-        cur.pr = f.pr;
+
+    // a prefetched env's registers -> this encoder; its dead-body words and obstacle list -> LDS
+    __device__ __forceinline__ void build(const Dev& d, const ObsPrefetch& f) {
+        pos = f.pos;
+        life = f.life;
+        wp = f.wp;
+        pr = f.pr;
         bool nz = false;
 #pragma unroll
         for (int i = 0; i < OBS_PF_D; i++)
@@ -1011,16 +1010,16 @@ __global__ void __launch_bounds__(64 * PATCH_WPG, ZS_OBS_PIPE_WAVES) k_obs_patch
                 deadl[lane + 64 * i] = f.dead[i];
                 nz |= f.dead[i] != 0u;
             }
-        cur.any_dead = __ballot(nz) != 0ull;
-        // obstacles away from the table's value: life off MAX_LIFE, or cleaned up
+        any_dead = __ballot(nz) != 0ull;
+        // obstacles away from the table's value: life off MAX_LIFE, or cleaned up.  The Box bits are read
+        // back per env rather than held (a loop-invariant register set the compiler would spill).
         const int ow = min(lane, d.OW - 1), nb = min(32, d.O - 32 * ow);
         const uint32_t full = nb == 32 ? 0xffffffffu : ((1u << nb) - 1u);
         bool odd = lane < d.OW && f.opres != full;
         const uint32_t boxm = boxl[lane];
 #pragma unroll
-        for (int i = 0; i < OBS_PF_H; i++)
-            odd |= lane + 64 * i < d.O && f.hp[i] != (((boxm >> i) & 1u) ? 10 : 200);
-        cur.nchg = 0;
+        for (int i = 0; i < OBS_PF_H; i++) odd |= lane + 64 * i < d.O && f.hp[i] != (((boxm >> i) & 1u) ? 10 : 200);
+        nchg = 0;
         if (__ballot(odd) == 0ull) return;
         if (lane < d.OW) presl[lane] = f.opres;
         wave_sync();  // the dead-body and present words before the lookups below
@@ -1042,14 +1041,13 @@ __global__ void __launch_bounds__(64 * PATCH_WPG, ZS_OBS_PIPE_WAVES) k_obs_patch
             }
             n += __popcll(m);
         }
-        cur.nchg = n;
-    };
-    // agent a's block of env e into the slot, then streamed out
-    auto encode = [&](int e, int a) __attribute__((always_inline)) {
-        const int32_t ap = __builtin_amdgcn_readlane(cur.pos, a);
+        nchg = n;
+    }
+
+    // agent a's 3 x 21 x 21 block into ot (elements of S)
+    __device__ __forceinline__ void block(const Dev& d, ZS_LDS S* ot, int a) const {
+        const int32_t ap = __builtin_amdgcn_readlane(pos, a);
         const int ax = unpack_x(ap), ay = unpack_y(ap);
-        T* o = out + ((size_t)e * NOBS + a) * 3 * PLANE;
-        ZS_LDS S* ot = (ZS_LDS S*)slot + (int)((uintptr_t)o & 15) / TS;
         const int pbase = ay * PW + ax;  // padded cell of the window's corner (ax - HALF, ay - HALF)
 #pragma unroll
         for (int i = 0; i < ((ZS_OBS_DIAG & 16) ? 0 : PER); i++) {  // diagnostic builds: 16 skips the encoding
@@ -1062,7 +1060,7 @@ __global__ void __launch_bounds__(64 * PATCH_WPG, ZS_OBS_PIPE_WAVES) k_obs_patch
             }
         }
         // obstacles off the table's value
-        for (int k = lane; k < cur.nchg; k += 64) {
+        for (int k = lane; k < nchg; k += 64) {
             const zs_v2i en = lst[k];
             const int dx = (en.x & 0xfff) - ax + HALF, dy = ((en.x >> 12) & 0xfff) - ay + HALF;
             if ((unsigned)dx < (unsigned)WW && (unsigned)dy < (unsigned)WW) {
@@ -1072,7 +1070,7 @@ __global__ void __launch_bounds__(64 * PATCH_WPG, ZS_OBS_PIPE_WAVES) k_obs_patch
             }
         }
         // dead bodies on cells without a map obstacle (a map obstacle's cell is the list's business)
-        if (cur.any_dead) {
+        if (any_dead) {
             const int c_lo = (ay - HALF) * W, c_hi = (ay + HALF + 1) * W;  // the window's rows
 #pragma unroll
             for (int i = 0; i < OBS_PF_D; i++) {
@@ -1096,22 +1094,44 @@ __global__ void __launch_bounds__(64 * PATCH_WPG, ZS_OBS_PIPE_WAVES) k_obs_patch
             }
         }
         // the present things
-        if (lane < d.E && cur.pr) {
-            const int dx = unpack_x(cur.pos) - ax + HALF, dy = unpack_y(cur.pos) - ay + HALF;
+        if (lane < d.E && pr) {
+            const int dx = unpack_x(pos) - ax + HALF, dy = unpack_y(pos) - ay + HALF;
             if ((unsigned)dx < (unsigned)WW && (unsigned)dy < (unsigned)WW) {
                 const int cc = dy * WW + dx;
                 ot[cc] = (S)code_s;
-                ot[PLANE + cc] = obs_val<S>(cur.life);
-                ot[2 * PLANE + cc] = (S)cur.wp;
+                ot[PLANE + cc] = obs_val<S>(life);
+                ot[2 * PLANE + cc] = (S)wp;
             }
         }
-        wave_sync();
-        if (!(ZS_OBS_DIAG & 8)) obs_stage_flush(slot, o, lane);
-        wave_sync();
-    };
+    }
+};
+
+// waves per workgroup: eight share one copy of the static tables (16 KB at bridge64), two workgroups
+// per CU
+#define PATCH_WPG 8
+template <typename T, int NOBS>
+__global__ void __launch_bounds__(64 * PATCH_WPG, ZS_OBS_PIPE_WAVES) k_obs_patch(Dev d, T* out, int env0, int env1) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) step_tail(d);  // a zs_step's tail (Dev::tail_*)
+    extern __shared__ __align__(16) uint8_t smem[];
+    typedef typename obs_stage<T>::type S;
+    constexpr int PLANE = 441, TS = (int)sizeof(T), SLOT = obs_stage_slot_bytes(TS);
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    patch_stage_static(d, smem);
+    const int waves = gridDim.x * PATCH_WPG;
+    int e = env0 + xcd_remap(blockIdx.x, gridDim.x) * PATCH_WPG + wave;
+    if (e >= env1) return;
+    lu8* wb = (lu8*)(smem + patch_static_bytes(d.opad_n, d.O) + wave * patch_wave_bytes(d.DW, d.O, SLOT));
+    lu8* slot = wb + patch_enc_bytes(d.DW, d.O);  // 16-B aligned
+    PatchEnc<S> pe(d, smem, wb, lane);
     auto process = [&](int e) __attribute__((always_inline)) {
 #pragma unroll
-        for (int a = 0; a < NOBS; a++) encode(e, a);
+        for (int a = 0; a < NOBS; a++) {
+            T* o = out + ((size_t)e * NOBS + a) * 3 * PLANE;
+            pe.block(d, (ZS_LDS S*)slot + (int)((uintptr_t)o & 15) / TS, a);
+            wave_sync();
+            if (!(ZS_OBS_DIAG & 8)) obs_stage_flush(slot, o, lane);
+            wave_sync();
+        }
     };
     // two envs of register prefetch in flight, as k_obs_lds
     ObsPrefetch fa, fb;
@@ -1120,7 +1140,7 @@ __global__ void __launch_bounds__(64 * PATCH_WPG, ZS_OBS_PIPE_WAVES) k_obs_patch
         obs_prefetch(d, e, min(e + 2 * waves, env1 - 1), obs_dirty(d, e), fa);
         obs_prefetch(d, e1, min(e1 + 2 * waves, env1 - 1), obs_dirty(d, e1), fb);
     }
-    build(fa);
+    pe.build(d, fa);
     for (;;) {
         {
             const int en = min(e + 2 * waves, env1 - 1);
@@ -1129,7 +1149,7 @@ __global__ void __launch_bounds__(64 * PATCH_WPG, ZS_OBS_PIPE_WAVES) k_obs_patch
         process(e);
         e += waves;
         if (e >= env1) break;
-        build(fb);
+        pe.build(d, fb);
         {
             const int en = min(e + 2 * waves, env1 - 1);
             obs_prefetch(d, en, min(en + 2 * waves, env1 - 1), fb.dirty_ahead, fb);
@@ -1137,7 +1157,7 @@ __global__ void __launch_bounds__(64 * PATCH_WPG, ZS_OBS_PIPE_WAVES) k_obs_patch
         process(e);
         e += waves;
         if (e >= env1) break;
-        build(fa);
+        pe.build(d, fa);
     }
 }
 
@@ -1198,7 +1218,12 @@ __device__ __forceinline__ void ring_wait(const ZS_LDS int* p, int v) {
     asm volatile("" ::: "memory");
 }
 
-template <typename T, int NOBS>
+// PATCHED: the encoders are k_obs_patch's (PatchEnc), static tables patch_static_bytes, encoder regions
+// patch_enc_bytes (ring_patch_lds_bytes)
+__host__ __device__ constexpr int ring_patch_lds_bytes(int static_bytes, int enc_bytes, int tsize, int nobs) {
+    return ring_lds_bytes(static_bytes, enc_bytes, tsize, nobs);
+}
+template <typename T, int NOBS, bool PATCHED = false>
 __global__ void __launch_bounds__(64 * (RING_ENC + RING_WRT), 1) k_obs_ring(Dev d, T* out, ObsLayout L, int env0, int env1) {
     if (blockIdx.x == 0 && threadIdx.x == 0) step_tail(d);  // a zs_step's tail (Dev::tail_*)
     extern __shared__ __align__(16) uint8_t smem[];
@@ -1207,14 +1232,19 @@ __global__ void __launch_bounds__(64 * (RING_ENC + RING_WRT), 1) k_obs_ring(Dev 
     constexpr int PAIR = ring_pair(TS, NOBS), US = RING_SLOTS / PAIR;  // envs per unit, unit slots
     constexpr int SLOT = obs_stage_slot_bytes(TS, NOBS * PAIR), BLK = NOBS * 3 * PLANE;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const int stat_bytes = 16 * d.DW;
+    const int stat_bytes = PATCHED ? patch_static_bytes(d.opad_n, d.O) : 16 * d.DW;
+    const int enc_bytes = PATCHED ? patch_enc_bytes(d.DW, d.O) : L.bytes;
     lv4u* st4 = (lv4u*)smem;
-    lu8* slots = (lu8*)(smem + stat_bytes + RING_ENC * L.bytes);
+    lu8* slots = (lu8*)(smem + stat_bytes + RING_ENC * enc_bytes);
     // state[PAIR * slot + h]: the protocol word of the unit's env h
     ZS_LDS int* state = (ZS_LDS int*)(slots + US * SLOT);
-    obs_stage_static4(d, st4, threadIdx.x, blockDim.x);
     if (threadIdx.x < RING_SLOTS) state[threadIdx.x] = 0;
-    __syncthreads();
+    if (PATCHED) {
+        patch_stage_static(d, smem);
+    } else {
+        obs_stage_static4(d, st4, threadIdx.x, blockDim.x);
+        __syncthreads();
+    }
     // unit g covers envs env0 + PAIR * g + h (h < PAIR, below env1); this workgroup's units are
     // g_first, g_first + G, ...; its items (envs) t = PAIR * u + h, the last one possibly absent
     const int G = gridDim.x, n_units = (env1 - env0 + PAIR - 1) / PAIR;
@@ -1245,7 +1275,8 @@ __global__ void __launch_bounds__(64 * (RING_ENC + RING_WRT), 1) k_obs_ring(Dev 
         return;
     }
     // encoder
-    lu8* img = (lu8*)(smem + stat_bytes + wave * L.bytes);
+    lu8* img = (lu8*)(smem + stat_bytes + wave * enc_bytes);
+    PatchEnc<S> pe(d, smem, img, lane);
     const li32* pos = (const li32*)(img + L.off_pos);
     const int code_s = lane < d.A ? d.agent_codes[lane < d.A ? lane : 0] : (lane < d.A + d.P ? ZS_THING_PLAYER : ZS_THING_ZOMBIE);
     auto item_env = [&](int t) { return unit_env(t / PAIR) + t % PAIR; };
@@ -1256,7 +1287,8 @@ __global__ void __launch_bounds__(64 * (RING_ENC + RING_WRT), 1) k_obs_ring(Dev 
     // dq reloaded for the item two iterations after that
     auto encode = [&](int t, ObsPrefetch& f, zs_v2u& dq, int ahead) {
         const int u = t / PAIR, h = t % PAIR, e = item_env(t);
-        obs_build_compact(d, L, img, f, code_s, lane);
+        if (PATCHED) pe.build(d, f);
+        else obs_build_compact(d, L, img, f, code_s, lane);
         const int tn = t + ahead * RING_ENC, tq = t + (ahead + 2) * RING_ENC;
         if (ahead == 1) {
             if (tn < count) obs_prefetch(d, item_env(tn), tn + RING_ENC < count ? item_env(tn + RING_ENC) : item_env(tn), f.dirty_ahead, f);
@@ -1267,17 +1299,21 @@ __global__ void __launch_bounds__(64 * (RING_ENC + RING_WRT), 1) k_obs_ring(Dev 
             dq = obs_dirty(d, item_env(tq < count ? tq : wave));
         }
         wave_sync();
-        obs_window_compact<NOBS>(d, L, img, lane);
+        if (!PATCHED) obs_window_compact<NOBS>(d, L, img, lane);
         const int q = u % US;
         if (u >= US) ring_wait(&state[PAIR * q + h], 2 * (u - US) + 2);
         wave_sync();
         ZS_LDS S* ot0 = (ZS_LDS S*)(slots + q * SLOT) + (int)((uintptr_t)(out + (size_t)(e - h) * BLK) & 15) / TS + h * BLK;
 #pragma unroll
         for (int a = 0; a < ((ZS_OBS_DIAG & 16) ? 0 : NOBS); a++) {
-            const int32_t ap = pos[a];
-            const int ox = unpack_x(ap) - WW / 2, oy = unpack_y(ap) - WW / 2;
-            const lu8* wm = img + a * PLANE;
-            obs_encode_block<S>(d, L, st4, img, wm, ox, oy, ot0 + a * 3 * PLANE, lane);
+            if (PATCHED) {
+                pe.block(d, ot0 + a * 3 * PLANE, a);
+            } else {
+                const int32_t ap = pos[a];
+                const int ox = unpack_x(ap) - WW / 2, oy = unpack_y(ap) - WW / 2;
+                const lu8* wm = img + a * PLANE;
+                obs_encode_block<S>(d, L, st4, img, wm, ox, oy, ot0 + a * 3 * PLANE, lane);
+            }
         }
         ring_state_store(&state[PAIR * q + h], 2 * u + 1);
     };

@@ -136,6 +136,7 @@ PATHS = {
     "obs_lds": {"ZS_OBS_LDS": "1"},                 # the LDS-staged store stream at any env count (k_obs_patch)
     "obs_lds_select": {"ZS_OBS_LDS": "1", "ZS_OBS_PATCH": "0"},  # ... k_obs_lds's per-cell select chain
     "obs_ring": {"ZS_OBS_LDS": "1", "ZS_OBS_RING": "1"},  # encoder / writer waves through an LDS ring
+    "obs_ring_select": {"ZS_OBS_LDS": "1", "ZS_OBS_RING": "1", "ZS_OBS_RING_PATCH": "0"},  # ... k_obs_lds's encoders
     "obs_scan": {"ZS_OBS_WIN": "0"},                # per-cell entity scan instead of the window map
     "obs_scan_in_step": {"ZS_OBS_WIN": "0", "ZS_FOBS": "1"},
     "obs_scell": {"ZS_OBS_STAT": "0"},              # per-cell static words instead of LDS bitmaps

@@ -151,6 +151,14 @@ def test_c5_odd_int16_ring_pairs(monkeypatch):
     run_full(c5, 4097, 24, seed0=555, min_resets=0)
 
 
+def test_c2_4096_ring_select_encoders(monkeypatch):
+    """k_obs_ring with k_obs_lds's select-chain encoders instead of the padded-table ones."""
+    monkeypatch.setenv("ZS_OBS_LDS", "1")
+    monkeypatch.setenv("ZS_OBS_RING", "1")
+    monkeypatch.setenv("ZS_OBS_RING_PATCH", "0")
+    run_full(c3, 4096, 40, seed0=4321)
+
+
 def test_c2_4096_one_obs_workgroup_per_cu_cells(monkeypatch):
     """The same walk through k_obs_pipe's per-cell stores."""
     monkeypatch.setenv("ZS_OBS_WGS", "1")
