@@ -661,6 +661,12 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
         TRY(dupload(h, &p_init, init));
         d.hp_init = p_init;
         d.hp_chunk = std::max(1, (d.O + 31) / 32);
+        d.hp_chunk_m = (uint32_t)(((1u << 20) + d.hp_chunk - 1) / d.hp_chunk);
+        std::vector<uint32_t> full(std::max(d.OW, 1), 0u);
+        for (int w = 0; w < d.OW; w++) full[w] = d.O - 32 * w >= 32 ? 0xffffffffu : ((1u << (d.O - 32 * w)) - 1u);
+        uint32_t* p_full;
+        TRY(dupload(h, &p_full, full));
+        d.opres_full = p_full;
     }
     TRY(dalloc(h, &d.obst_present, (size_t)d.OW * N));
     TRY(dalloc(h, &d.obst_nonpos, (size_t)d.OW * N));
@@ -672,6 +678,9 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
         TRY(dupload(h, &p_zero, zero));
         d.dead_zero = p_zero;
         d.dead_chunk = std::max(1, (d.DW + 31) / 32);
+        d.dead_chunk_m = (uint32_t)(((1u << 20) + d.dead_chunk - 1) / d.dead_chunk);
+        // exact for every cell when cells * (w_m * W - 2^20) < 2^20 (w_m * W - 2^20 < W)
+        d.w_m = (long)d.W * d.H * d.W < (1L << 20) ? (uint32_t)(((1u << 20) + d.W - 1) / d.W) : 0u;
     }
     TRY(dalloc(h, &d.ring, (size_t)ZS_RING_WORDS * N));
     TRY(dalloc(h, &d.rngst, N));

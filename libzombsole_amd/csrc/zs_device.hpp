@@ -142,12 +142,16 @@ struct Dev {
     uint32_t* hp_dirty;
     const int32_t* hp_init;  // [O] Box / Wall MAX_LIFE
     int hp_chunk;            // ceil(O / 32)
+    uint32_t hp_chunk_m;     // ceil(2^20 / hp_chunk): o / hp_chunk = (o * hp_chunk_m) >> 20 for o < 2^16 / hp_chunk
     // [N]: bit k set once a dead-body word of chunk k (words k * dead_chunk .. + dead_chunk - 1) may be
     // non-zero (tick cleanup, zs_set_state; k_reset clears it with the row): the prefetching observation
     // kernels read a clean chunk from dead_zero, so an env with few bodies reads few dead words
     uint32_t* dead_dirty;
     const uint32_t* dead_zero;  // [DW] zeros
     int dead_chunk;             // ceil(DW / 32)
+    uint32_t dead_chunk_m;      // ceil(2^20 / dead_chunk), as hp_chunk_m
+    const uint32_t* opres_full;  // [OW] every obstacle present (the row of an env with no HP chunk dirty)
+    uint32_t w_m;               // ceil(2^20 / W): c / W = (c * w_m) >> 20 for every cell c (0: not exact, divide)
     uint32_t* obst_present;
     uint32_t* obst_nonpos;
     uint32_t* dead;

@@ -522,14 +522,15 @@ __device__ __forceinline__ void obs_prefetch_env(const Dev& d, int e, zs_v2u dir
 #pragma unroll
     for (int i = 0; i < OBS_PF_D; i++) {
         const int w = min(lane + 64 * i, d.DW - 1);
-        f.dead[i] = (((dirty.y >> (w / d.dead_chunk)) & 1u) ? dr : d.dead_zero)[w];
+        f.dead[i] = (((dirty.y >> ((w * d.dead_chunk_m) >> 20)) & 1u) ? dr : d.dead_zero)[w];
     }
-    f.opres = d.obst_present[(size_t)ed * d.OW + min(lane, d.OW - 1)];
+    // an obstacle is cleaned up only at life <= 0, so an env with no HP chunk dirty has every one
+    f.opres = (dirty.x ? d.obst_present + (size_t)ed * d.OW : d.opres_full)[min(lane, d.OW - 1)];
     const int32_t* hr = d.obst_hp + (size_t)eh * d.O;
 #pragma unroll
     for (int i = 0; i < OBS_PF_H; i++) {
         const int o = min(lane + 64 * i, d.O - 1);
-        f.hp[i] = (((dirty.x >> (o / d.hp_chunk)) & 1u) ? hr : d.hp_init)[o];
+        f.hp[i] = (((dirty.x >> ((o * d.hp_chunk_m) >> 20)) & 1u) ? hr : d.hp_init)[o];
     }
 }
 __device__ __forceinline__ void obs_prefetch(const Dev& d, int e, int ahead, zs_v2u dirty, ObsPrefetch& f) {
@@ -934,8 +935,11 @@ __host__ __device__ constexpr int patch_static_bytes(int opad_n, int O) {
     return ((opad_n * 2 + 15) / 16) * 16 + ((O * 4 + 15) / 16) * 16 + 256;
 }
 
-__host__ __device__ constexpr int patch_enc_bytes(int DW, int O) {  // dead words, present words, list
-    return ((DW * 4 + 15) / 16) * 16 + 256 + patch_list_bytes(O);
+// per-env list of dead-body cells (without a map obstacle) the encoder patches; an env with more takes
+// the per-word scan
+#define PATCH_DEAD_CAP 256
+__host__ __device__ constexpr int patch_enc_bytes(int DW, int O) {  // dead words, present words, dead list, list
+    return ((DW * 4 + 15) / 16) * 16 + 256 + 4 * PATCH_DEAD_CAP + 16 + patch_list_bytes(O);
 }
 __host__ __device__ constexpr int patch_wave_bytes(int DW, int O, int slot) { return patch_enc_bytes(DW, O) + slot; }
 
@@ -967,6 +971,8 @@ struct PatchEnc {
     const lu32* boxl;
     lu32* deadl;
     lu32* presl;
+    lu32* dlist;  // dead-body cells x | y << 16
+    lu32* dcnt;
     ZS_LDS zs_v2i* lst;
     int lane, PW, W, code_s;
     // per lane, for the whole walk: its window cells' offsets in the padded table from a window's
@@ -975,6 +981,7 @@ struct PatchEnc {
     int32_t pos, life;
     int wp, pr;
     int nchg;       // entries of the obstacle list (wave-uniform)
+    int ndead;      // entries of the dead-body list, -1: more than PATCH_DEAD_CAP (wave-uniform)
     bool any_dead;  // some dead-body word is non-zero (wave-uniform)
 
     __device__ __forceinline__ PatchEnc(const Dev& d, uint8_t* smem, lu8* wb, int lane_) : lane(lane_) {
@@ -984,7 +991,9 @@ struct PatchEnc {
         boxl = (const lu32*)(smem + padb + okb);
         deadl = (lu32*)wb;
         presl = (lu32*)(wb + ((d.DW * 4 + 15) / 16) * 16);  // OW <= 64
-        lst = (ZS_LDS zs_v2i*)(wb + ((d.DW * 4 + 15) / 16) * 16 + 256);
+        dlist = (lu32*)(wb + ((d.DW * 4 + 15) / 16) * 16 + 256);
+        dcnt = dlist + PATCH_DEAD_CAP;
+        lst = (ZS_LDS zs_v2i*)(wb + ((d.DW * 4 + 15) / 16) * 16 + 256 + 4 * PATCH_DEAD_CAP + 16);
         PW = d.opad_w;
         W = d.W;
         code_s = lane < d.A ? d.agent_codes[lane < d.A ? lane : 0] : (lane < d.A + d.P ? ZS_THING_PLAYER : ZS_THING_ZOMBIE);
@@ -1011,6 +1020,37 @@ struct PatchEnc {
                 nz |= f.dead[i] != 0u;
             }
         any_dead = __ballot(nz) != 0ull;
+        ndead = 0;
+        if (any_dead) {
+            // the env's dead-body cells that no map obstacle covers (a map obstacle's cell is the obstacle
+            // list's business), compacted once for every agent's window
+            if (lane == 0) *dcnt = 0u;
+            wave_sync();
+#pragma unroll
+            for (int i = 0; i < OBS_PF_D; i++) {
+                const int w = lane + 64 * i;
+                uint32_t bits = w < d.DW ? f.dead[i] : 0u;
+                if (bits) {
+                    uint32_t k = __hip_atomic_fetch_add(dcnt, (uint32_t)__popc(bits), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                    while (bits) {
+                        const int c = 32 * w + __ffs(bits) - 1;
+                        bits &= bits - 1u;
+                        const int y = d.w_m ? (int)(((uint32_t)c * d.w_m) >> 20) : c / W, x = c - y * W;
+                        const uint32_t sc = pad[(y + HALF) * PW + x + HALF] & 7u;
+                        if (sc != ZS_THING_BOX && sc != ZS_THING_WALL) {
+                            if (k < PATCH_DEAD_CAP) dlist[k] = (uint32_t)x | ((uint32_t)y << 16);
+                            k++;
+                        } else {
+                            dlist[k < PATCH_DEAD_CAP ? k : 0] = 0xffffffffu;  // a hole: matches no window
+                            k++;
+                        }
+                    }
+                }
+            }
+            wave_sync();
+            const int n = (int)__builtin_amdgcn_readfirstlane(*dcnt);
+            ndead = n <= PATCH_DEAD_CAP ? n : -1;
+        }
         // obstacles away from the table's value: life off MAX_LIFE, or cleaned up.  The Box bits are read
         // back per env rather than held (a loop-invariant register set the compiler would spill).
         const int ow = min(lane, d.OW - 1), nb = min(32, d.O - 32 * ow);
@@ -1070,17 +1110,35 @@ struct PatchEnc {
             }
         }
         // dead bodies on cells without a map obstacle (a map obstacle's cell is the list's business)
-        if (any_dead) {
+        for (int k = lane; k < ((ZS_OBS_DIAG & 32) ? 0 : ndead); k += 64) {  // diagnostic builds: 32 skips them
+            const uint32_t en = dlist[k];
+            const int dx = (int)(en & 0xffffu) - ax + HALF, dy = (int)(en >> 16) - ay + HALF;
+            if ((unsigned)dx < (unsigned)WW && (unsigned)dy < (unsigned)WW) {
+                const int cc = dy * WW + dx;
+                ot[cc] = (S)ZS_THING_DEADBODY;
+                ot[PLANE + cc] = (S)0;
+            }
+        }
+        if (ndead < 0 && !(ZS_OBS_DIAG & 32)) {  // more bodies than the list holds: the per-word scan
             const int c_lo = (ay - HALF) * W, c_hi = (ay + HALF + 1) * W;  // the window's rows
+            // maps whose rows are whole words: the window's columns as a mask of each word's bits
+            const int x0 = ax - HALF, wpr = W >> 5;
+            const bool rowwords = (W & 31) == 0;
 #pragma unroll
             for (int i = 0; i < OBS_PF_D; i++) {
                 const int w = lane + 64 * i;
                 uint32_t bits = w < d.DW ? deadl[w] : 0u;
                 if (32 * w + 31 < c_lo || 32 * w >= c_hi) bits = 0u;
+                if (rowwords) {  // columns [x0 - base, x0 - base + 21) of this word's 32
+                    const int lo = x0 - 32 * (w - (w / wpr) * wpr);
+                    const uint32_t m_hi = lo + WW >= 32 ? 0xffffffffu : (lo + WW <= 0 ? 0u : ((1u << (lo + WW)) - 1u));
+                    const uint32_t m_lo = lo <= 0 ? 0xffffffffu : (lo >= 32 ? 0u : ~((1u << lo) - 1u));
+                    bits &= m_hi & m_lo;
+                }
                 while (bits) {
                     const int c = 32 * w + __ffs(bits) - 1;
                     bits &= bits - 1u;
-                    const int y = c / W, x = c - y * W;
+                    const int y = d.w_m ? (int)(((uint32_t)c * d.w_m) >> 20) : c / W, x = c - y * W;
                     const int dx = x - ax + HALF, dy = y - ay + HALF;
                     if ((unsigned)dx < (unsigned)WW && (unsigned)dy < (unsigned)WW) {
                         const uint32_t sc = pad[(y + HALF) * PW + x + HALF] & 7u;
