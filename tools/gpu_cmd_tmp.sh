@@ -1,16 +1,9 @@
-cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
-for c in FETCH_SIZE WRITE_SIZE; do
-timeout -s KILL 120 rocprofv3 --pmc $c -T --output-format csv -d $PWD/gpurun_out/tickio_$c -o run -- ./tools/probe/tickio > gpurun_out/tickio_$c.log 2>&1 || exit 1
-done
-python3 - <<'PY'
-import csv, glob
-for c in ("FETCH_SIZE", "WRITE_SIZE"):
-    vals = {}
-    for f in glob.glob("gpurun_out/tickio_%s/**/*counter_collection.csv" % c, recursive=True):
-        for row in csv.DictReader(open(f)):
-            if "k_tick_io" in row["Kernel_Name"]:
-                vals.setdefault(row["Dispatch_Id"], 0.0)
-                vals[row["Dispatch_Id"]] += float(row["Counter_Value"])
-    print(c, [round(v) for k, v in sorted(vals.items(), key=lambda kv: int(kv[0]))])
-PY
-head -3 gpurun_out/tickio_FETCH_SIZE.log | tail -1; grep "k_tick_io read" gpurun_out/tickio_*.log
+#!/bin/bash
+# scratch GPU command of the current session (not part of the product)
+cd "$(dirname "$0")/.." || exit 2
+mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread \
+    -k "obstacle_hp or store_stream or kernel_paths or ring or c5_65536 or c3_65536_graph or set_state or golden" > gpurun_out/pytest_patch.log 2>&1 || { tail -40 gpurun_out/pytest_patch.log; exit 1; }
+tail -2 gpurun_out/pytest_patch.log
+CFGS="c5" VAR=ZS_OBS_RING VALS="0 1" STEPS=100 bash tools/ab_env.sh 2>&1 | tee gpurun_out/ab_ring5b.log
+TAG=r03b CFGS="c3 c2 c4 c5 n8" PCFGS="c3 c5" bash tools/profile_round.sh 2>&1 | tail -20
