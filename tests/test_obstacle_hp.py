@@ -211,3 +211,44 @@ def test_raise_kind_only_in_debug_envs():
                 assert eng.get_state(k).canonical([x[2] for x in eng.builder.map.obstacles]) == o.state()
         assert all(v == 0 for v in t)  # World.t advanced once from -1 either way
         eng.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [_abi.DTYPE_I16, _abi.DTYPE_I64])
+def test_patch_encoder_against_select_chain(dtype, monkeypatch):
+    """k_obs_patch (padded static table + per-env patches) against k_obs_lds's per-cell select chain
+    (itself pinned to the oracle) on the same poked states of bridge64 with 4 agents: 40 to 900
+    dead-body cells per env (more than PATCH_DEAD_CAP = 256 cells takes the per-word scan), bodies
+    under map obstacles, damaged and cleaned-up obstacles, a life below the int16 range."""
+    import torch
+    from libzombsole_amd.engine import Engine
+    n = 64
+
+    def cfg(k):
+        return _abi.multi_env_config(k, "extermination", [], "bridge64", ["0", "1", "2", "3"], initial_zombies=20,
+                                     obs_dtype=dtype)
+
+    obs = {}
+    for patch in ("1", "0"):
+        monkeypatch.setenv("ZS_OBS_LDS", "1")
+        monkeypatch.setenv("ZS_OBS_RING", "0")
+        monkeypatch.setenv("ZS_OBS_PATCH", patch)
+        eng = Engine(cfg(n))
+        eng.seed([900 + i for i in range(n)])
+        eng.reset()
+        rng = np.random.default_rng(11)
+        cells = eng.get_state(0).W * eng.get_state(0).H
+        for e in range(n):
+            st = eng.get_state(e)
+            dw = st.dead_words.view(np.uint32)  # writes through to the record
+            for c in rng.choice(cells, size=(40, 200, 300, 900)[e % 4], replace=False):
+                dw[int(c) >> 5] |= np.uint32(1 << (int(c) & 31))
+            for i in rng.choice(st.O, size=12, replace=False):
+                st.obst_life[i] = int(rng.integers(-40000, 199))
+                if st.obst_life[i] <= 0 and rng.integers(2):
+                    st.obst_present[i] = 0
+            eng.set_state(e, st)
+        obs[patch] = eng.observe().cpu().numpy().copy()
+        assert eng.describe()["obs_kernel"] == ("k_obs_patch" if patch == "1" else "k_obs_lds")
+        eng.close()
+    assert np.array_equal(obs["1"], obs["0"])
