@@ -167,8 +167,15 @@ def test_c2_4096_one_obs_workgroup_per_cu_cells(monkeypatch):
 
 
 def test_c5_65536_int16_graph():
-    """C5's engine side: 4 agents + 20 zombies, int16 observations (the gathered form)."""
+    """C5's engine side: 4 agents + 20 zombies, int16 observations (the gathered form); k_obs_ring
+    with the padded-table encoders."""
     run_full(c5, 65536, 32, min_resets=0)
+
+
+def test_c5_65536_int16_patch(monkeypatch):
+    """C5 through k_obs_patch (the padded-table encoder with per-wave flushes)."""
+    monkeypatch.setenv("ZS_OBS_RING", "0")
+    run_full(c5, 65536, 32, seed0=77, min_resets=0)
 
 
 def test_c5_65536_int16_truncation_waves():

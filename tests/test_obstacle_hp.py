@@ -56,9 +56,11 @@ def _poke_all(eng, pokes):
         eng.set_state(k, st)
 
 
-# observation kernels: the engine's pick for the size (int16 / int32: k_obs_patch), the store stream
-# forced at 64 envs (int64 too: k_obs_patch), and k_obs_lds's per-cell select chain
-OBS_PATHS = {"default": {}, "patch": {"ZS_OBS_LDS": "1"}, "lds_select": {"ZS_OBS_LDS": "1", "ZS_OBS_PATCH": "0"}}
+# observation kernels: the engine's pick for the size (int16: k_obs_ring, int32: k_obs_patch), the
+# store streams forced at 64 envs (int64 too: k_obs_patch, k_obs_ring), and k_obs_lds's select chain
+OBS_PATHS = {"default": {}, "patch": {"ZS_OBS_LDS": "1", "ZS_OBS_RING": "0"},
+             "ring": {"ZS_OBS_LDS": "1", "ZS_OBS_RING": "1"},
+             "lds_select": {"ZS_OBS_LDS": "1", "ZS_OBS_PATCH": "0", "ZS_OBS_RING": "0"}}
 
 
 @pytest.mark.gpu
