@@ -68,7 +68,11 @@ def parse():
     p.add_argument("--no-graph", action="store_true",
                    help="launch every step's kernels from the host instead of replaying the step as a hipGraph")
     p.add_argument("--cpu-steps", type=int, default=2000)
+    p.add_argument("--launch", default="",
+                   help="launch overrides for A/B runs, 'field=v,...' (zs_launch fields; 1 = on, -1 = off, n = size)")
+    p.add_argument("--engine-lib", default=None, help="(tools) another build of the engine's sources, e.g. an A/B build")
     a = p.parse_args()
+    a.launch = dict((kv.split("=")[0], int(kv.split("=")[1])) for kv in a.launch.split(",") if kv)
     for k, v in PRESETS[a.config].items():
         if getattr(a, k) is None:
             setattr(a, k, v)
@@ -170,11 +174,13 @@ def cpu_baseline(args, builder_fn):
 
 def env_range(rank, world, total_envs, envs_per_gpu=0):
     """(envs on this rank, first global env, scaling, node-wide envs): a fixed count per rank (weak
-    scaling) or the node's total split into contiguous ranges (strong)."""
+    scaling) or the node's total split into contiguous ranges by vector.shard_range, the partition
+    the batched API documents (strong)."""
+    from libzombsole_amd.vector import shard_range
     if envs_per_gpu:
         return envs_per_gpu, rank * envs_per_gpu, "weak", envs_per_gpu * world
-    env0 = rank * total_envs // world
-    return (rank + 1) * total_envs // world - env0, env0, "strong", total_envs
+    env0, n = shard_range(total_envs, rank, world)
+    return n, env0, "strong", total_envs
 
 
 def timed_loop(one_step, steps, warmup, sync, distributed, before_timing=None):
@@ -215,7 +221,10 @@ def main():
     import torch.distributed as dist
 
     from libzombsole_amd import _abi
+    from libzombsole_amd import engine as engine_mod
     from libzombsole_amd.engine import Engine
+    if args.engine_lib:
+        engine_mod.use_library(args.engine_lib)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     # under torchrun (even --nproc-per-node 1) the ranks form an RCCL group: C5's gather then runs
@@ -235,12 +244,14 @@ def main():
     def builder(n):
         return _abi.multi_env_config(n, args.rules, [], args.map, agent_ids, initial_zombies=args.zombies,
                                      minimum_zombies=args.min_zombies, max_episode_steps=args.max_episode_steps,
-                                     obs_dtype=dtype, lanes_per_env=args.lanes_per_env)
+                                     obs_dtype=dtype, lanes_per_env=args.lanes_per_env).set_launch(args.launch)
 
     n_local, env0, scaling, total_envs = env_range(rank, world, args.envs, args.envs_per_gpu)
     eng = Engine(builder(n_local), device=dev)
     launch = eng.describe()
     launch["step_graph"] = not args.no_graph
+    if args.launch:
+        launch["overrides"] = args.launch
     eng.seed([env0 + i for i in range(n_local)])
     eng.reset()
     torch.cuda.synchronize()

@@ -134,6 +134,39 @@ typedef struct zs_map_desc {
     const int32_t* zombie_spawn_xy;
 } zs_map_desc;
 
+/* ---- launch overrides ----------------------------------------------------------
+ * zs_create picks every kernel and layout from the config and the env count.  A non-NULL
+ * zs_config.launch forces one of the alternatives it would pick elsewhere, or sizes a grid (parity
+ * tests run every alternative; A/B measurements compare them).  Every field: 0 = automatic.
+ * Switches: 1 = on, -1 = off.  The block is copied into the handle: no process-wide state, and
+ * no environment variable selects a kernel. */
+typedef struct zs_launch {
+    int32_t fused;           /* reset work inside the step launch (k_step) instead of its own launch  */
+    int32_t fobs;            /* observations written by the step launch itself                        */
+    int32_t tick_waves;      /* k_tick's register budget: 5 or 6 waves per SIMD                        */
+    int32_t lds_budget;      /* -1: largest optional LDS copies instead of the most resident workgroups */
+    int32_t rw_need;         /* RNG window words a plain step prefetches (32..512)                    */
+    int32_t reset_wgs;       /* reset-work workgroups of a fused step launch                          */
+    int32_t reset_stream;    /* -1: an unfused reset launch on the caller's stream, not a side stream  */
+    int32_t reset_lists;     /* -1: k_reset reads the spawn lists from HBM instead of LDS              */
+    int32_t reset_grid;      /* k_reset workgroups (pending-list mode)                                 */
+    int32_t defer_respawn;   /* 1: zombie respawn by k_respawn, -1: by the tick's leader               */
+    int32_t respawn_grid;    /* k_respawn workgroups                                                   */
+    int32_t obs_pipe;        /* -1: no prefetching store-stream observation kernel (k_obs_pipe family) */
+    int32_t obs_lds;         /* k_obs_lds's LDS-staged 16-B stores (and its patch / ring variants)     */
+    int32_t obs_patch;       /* the padded-table encoder kernel k_obs_patch                            */
+    int32_t obs_ring;        /* encoder / writer waves through an LDS ring (k_obs_ring)                */
+    int32_t obs_ring_patch;  /* k_obs_ring with the padded-table encoders                              */
+    int32_t obs_gather;      /* -1: no k_obs_gather (large maps then use k_obs)                        */
+    int32_t obs_gather_stat; /* -1: k_obs_gather reads static words from HBM instead of LDS tables     */
+    int32_t obs_stat;        /* -1: per-cell static words instead of LDS bitmaps                       */
+    int32_t obs_win;         /* -1: per-cell entity scan instead of the window map                     */
+    int32_t obs_wgs;         /* observation workgroups per CU (store-stream kernels)                   */
+    int32_t par_exec;        /* -1: the leader lane executes the shuffled actions serially instead of
+                              * the env's lanes in parallel (core.py:103-119)                          */
+    int32_t reserved[10];
+} zs_launch;
+
 typedef struct zs_config {
     int32_t num_envs;
     zs_map_desc map;
@@ -153,6 +186,7 @@ typedef struct zs_config {
     int32_t max_episode_steps;    /* 0 = none; else TimeLimit-style truncation       */
     uint32_t flags;               /* ZS_FLAG_*                                       */
     int32_t lanes_per_env;        /* k_tick lanes per env (1..64, power of 2); 0 = auto */
+    const zs_launch* launch;      /* NULL = every launch choice automatic                 */
 } zs_config;
 
 typedef struct zs_handle zs_handle;

@@ -50,6 +50,16 @@ class zs_map_desc(C.Structure):
                 ("n_zombie_spawns", C.c_int32), ("zombie_spawn_xy", C.POINTER(C.c_int32))]
 
 
+LAUNCH_FIELDS = ["fused", "fobs", "tick_waves", "lds_budget", "rw_need", "reset_wgs", "reset_stream", "reset_lists",
+                 "reset_grid", "defer_respawn", "respawn_grid", "obs_pipe", "obs_lds", "obs_patch", "obs_ring",
+                 "obs_ring_patch", "obs_gather", "obs_gather_stat", "obs_stat", "obs_win", "obs_wgs", "par_exec"]
+
+
+class zs_launch(C.Structure):
+    """Launch overrides (include/zombsole_mi355x.h): 0 = automatic; switches 1 = on, -1 = off."""
+    _fields_ = [(f, C.c_int32) for f in LAUNCH_FIELDS] + [("reserved", C.c_int32 * 10)]
+
+
 class zs_config(C.Structure):
     _fields_ = [("num_envs", C.c_int32), ("map", zs_map_desc), ("rules", C.c_int32),
                 ("num_agents", C.c_int32), ("agent_weapons", C.POINTER(C.c_int32)),
@@ -58,7 +68,8 @@ class zs_config(C.Structure):
                 ("initial_zombies", C.c_int32), ("minimum_zombies", C.c_int32),
                 ("reward_mode", C.c_int32), ("obs_scope", C.c_int32), ("obs_encoding", C.c_int32),
                 ("obs_width", C.c_int32), ("obs_dtype", C.c_int32),
-                ("max_episode_steps", C.c_int32), ("flags", C.c_uint32), ("lanes_per_env", C.c_int32)]
+                ("max_episode_steps", C.c_int32), ("flags", C.c_uint32), ("lanes_per_env", C.c_int32),
+                ("launch", C.POINTER(zs_launch))]
 
 
 def rules_id(rules_name):
@@ -167,6 +178,28 @@ class ConfigBuilder(object):
                              int(obs_dtype), int(max_episode_steps),
                              (FLAG_AUTORESET if autoreset else 0) | (FLAG_DEBUG if debug else 0),
                              int(lanes_per_env))
+        self._launch = None
+
+    def set_launch(self, overrides):
+        """Force launch alternatives for the handles built from this config: a dict of zs_launch fields
+        (LAUNCH_FIELDS), e.g. {"fused": -1, "obs_ring": 1}; None or {} = every choice automatic."""
+        if not overrides:
+            self._launch = None
+            self.cfg.launch = C.POINTER(zs_launch)()
+            return self
+        unknown = set(overrides) - set(LAUNCH_FIELDS)
+        if unknown:
+            raise ValueError("unknown launch overrides: %s" % sorted(unknown))
+        self._launch = zs_launch(**{k: int(v) for k, v in overrides.items()})
+        self.cfg.launch = C.pointer(self._launch)
+        return self
+
+    @property
+    def launch(self):
+        """The overrides set on this config, as a dict of the non-zero fields."""
+        if self._launch is None:
+            return {}
+        return {f: getattr(self._launch, f) for f in LAUNCH_FIELDS if getattr(self._launch, f)}
 
     @property
     def num_agents(self):

@@ -20,26 +20,9 @@
 
 #include "zs_device.hpp"
 
+#include "zs_launch.hpp"
 #include "zs_reset.hpp"
 #include "zs_obs.hpp"
-
-// One launch per step: workgroups [0, n_reset) rebuild the envs of the pending list (next-step
-// autoreset, World rebuilt as in game.py:151-169), the others tick every other env (zs_tick.hpp).
-// An env is either pending (reset work only; the tick reports it as reset without touching its
-// state) or stepping (tick only), so the two roles never share an env.
-template <int G>
-__global__ void __launch_bounds__(64, ZS_FUSED_WAVES) k_step(Dev d, int n_reset, const int32_t* actions, double* rew,
-                                             uint8_t* done_out, uint8_t* trunc_out, uint8_t* listed_out,
-                                             uint8_t* reset_out, int* reset_list, int* reset_count,
-                                             const int* cur_list, const int* cur_count, int* err_out, void* obs_out) {
-    TL(0);
-    if ((int)blockIdx.x < n_reset)
-        reset_role(d, 1, cur_list, cur_count, nullptr, err_out, blockIdx.x, n_reset, d.fobs ? obs_out : nullptr);
-    else
-        tick_wg<G>(d, xcd_remap(blockIdx.x - n_reset, gridDim.x - n_reset), actions, rew, done_out, trunc_out,
-                   listed_out, reset_out, reset_list, reset_count, obs_out, 0, d.N);
-    TL(1);
-}
 
 // ---------------------------------------------------------------------------
 // seeding: random.seed(int) (init_by_array over abs(n) in 32-bit little-endian words)
@@ -234,6 +217,16 @@ static int fail(int code, const std::string& msg) {
     return code;
 }
 
+// the observation launcher of the handle's output dtype (k_obs_t.hip)
+static hipError_t obs_launch(int dtype, const ObsLaunch& o, hipStream_t s, const Dev& d) {
+    return dtype == ZS_DTYPE_I64 ? launch_obs_i64(o, s, d) : dtype == ZS_DTYPE_I32 ? launch_obs_i32(o, s, d) : launch_obs_i16(o, s, d);
+}
+static hipError_t obs_attr(int dtype, int kind, int nobs, int patched, int bytes) {
+    return dtype == ZS_DTYPE_I64   ? obs_lds_attr_i64(kind, nobs, patched, bytes)
+           : dtype == ZS_DTYPE_I32 ? obs_lds_attr_i32(kind, nobs, patched, bytes)
+                                   : obs_lds_attr_i16(kind, nobs, patched, bytes);
+}
+
 #define HIPCHK(x)                                                                              \
     do {                                                                                       \
         hipError_t _e = (x);                                                                   \
@@ -242,6 +235,7 @@ static int fail(int code, const std::string& msg) {
 
 struct zs_handle {
     zs_config cfg;
+    zs_launch ov;   // launch overrides (zs_config.launch, zeroed when NULL)
     int device;
     Dev d;
     int G;          // lanes per env in k_tick
@@ -251,14 +245,14 @@ struct zs_handle {
     int obs_wpg;      // k_obs waves (envs) per workgroup
     int obs_pipe = 0;      // k_obs_pipe<NOBS> usable (NOBS = 1, 2, 4), else 0
     int obs_lds = 0;       // k_obs_pipe's walk with LDS-staged 16-B stores (k_obs_lds), channels encoding
-    int obs_ring = 0;      // k_obs_ring: encoder and writer waves through an LDS ring (ZS_OBS_RING)
+    int obs_ring = 0;      // k_obs_ring: encoder and writer waves through an LDS ring (zs_launch.obs_ring)
     size_t obs_ring_bytes = 0;
     size_t obs_lds_bytes = 0;
-    int obs_patch = 0;     // k_obs_lds's walk with the padded-table encoder (k_obs_patch, ZS_OBS_PATCH)
+    int obs_patch = 0;     // k_obs_lds's walk with the padded-table encoder (k_obs_patch, zs_launch.obs_patch)
     size_t obs_patch_bytes = 0;
     int obs_patch_wgs = 2;  // its workgroups (PATCH_WPG waves) per CU
     int obs_gather = 0;    // else k_obs_gather<NOBS> usable (NOBS = 1, 2, 4), else 0 (k_obs)
-    int obs_gather_stat = 0;    // k_obs_gather reads the static words from LDS tables (ZS_OBS_GATHER_STAT)
+    int obs_gather_stat = 0;    // k_obs_gather reads the static words from LDS tables (zs_launch.obs_gather_stat)
     ObsLayout obs_gl;      // its per-wave image
     // zs_step_graph: one captured hipGraph per autoreset-list parity (the step alternates the two
     // pending-reset lists), replayed on the caller's stream; keyed by the caller's buffers
@@ -399,16 +393,8 @@ static int validate(const zs_config* c) {
 // workgroups (at most 32 one-wave workgroups per CU), then the largest optional LDS copies (RNG
 // window beyond 64 words, spawn candidates, spawn lists).  A fused launch (reset work + tick in
 // one) allocates max(tick image, reset image) for every workgroup.
-// reset-work workgroups of a fused step launch (ZS_RESET_WGS overrides)
-static int reset_wgs() {
-    static const int n = getenv("ZS_RESET_WGS") ? std::max(1, atoi(getenv("ZS_RESET_WGS"))) : 256;
-    return n;
-}
-
-static bool getenv_off(const char* name) {
-    const char* f = getenv(name);
-    return f && atoi(f) == 0;
-}
+// reset-work workgroups of a fused step launch (zs_launch.reset_wgs overrides)
+static int reset_wgs(const zs_handle* h) { return h->ov.reset_wgs > 0 ? h->ov.reset_wgs : 256; }
 
 static int choose_layout(zs_handle* h, int want_g, bool fused, int obs_bytes) {
     Dev& d = h->d;
@@ -429,12 +415,12 @@ static int choose_layout(zs_handle* h, int want_g, bool fused, int obs_bytes) {
     // max 63; C4 (E = 54) median 82.  2E + 8 rounded up to a power of two covers them.
     int rw_need = 32;
     while (rw_need < 512 && rw_need < 2 * d.E + 8) rw_need *= 2;
-    if (getenv("ZS_RW_NEED")) rw_need = std::max(32, std::min(512, atoi(getenv("ZS_RW_NEED"))));
+    if (h->ov.rw_need > 0) rw_need = std::max(32, std::min(512, (int)h->ov.rw_need));
     int lists = (d.nps + d.nzs <= 4096) ? d.nps + d.nzs : 0;
     for (int G = g0; G <= 64; G *= 2) {
         int ne = 64 / G;
-        int wgs = (d.N + ne - 1) / ne + (fused ? std::min(d.N, reset_wgs()) : 0);
-        int want = getenv_off("ZS_LDS_BUDGET") ? 1 : std::min(32, std::max(1, (wgs + 255) / 256));
+        int wgs = (d.N + ne - 1) / ne + (fused ? std::min(d.N, reset_wgs(h)) : 0);
+        int want = h->ov.lds_budget < 0 ? 1 : std::min(32, std::max(1, (wgs + 255) / 256));
         int best_res = -1;
         for (int pass = 0; pass < 2 && best_res < 0; pass++)  // windows below the need only if nothing else fits
         for (int cand : {cand_full, 0})
@@ -469,6 +455,9 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
     HIPCHK(hipSetDevice(device));
     zs_handle* h = new zs_handle();
     h->cfg = *cfg;
+    memset(&h->ov, 0, sizeof(h->ov));
+    if (cfg->launch) h->ov = *cfg->launch;
+    h->cfg.launch = nullptr;
     h->device = device;
     const zs_map_desc& m = cfg->map;
     Dev& d = h->d;
@@ -498,13 +487,16 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
     d.minimum_zombies = cfg->minimum_zombies;
     d.flags = cfg->flags;
     // zombie respawn as wave work after the tick (k_respawn) when its shuffle is long: the tick's
-    // leader would draw one word per candidate serially.  ZS_DEFER_RESPAWN=0/1 forces either.
+    // leader would draw one word per candidate serially.  zs_launch.defer_respawn forces either.
     {
         const int cands = m.n_zombie_spawns ? m.n_zombie_spawns : d.W * d.H;
-        const char* dr = getenv("ZS_DEFER_RESPAWN");
-        d.defer_respawn = d.minimum_zombies > 0 && (dr ? atoi(dr) != 0 : cands > 64);
+        const int dr = h->ov.defer_respawn;
+        d.defer_respawn = d.minimum_zombies > 0 && (dr ? dr > 0 : cands > 64);
     }
 
+    // the shuffle and execution of a tick's actions by the env's lanes (zs_tick.hpp grp_execute) instead of
+    // its leader lane alone; zs_launch.par_exec = -1 keeps the leader's serial loop (A/B, parity tests)
+    d.par_exec = h->ov.par_exec >= 0;
     // static tables
     std::vector<int16_t> cellmap((size_t)d.W * d.H, -1);
     std::vector<int32_t> oxy(d.O);
@@ -699,12 +691,12 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
         // observation images: k_obs (four envs per workgroup when their images fit 64 KiB, else one;
         // window map and staged HP while one image fits 32 KiB) and, when the step launch writes the
         // observations itself (fobs), one env's image inside the tick / reset LDS (HP staged when the
-        // image still fits the MT twist buffer it aliases).  ZS_OBS_WIN=0 forces the per-cell
+        // image still fits the MT twist buffer it aliases).  zs_launch.obs_win forces the per-cell
         // entity scan (parity tests of that path).
         const bool world = d.obs_scope == ZS_OBS_WORLD;
         const int nobs = obs_count(d.obs_scope, d.reward_mode, d.A);
         const int plane = world ? d.W * d.H : d.obs_w * d.obs_w;
-        const bool win = !getenv_off("ZS_OBS_WIN");
+        const bool win = h->ov.obs_win >= 0;
         ObsLayout L = obs_layout(nobs, plane, d.E, d.DW, d.OW, d.O, win, true);
         if (L.bytes > 32 * 1024) L = obs_layout(nobs, plane, d.E, d.DW, d.OW, d.O, win, false);
         if (L.bytes > 32 * 1024) L = obs_layout(nobs, plane, d.E, d.DW, d.OW, d.O, false, false);
@@ -714,34 +706,34 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
             return fail(ZS_EINVAL, "map too large for the observation kernel's LDS image");
         }
         // static tables (4 x DW words) beside the images: per k_obs workgroup, and inside the step
-        // launch's image region; ZS_OBS_STAT=0 forces the per-cell static words (parity tests)
-        d.obs_stat = (rank_order && d.DW <= 1024 && !getenv_off("ZS_OBS_STAT")) ? 4 * d.DW : 0;
+        // launch's image region; zs_launch.obs_stat forces the per-cell static words (parity tests)
+        d.obs_stat = (rank_order && d.DW <= 1024 && h->ov.obs_stat >= 0) ? 4 * d.DW : 0;
         h->obs_l = L;
         h->obs_wpg = d.obs_stat * 4 + 4 * L.bytes <= 64 * 1024 ? 4 : 1;
         // k_obs_pipe: surroundings of width 21, 1/2/4 observations, static tables, staged HP, window
-        // map, every entity on its own lane, prefetch arrays large enough (ZS_OBS_PIPE=0 disables)
+        // map, every entity on its own lane, prefetch arrays large enough (zs_launch.obs_pipe disables)
         if (!world && d.obs_w == 21 && (nobs == 1 || nobs == 2 || nobs == 4) && d.obs_stat && L.hp_cap && L.win &&
             d.O > 0 && d.E <= 64 && d.DW <= 64 * OBS_PF_D && d.O <= 64 * OBS_PF_H && d.OW <= 64 &&
-            d.obs_stat * 4 + 4 * L.bytes <= 64 * 1024 && !getenv_off("ZS_OBS_PIPE")) {
+            d.obs_stat * 4 + 4 * L.bytes <= 64 * 1024 && h->ov.obs_pipe >= 0) {
             h->obs_pipe = nobs;
             // two workgroups (8 waves) per CU: measured at 65536 envs, 0.350 ms per launch against 0.375
             // at 8 and 0.38 at 3-4 (a smaller set of env blocks in flight at once); one contiguous env
             // range per wave instead of the strided walk measured slower (0.383)
             h->obs_pipe_wgs = std::max(1, std::min(2, 160 * 1024 / (d.obs_stat * 4 + 4 * L.bytes)));
-            if (getenv("ZS_OBS_WGS")) h->obs_pipe_wgs = std::max(1, std::min(32, atoi(getenv("ZS_OBS_WGS"))));
+            if (h->ov.obs_wgs > 0) h->obs_pipe_wgs = std::min(32, (int)h->ov.obs_wgs);
         }
         // k_obs_lds: the same walk with each observation block staged in LDS and streamed out as 16-B
         // stores (channels encoding).  Measured on one MI355X: int16 blocks (C5) 341 -> 264 us per
         // launch at 4 workgroups per CU (2: 334, 3: 278, 5: 307); int64 blocks (staged as int32) at
         // up to 4 per CU.  It pays when every wave walks several envs (C3 65536 envs; at 8192, one env
-        // per wave, k_obs_pipe's per-cell stores measured 33 vs 36 us).  ZS_OBS_LDS=0/1 forces either,
-        // ZS_OBS_WGS sets the workgroups per CU.
-        if (h->obs_pipe && d.obs_enc == ZS_ENC_CHANNELS && !getenv_off("ZS_OBS_LDS")) {
+        // per wave, k_obs_pipe's per-cell stores measured 33 vs 36 us).  zs_launch.obs_lds forces either,
+        // zs_launch.obs_wgs sets the workgroups per CU.
+        if (h->obs_pipe && d.obs_enc == ZS_ENC_CHANNELS && h->ov.obs_lds >= 0) {
             const int ts = d.obs_dtype == ZS_DTYPE_I64 ? 8 : d.obs_dtype == ZS_DTYPE_I32 ? 4 : 2;
             const size_t lb = (size_t)d.obs_stat * 4 + 4 * ((size_t)L.bytes + (size_t)obs_stage_slot_bytes(ts));
             int wgs = std::max(1, std::min(ts == 8 ? 2 : 4, (int)(160 * 1024 / lb)));
-            if (getenv("ZS_OBS_WGS")) wgs = std::max(1, std::min(32, atoi(getenv("ZS_OBS_WGS"))));
-            const bool forced = getenv("ZS_OBS_LDS") != nullptr;
+            if (h->ov.obs_wgs > 0) wgs = std::min(32, (int)h->ov.obs_wgs);
+            const bool forced = h->ov.obs_lds > 0;
             const bool pays = ts < 8 || (long)d.N >= 24L * 256 * 2 * 4;
             if (lb <= 64 * 1024 && (pays || forced)) {
                 h->obs_lds = 1;
@@ -750,67 +742,44 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
             }
         }
         // k_obs_patch: k_obs_lds with the padded-table encoder (maps up to 4095 x 4095, rows of the
-        // padded table in the workgroup's LDS).  ZS_OBS_PATCH=0/1 forces either.
+        // padded table in the workgroup's LDS).  zs_launch.obs_patch forces either.
         if (h->obs_lds && d.OW <= 64 && (long)(d.W + 20) * 21 < 65536 && d.H < 4096) {
             const int ts = d.obs_dtype == ZS_DTYPE_I64 ? 8 : d.obs_dtype == ZS_DTYPE_I32 ? 4 : 2;
             const size_t pb = (size_t)patch_static_bytes(d.opad_n, d.O) +
                               PATCH_WPG * (size_t)patch_wave_bytes(d.DW, d.O, obs_stage_slot_bytes(ts));
-            const char* pz = getenv("ZS_OBS_PATCH");
-            const void* fn = nullptr;
+            const int pz = h->ov.obs_patch;
             const int nobs = obs_count(d.obs_scope, d.reward_mode, d.A);
-#define ZS_PATCH_FN(TT)                                                                             \
-    fn = nobs == 1 ? (const void*)k_obs_patch<TT, 1> : nobs == 2 ? (const void*)k_obs_patch<TT, 2> \
-                                                                 : (const void*)k_obs_patch<TT, 4>
-            if (ts == 8) ZS_PATCH_FN(int64_t);
-            else if (ts == 4) ZS_PATCH_FN(int32_t);
-            else ZS_PATCH_FN(int16_t);
-#undef ZS_PATCH_FN
-            if (pb <= 160 * 1024 && (pz ? atoi(pz) != 0 : true) &&
-                hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pb) == hipSuccess) {
+            if (pb <= 160 * 1024 && pz >= 0 &&
+                obs_attr(d.obs_dtype, OBSK_PATCH, nobs, 0, (int)pb) == hipSuccess) {
                 h->obs_patch = 1;
                 h->obs_patch_bytes = pb;
                 h->obs_patch_wgs = std::max(1, (int)(160 * 1024 / pb));
-                if (getenv("ZS_OBS_WGS")) h->obs_patch_wgs = std::max(1, std::min(32, atoi(getenv("ZS_OBS_WGS"))));
+                if (h->ov.obs_wgs > 0) h->obs_patch_wgs = std::min(32, (int)h->ov.obs_wgs);
             }
         }
         // k_obs_ring (zs_obs.hpp): the k_obs_lds shape with dedicated writer waves.  Measured on one
         // MI355X (2 runs each): C3 (int64) observations 292 / 280 -> 285 / 273 us; C5 (int16) even.
-        // Default for int64 blocks; ZS_OBS_RING=0/1 forces either.
+        // Default for int64 blocks; zs_launch.obs_ring forces either.
         if (h->obs_lds && d.obs_enc == ZS_ENC_CHANNELS) {
             const int ts = d.obs_dtype == ZS_DTYPE_I64 ? 8 : d.obs_dtype == ZS_DTYPE_I32 ? 4 : 2;
-            // the ring's encoders are k_obs_patch's when its tables fit (ZS_OBS_RING_PATCH=0/1 forces either)
-            const char* rp = getenv("ZS_OBS_RING_PATCH");
-            const bool patched = h->obs_patch && (rp ? atoi(rp) != 0 : true);
+            // the ring's encoders are k_obs_patch's when its tables fit (zs_launch.obs_ring_patch forces either)
+            const bool patched = h->obs_patch && h->ov.obs_ring_patch >= 0;
             const size_t rb = patched ? (size_t)ring_lds_bytes(patch_static_bytes(d.opad_n, d.O), patch_enc_bytes(d.DW, d.O), ts, nobs)
                                       : (size_t)ring_lds_bytes(16 * d.DW, L.bytes, ts, nobs);
-            const char* rg = getenv("ZS_OBS_RING");
+            const int rg = h->ov.obs_ring;
             // default for int64 blocks, and for int16 ones with the padded-table encoders (C5 on one MI355X,
             // 2 runs each: 215.2 / 216.5 us against k_obs_patch's 222.7 / 223.0)
-            if (rb <= 160 * 1024 && (rg ? atoi(rg) != 0 : ts == 8 || (patched && ts == 2))) {
-                const void* fn = nullptr;
-#define ZS_RING_FN(TT, P)                                                                      \
-    fn = nobs == 1 ? (const void*)k_obs_ring<TT, 1, P> : nobs == 2 ? (const void*)k_obs_ring<TT, 2, P> \
-                                                                   : (const void*)k_obs_ring<TT, 4, P>
-                if (patched) {
-                    if (ts == 8) ZS_RING_FN(int64_t, true);
-                    else if (ts == 4) ZS_RING_FN(int32_t, true);
-                    else ZS_RING_FN(int16_t, true);
-                } else {
-                    if (ts == 8) ZS_RING_FN(int64_t, false);
-                    else if (ts == 4) ZS_RING_FN(int32_t, false);
-                    else ZS_RING_FN(int16_t, false);
-                }
-#undef ZS_RING_FN
-                if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)rb) == hipSuccess) {
+            if (rb <= 160 * 1024 && (rg ? rg > 0 : ts == 8 || (patched && ts == 2))) {
+                if (obs_attr(d.obs_dtype, OBSK_RING, nobs, patched ? 1 : 0, (int)rb) == hipSuccess) {
                     h->obs_ring = patched ? 2 : 1;
                     h->obs_ring_bytes = rb;
                 }
             }
         }
         // k_obs_gather when the store-stream kernel does not apply (e.g. city128's 3689 obstacles):
-        // window-only static words and HP instead of per-env staging.  ZS_OBS_GATHER=0 disables.
+        // window-only static words and HP instead of per-env staging.  zs_launch.obs_gather disables.
         if (!h->obs_pipe && !world && d.obs_w == 21 && (nobs == 1 || nobs == 2 || nobs == 4) &&
-            !getenv_off("ZS_OBS_GATHER")) {
+            h->ov.obs_gather >= 0) {
             ObsLayout G = obs_layout(nobs, plane, d.E, d.DW, d.OW, d.O, true, false);
             if (4 * G.bytes <= 64 * 1024) {
                 h->obs_gather = nobs;
@@ -818,33 +787,32 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
                 // static words from the LDS tables (rank order, as obs_stat) instead of a global load
                 // round per window cell
                 const size_t gb = 4 * (size_t)G.bytes;
-                h->obs_gather_stat = d.obs_stat && gb + 16 * (size_t)d.DW <= 64 * 1024 && !getenv_off("ZS_OBS_GATHER_STAT");
+                h->obs_gather_stat = d.obs_stat && gb + 16 * (size_t)d.DW <= 64 * 1024 && h->ov.obs_gather_stat >= 0;
             }
         }
         // with the store-stream kernel available the observations are its job (measured faster than
-        // writing them from the tick workgroups at both 8192 and 65536 envs); ZS_FOBS=1 forces them
+        // writing them from the tick workgroups at both 8192 and 65536 envs); zs_launch.fobs forces them
         // into the step launch
         d.obsl = L;
-        d.fobs = L.bytes + 4 * d.obs_stat <= 16 * 1024 && !getenv_off("ZS_FOBS");
-        if (h->obs_pipe && !(getenv("ZS_FOBS") && atoi(getenv("ZS_FOBS")) != 0)) d.fobs = 0;
+        d.fobs = L.bytes + 4 * d.obs_stat <= 16 * 1024 && h->ov.fobs >= 0;
+        if (h->obs_pipe && h->ov.fobs <= 0) d.fobs = 0;
         if (d.defer_respawn) d.fobs = 0;  // the observations must see k_respawn's zombies
     }
     // Fused step launch (reset work + tick in one) when the whole launch is resident at once: then
     // the step is one latency-bound round and the reset work hides under the ticks (measured: 8192
     // envs, 1 round, fused 0.097 ms vs 0.13 ms).  With many rounds per CU (65536 envs) the reset
     // image and the reset role's registers cost every tick workgroup occupancy, so the reset work
-    // runs as its own short launch (0.54 ms vs 0.59 ms).  ZS_FUSED=0/1 forces either.
+    // runs as its own short launch (0.54 ms vs 0.59 ms).  zs_launch.fused forces either.
     {
         const int obs_b = d.fobs ? d.obsl.bytes + 4 * d.obs_stat : 0;
         TRY(choose_layout(h, cfg->lanes_per_env, true, obs_b));
-        const char* fz = getenv("ZS_FUSED");
-        h->fused = fz ? atoi(fz) != 0 : h->resident >= h->want;
+        h->fused = h->ov.fused ? h->ov.fused > 0 : h->resident >= h->want;
         if (!h->fused) {
             TRY(choose_layout(h, cfg->lanes_per_env, false, obs_b));
             // k_tick's register budget: 5 waves per SIMD (96 VGPRs, 20 B of scratch per lane) unless 6 (80
             // VGPRs, 52 B of scratch on the leader's paths) saves a round of resident workgroups.  Measured
             // on one MI355X: C3 tick 95.6 -> 91.9 us and C4 185 -> 179 us at 5; C5 (16 384 workgroups:
-            // 2.7 rounds at 6 waves, 3.2 at 5) 167 -> 178 us.  ZS_TICK_WAVES=5/6 forces either.
+            // 2.7 rounds at 6 waves, 3.2 at 5) 167 -> 178 us.  zs_launch.tick_waves forces either.
             const int wgs = (d.N + 64 / h->G - 1) / (64 / h->G);
             const int lres = std::max(1, 160 * 1024 / (int)h->lds);
             auto rounds = [&](int w) {
@@ -852,14 +820,14 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
                 return (wgs + 256 * r - 1) / (256 * r);
             };
             h->tick_waves = rounds(5) <= rounds(6) ? 5 : 6;
-            if (getenv("ZS_TICK_WAVES") && atoi(getenv("ZS_TICK_WAVES")) > 0) h->tick_waves = atoi(getenv("ZS_TICK_WAVES")) == 5 ? 5 : 6;
+            if (h->ov.tick_waves > 0) h->tick_waves = h->ov.tick_waves == 5 ? 5 : 6;
             h->resident = std::min(h->resident, 4 * h->tick_waves);
         }
         // the reset launch stages the static spawn lists whenever they fit (no serial global loads in
         // its candidate filters); a fused launch shares the tick's choice
         d.rlists_cap = d.lists_cap;
         if (!h->fused && d.nps + d.nzs <= 4096 &&
-            reset_lds_bytes(d.E, d.DW, d.ncand, d.nps + d.nzs, obs_b) <= 64 * 1024 && !getenv_off("ZS_RESET_LISTS"))
+            reset_lds_bytes(d.E, d.DW, d.ncand, d.nps + d.nzs, obs_b) <= 64 * 1024 && h->ov.reset_lists >= 0)
             d.rlists_cap = d.nps + d.nzs;
         h->reset_lds = (size_t)reset_lds_bytes(d.E, d.DW, d.ncand, d.rlists_cap, obs_b);
     }
@@ -868,17 +836,13 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
         delete h;
         return fail(ZS_EINVAL, "map too large for the reset kernel's LDS image");
     }
-    // side-stream reset work (unfused steps; ZS_RESET_STREAM=0 keeps it on the caller's stream)
-    if (!h->fused && !getenv_off("ZS_RESET_STREAM")) {
+    // side-stream reset work (unfused steps; zs_launch.reset_stream keeps it on the caller's stream)
+    if (!h->fused && h->ov.reset_stream >= 0) {
         h->reset_side = hipStreamCreateWithFlags(&h->s_reset, hipStreamNonBlocking) == hipSuccess &&
                         hipEventCreateWithFlags(&h->ev_rfork, hipEventDisableTiming) == hipSuccess &&
                         hipEventCreateWithFlags(&h->ev_rjoin, hipEventDisableTiming) == hipSuccess;
     }
-    if (h->reset_lds > 64 * 1024 &&
-        (hipFuncSetAttribute((const void*)k_reset, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->reset_lds) !=
-             hipSuccess ||
-         hipFuncSetAttribute((const void*)k_respawn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->reset_lds) !=
-             hipSuccess)) {
+    if (h->reset_lds > 64 * 1024 && reset_lds_attr((int)h->reset_lds) != hipSuccess) {
         free_all(h);
         delete h;
         return fail(ZS_EHIP, "cannot raise k_reset's dynamic LDS limit");
@@ -952,128 +916,48 @@ static int launch_obs(zs_handle* h, void* obs, const uint8_t* mask, hipStream_t 
     int i0 = -1, i1 = -1;
     if (h->prof) HIPCHK(hipEventRecord(prof_event(h, &i0), s));
     if (env1 < 0) env1 = d.N;
+    ObsLaunch o;
+    memset(&o, 0, sizeof(o));
+    o.obs = obs;
+    o.mask = mask;
+    o.env0 = env0;
+    o.env1 = env1;
+    o.nobs = h->obs_pipe;
+    o.L = h->obs_l;
     if (!mask && h->obs_ring) {  // encoder / writer waves, one workgroup per CU
         const int ts = d.obs_dtype == ZS_DTYPE_I64 ? 8 : d.obs_dtype == ZS_DTYPE_I32 ? 4 : 2;
         const int pair = ring_pair(ts, h->obs_pipe);
-        const unsigned g = (unsigned)std::min((env1 - env0 + pair - 1) / pair, 256);
-        const size_t lds = h->obs_ring_bytes;
-#define ZS_RING(TT, NB)                                                                                          \
-    do {                                                                                                         \
-        if (h->obs_ring == 2)                                                                                    \
-            hipLaunchKernelGGL((k_obs_ring<TT, NB, true>), dim3(g), dim3(64 * (RING_ENC + RING_WRT)), lds, s, d, \
-                               (TT*)obs, h->obs_l, env0, env1);                                                  \
-        else                                                                                                     \
-            hipLaunchKernelGGL((k_obs_ring<TT, NB, false>), dim3(g), dim3(64 * (RING_ENC + RING_WRT)), lds, s, d, \
-                               (TT*)obs, h->obs_l, env0, env1);                                                  \
-    } while (0)
-#define ZS_RING_T(TT)                   \
-    if (h->obs_pipe == 1) ZS_RING(TT, 1); \
-    else if (h->obs_pipe == 2) ZS_RING(TT, 2); \
-    else ZS_RING(TT, 4)
-        if (d.obs_dtype == ZS_DTYPE_I64) {
-            ZS_RING_T(int64_t);
-        } else if (d.obs_dtype == ZS_DTYPE_I32) {
-            ZS_RING_T(int32_t);
-        } else {
-            ZS_RING_T(int16_t);
-        }
-#undef ZS_RING_T
-#undef ZS_RING
-        HIPCHK(hipGetLastError());
-        if (h->prof) {
-            HIPCHK(hipEventRecord(prof_event(h, &i1), s));
-            h->ev_obs.push_back({i0, i1});
-        }
-        return ZS_OK;
+        o.kind = OBSK_RING;
+        o.patched = h->obs_ring == 2;
+        o.grid = (unsigned)std::min((env1 - env0 + pair - 1) / pair, 256);
+        o.block = 64 * (RING_ENC + RING_WRT);
+        o.lds = h->obs_ring_bytes;
+    } else if (!mask && h->obs_patch) {  // every env of [env0, env1): the padded-table encoder's store stream
+        o.kind = OBSK_PATCH;
+        o.grid = (unsigned)std::min((env1 - env0 + PATCH_WPG - 1) / PATCH_WPG, 256 * h->obs_patch_wgs);
+        o.block = 64 * PATCH_WPG;
+        o.lds = h->obs_patch_bytes;
+    } else if (!mask && h->obs_pipe) {  // every env of [env0, env1), registered shape: the prefetching store stream
+        o.kind = h->obs_lds ? OBSK_LDS : OBSK_PIPE;
+        o.grid = (unsigned)std::min((env1 - env0 + 3) / 4, 256 * h->obs_pipe_wgs);
+        o.block = 256;
+        o.lds = h->obs_lds ? h->obs_lds_bytes : (size_t)d.obs_stat * 4 + 4 * (size_t)h->obs_l.bytes;
+    } else if (h->obs_gather) {  // one env per wave, four per workgroup, window-only fetches
+        o.kind = OBSK_GATHER;
+        o.nobs = h->obs_gather;
+        o.grid = (unsigned)((d.N + 3) / 4);
+        o.block = 256;
+        o.lds = 4 * (size_t)h->obs_gl.bytes + (h->obs_gather_stat ? 16 * (size_t)d.DW : 0);
+        o.L = h->obs_gl;
+        o.stat = h->obs_gather_stat;
+    } else {
+        o.kind = OBSK_OBS;
+        o.grid = (unsigned)((d.N + h->obs_wpg - 1) / h->obs_wpg);
+        o.block = 64 * h->obs_wpg;
+        o.lds = (size_t)d.obs_stat * 4 + (size_t)h->obs_wpg * h->obs_l.bytes;
+        o.stat = d.obs_stat;
     }
-    if (!mask && h->obs_patch) {  // every env of [env0, env1): the padded-table encoder's store stream
-        const unsigned g = (unsigned)std::min((env1 - env0 + PATCH_WPG - 1) / PATCH_WPG, 256 * h->obs_patch_wgs);
-        const size_t lds = h->obs_patch_bytes;
-#define ZS_PATCH(TT)                                                                                                   \
-    do {                                                                                                               \
-        if (h->obs_pipe == 1)                                                                                          \
-            hipLaunchKernelGGL((k_obs_patch<TT, 1>), dim3(g), dim3(64 * PATCH_WPG), lds, s, d, (TT*)obs, env0, env1);  \
-        else if (h->obs_pipe == 2)                                                                                     \
-            hipLaunchKernelGGL((k_obs_patch<TT, 2>), dim3(g), dim3(64 * PATCH_WPG), lds, s, d, (TT*)obs, env0, env1);  \
-        else                                                                                                           \
-            hipLaunchKernelGGL((k_obs_patch<TT, 4>), dim3(g), dim3(64 * PATCH_WPG), lds, s, d, (TT*)obs, env0, env1);  \
-    } while (0)
-        if (d.obs_dtype == ZS_DTYPE_I64) ZS_PATCH(int64_t);
-        else if (d.obs_dtype == ZS_DTYPE_I32) ZS_PATCH(int32_t);
-        else ZS_PATCH(int16_t);
-#undef ZS_PATCH
-        HIPCHK(hipGetLastError());
-        if (h->prof) {
-            HIPCHK(hipEventRecord(prof_event(h, &i1), s));
-            h->ev_obs.push_back({i0, i1});
-        }
-        return ZS_OK;
-    }
-    if (!mask && h->obs_pipe) {  // every env of [env0, env1), registered shape: the prefetching store stream
-        const unsigned g = (unsigned)std::min((env1 - env0 + 3) / 4, 256 * h->obs_pipe_wgs);
-        const size_t lds = h->obs_lds ? h->obs_lds_bytes : (size_t)d.obs_stat * 4 + 4 * (size_t)h->obs_l.bytes;
-#define ZS_PIPE(TT, NB)                                                                                                 \
-    do {                                                                                                                \
-        if (h->obs_lds)                                                                                                 \
-            hipLaunchKernelGGL((k_obs_lds<TT, NB>), dim3(g), dim3(256), lds, s, d, (TT*)obs, h->obs_l, env0, env1);   \
-        else                                                                                                            \
-            hipLaunchKernelGGL((k_obs_pipe<TT, NB>), dim3(g), dim3(256), lds, s, d, (TT*)obs, h->obs_l, env0, env1);   \
-    } while (0)
-#define ZS_PIPE_T(TT)                   \
-    if (h->obs_pipe == 1) ZS_PIPE(TT, 1); \
-    else if (h->obs_pipe == 2) ZS_PIPE(TT, 2); \
-    else ZS_PIPE(TT, 4)
-        if (d.obs_dtype == ZS_DTYPE_I64) {
-            ZS_PIPE_T(int64_t);
-        } else if (d.obs_dtype == ZS_DTYPE_I32) {
-            ZS_PIPE_T(int32_t);
-        } else {
-            ZS_PIPE_T(int16_t);
-        }
-#undef ZS_PIPE_T
-#undef ZS_PIPE
-        HIPCHK(hipGetLastError());
-        if (h->prof) {
-            HIPCHK(hipEventRecord(prof_event(h, &i1), s));
-            h->ev_obs.push_back({i0, i1});
-        }
-        return ZS_OK;
-    }
-    if (h->obs_gather) {  // one env per wave, four per workgroup, window-only fetches
-        const unsigned g = (unsigned)((d.N + 3) / 4);
-        const size_t lds = 4 * (size_t)h->obs_gl.bytes + (h->obs_gather_stat ? 16 * (size_t)d.DW : 0);
-#define ZS_GATH(TT, NB) \
-    hipLaunchKernelGGL((k_obs_gather<TT, NB>), dim3(g), dim3(256), lds, s, d, (TT*)obs, mask, h->obs_gl, h->obs_gather_stat)
-#define ZS_GATH_T(TT)                         \
-    if (h->obs_gather == 1) ZS_GATH(TT, 1);     \
-    else if (h->obs_gather == 2) ZS_GATH(TT, 2); \
-    else ZS_GATH(TT, 4)
-        if (d.obs_dtype == ZS_DTYPE_I64) {
-            ZS_GATH_T(int64_t);
-        } else if (d.obs_dtype == ZS_DTYPE_I32) {
-            ZS_GATH_T(int32_t);
-        } else {
-            ZS_GATH_T(int16_t);
-        }
-#undef ZS_GATH_T
-#undef ZS_GATH
-        HIPCHK(hipGetLastError());
-        if (h->prof) {
-            HIPCHK(hipEventRecord(prof_event(h, &i1), s));
-            h->ev_obs.push_back({i0, i1});
-        }
-        return ZS_OK;
-    }
-    const unsigned grid = (unsigned)((d.N + h->obs_wpg - 1) / h->obs_wpg);
-    const dim3 blk(64 * h->obs_wpg);
-    const size_t lds = (size_t)d.obs_stat * 4 + (size_t)h->obs_wpg * h->obs_l.bytes;
-    if (d.obs_dtype == ZS_DTYPE_I64)
-        hipLaunchKernelGGL(k_obs<int64_t>, dim3(grid), blk, lds, s, d, (int64_t*)obs, mask, h->obs_l, d.obs_stat);
-    else if (d.obs_dtype == ZS_DTYPE_I32)
-        hipLaunchKernelGGL(k_obs<int32_t>, dim3(grid), blk, lds, s, d, (int32_t*)obs, mask, h->obs_l, d.obs_stat);
-    else
-        hipLaunchKernelGGL(k_obs<int16_t>, dim3(grid), blk, lds, s, d, (int16_t*)obs, mask, h->obs_l, d.obs_stat);
-    HIPCHK(hipGetLastError());
+    HIPCHK(obs_launch(d.obs_dtype, o, s, d));
     if (h->prof) {
         HIPCHK(hipEventRecord(prof_event(h, &i1), s));
         h->ev_obs.push_back({i0, i1});
@@ -1092,30 +976,35 @@ static int launch_tick(zs_handle* h, const int32_t* actions, double* rew, uint8_
     const int p = h->rpar;
     // fused: the first n_reset workgroups rebuild the envs of the pending list (ended at the previous
     // call) while the others tick every other env; the two sets of envs are disjoint
-    const int n_reset = std::min(d.N, reset_wgs());
+    const int n_reset = std::min(d.N, reset_wgs(h));
     if (h->prof) HIPCHK(hipEventRecord(prof_event(h, &i0), s));
-#define ZS_TICK(GG)                                                                                                   \
-    if (h->fused)                                                                                                     \
-        hipLaunchKernelGGL(k_step<GG>, dim3(grid + n_reset), dim3(64), h->lds, s, d, n_reset, actions, rew, done,    \
-                           trunc, listed, reset_out, rlist, rcount, (const int*)h->d_rlist[p],                        \
-                           (const int*)(h->d_rcount + p), h->d_err, obs);                                             \
-    else if (h->tick_waves == 5)                                                                                      \
-        hipLaunchKernelGGL((k_tick<GG, 5>), dim3(grid), dim3(64), h->lds, s, d, actions, rew, done, trunc, listed,   \
-                           reset_out, rlist, rcount, obs, env0, env1);                                                \
-    else                                                                                                              \
-        hipLaunchKernelGGL((k_tick<GG, 6>), dim3(grid), dim3(64), h->lds, s, d, actions, rew, done, trunc, listed,   \
-                           reset_out, rlist, rcount, obs, env0, env1)
+    TickArgs a;
+    a.actions = actions;
+    a.rew = rew;
+    a.done = done;
+    a.trunc = trunc;
+    a.listed = listed;
+    a.reset_out = reset_out;
+    a.rlist = rlist;
+    a.rcount = rcount;
+    a.obs = obs;
+    a.env0 = env0;
+    a.env1 = env1;
+    a.n_reset = h->fused ? n_reset : 0;
+    a.cur_list = (const int*)h->d_rlist[p];
+    a.cur_count = (const int*)(h->d_rcount + p);
+    a.err = h->d_err;
+    hipError_t le;
     switch (h->G) {
-    case 1: ZS_TICK(1); break;
-    case 2: ZS_TICK(2); break;
-    case 4: ZS_TICK(4); break;
-    case 8: ZS_TICK(8); break;
-    case 16: ZS_TICK(16); break;
-    case 32: ZS_TICK(32); break;
-    default: ZS_TICK(64); break;
+    case 1: le = launch_tick_g1(h->fused, h->tick_waves, grid, h->lds, s, d, a); break;
+    case 2: le = launch_tick_g2(h->fused, h->tick_waves, grid, h->lds, s, d, a); break;
+    case 4: le = launch_tick_g4(h->fused, h->tick_waves, grid, h->lds, s, d, a); break;
+    case 8: le = launch_tick_g8(h->fused, h->tick_waves, grid, h->lds, s, d, a); break;
+    case 16: le = launch_tick_g16(h->fused, h->tick_waves, grid, h->lds, s, d, a); break;
+    case 32: le = launch_tick_g32(h->fused, h->tick_waves, grid, h->lds, s, d, a); break;
+    default: le = launch_tick_g64(h->fused, h->tick_waves, grid, h->lds, s, d, a); break;
     }
-#undef ZS_TICK
-    HIPCHK(hipGetLastError());
+    HIPCHK(le);
     if (h->prof) {
         HIPCHK(hipEventRecord(prof_event(h, &i1), s));
         h->ev_tick.push_back({i0, i1});
@@ -1126,14 +1015,12 @@ static int launch_tick(zs_handle* h, const int32_t* actions, double* rew, uint8_
 static int launch_reset(zs_handle* h, int list_mode, const uint8_t* mask, void* obs, hipStream_t s) {
     const Dev& d = h->d;
     // enough one-wave workgroups that a step's resets (~850 at 65536 envs, bridge64) run in one round
-    static const int rgrid = getenv("ZS_RESET_GRID") ? std::max(1, atoi(getenv("ZS_RESET_GRID"))) : 2048;
+    const int rgrid = h->ov.reset_grid > 0 ? h->ov.reset_grid : 2048;
     unsigned grid = (unsigned)std::min(d.N, list_mode ? rgrid : 4096);
     int p = h->rpar;
     int i0 = -1, i1 = -1;
     if (h->prof) HIPCHK(hipEventRecord(prof_event(h, &i0), s));
-    hipLaunchKernelGGL(k_reset, dim3(grid), dim3(64), h->reset_lds, s, d, list_mode, h->d_rlist[p], h->d_rcount + p,
-                       mask, h->d_err, obs);
-    HIPCHK(hipGetLastError());
+    HIPCHK(launch_reset_k(grid, h->reset_lds, s, d, list_mode, h->d_rlist[p], h->d_rcount + p, mask, h->d_err, obs));
     if (h->prof) {
         HIPCHK(hipEventRecord(prof_event(h, &i1), s));
         h->ev_reset.push_back({i0, i1});
@@ -1146,11 +1033,10 @@ static int launch_respawn(zs_handle* h, hipStream_t s) {
     const Dev& d = h->d;
     // enough one-wave workgroups for a step's respawns in one pass (C4: 2048 -> 8192 took the launch
     // from 88 to 70 us; workgroups past the list's end exit at once)
-    static const int grid = getenv("ZS_RESPAWN_GRID") ? std::max(1, atoi(getenv("ZS_RESPAWN_GRID"))) : 8192;
+    const int grid = h->ov.respawn_grid > 0 ? h->ov.respawn_grid : 8192;
     int i0 = -1, i1 = -1;
     if (h->prof) HIPCHK(hipEventRecord(prof_event(h, &i0), s));
-    hipLaunchKernelGGL(k_respawn, dim3((unsigned)std::min(d.N, grid)), dim3(64), h->reset_lds, s, d);
-    HIPCHK(hipGetLastError());
+    HIPCHK(launch_respawn_k((unsigned)std::min(d.N, grid), h->reset_lds, s, d));
     if (h->prof) {
         HIPCHK(hipEventRecord(prof_event(h, &i1), s));
         h->ev_respawn.push_back({i0, i1});
@@ -1172,10 +1058,9 @@ extern "C" int zs_reset(zs_handle* h, const uint8_t* env_mask_dev, void* obs_dev
             HIPCHK(hipMemsetAsync(h->d_rcount + p, 0, sizeof(int), s));
         } else {
             HIPCHK(hipMemsetAsync(h->d_rcount + q, 0, sizeof(int), s));
-            hipLaunchKernelGGL(k_list_filter, dim3(std::min(64, (h->d.N + 255) / 256)), dim3(256), 0, s,
-                               (const int*)h->d_rlist[p], (const int*)(h->d_rcount + p), h->d_rlist[q],
-                               h->d_rcount + q, env_mask_dev, h->d.N);
-            HIPCHK(hipGetLastError());
+            HIPCHK(launch_list_filter((unsigned)std::min(64, (h->d.N + 255) / 256), s, (const int*)h->d_rlist[p],
+                                      (const int*)(h->d_rcount + p), h->d_rlist[q], h->d_rcount + q, env_mask_dev,
+                                      h->d.N));
             // the list the next step appends to (list[p] now) starts empty (zs_step's counter protocol)
             HIPCHK(hipMemsetAsync(h->d_rcount + p, 0, sizeof(int), s));
             h->rpar = q;
@@ -1254,13 +1139,24 @@ extern "C" int zs_step(zs_handle* h, const int32_t* actions_dev, void* obs_dev, 
                      h->d_rcount + q, obs_dev, s);
     if (rc) return rc;
     h->rpar = q;
+    // a launch failing after the tick was queued: the step's tail (the counter protocol above) is done
+    // here instead, so the next step does not append after stale counts (not while capturing: a failed
+    // capture is discarded, and nothing of it ran)
+    auto tail_on_error = [&](int code) {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone) {
+            (void)hipMemsetAsync(h->d_rcount + p, 0, sizeof(int), s);
+            if (h->d.defer_respawn) (void)hipMemsetAsync(h->d.resp_count, 0, sizeof(int), s);
+        }
+        return code;
+    };
     if (h->d.defer_respawn) {
         rc = launch_respawn(h, s);
-        if (rc) return rc;
+        if (rc) return tail_on_error(rc);
     }
     // join the reset work, then 3) observations of every env (already written by the step launch
     // when fobs), carrying the step's tail
-    if (side) HIPCHK(hipStreamWaitEvent(s, h->ev_rjoin, 0));
+    if (side && hipStreamWaitEvent(s, h->ev_rjoin, 0) != hipSuccess) return tail_on_error(fail(ZS_EHIP, "hipStreamWaitEvent"));
     struct TailScope {
         Dev& d;
         TailScope(Dev& dd, int* c0, int* c1, uint64_t* st) : d(dd) {
@@ -1272,10 +1168,11 @@ extern "C" int zs_step(zs_handle* h, const int32_t* actions_dev, void* obs_dev, 
     } tail(h->d, h->d_rcount + p, h->d.defer_respawn ? h->d.resp_count : nullptr, h->graph_pol ? h->d_gstep : nullptr);
     if (h->d.fobs || !obs_dev) {
         hipLaunchKernelGGL(k_tail, dim3(1), dim3(64), 0, s, h->d);
-        HIPCHK(hipGetLastError());
-        return ZS_OK;
+        const hipError_t le = hipGetLastError();
+        return le == hipSuccess ? ZS_OK : tail_on_error(fail(ZS_EHIP, std::string("k_tail: ") + hipGetErrorString(le)));
     }
-    return launch_obs(h, obs_dev, nullptr, s);
+    rc = launch_obs(h, obs_dev, nullptr, s);
+    return rc ? tail_on_error(rc) : ZS_OK;
 }
 
 extern "C" int zs_gen_actions(zs_handle* h, uint64_t step, int32_t n_discrete, int32_t* actions_dev, void* stream) {
@@ -1390,6 +1287,12 @@ extern "C" int zs_get_state(zs_handle* h, int32_t env, int32_t* buf_host, void* 
 extern "C" int zs_set_state(zs_handle* h, int32_t env, const int32_t* buf_host, void* stream) {
     if (!h || !buf_host) return fail(ZS_EINVAL, "null argument");
     if (env < 0 || env >= h->d.N) return fail(ZS_EINVAL, "env index out of range");
+    {  // a present thing stands on a map cell (the occupancy and observation kernels index the map by it)
+        const int32_t* r = buf_host + ZS_STATE_HEADER;
+        for (int s = 0; s < h->d.E; s++, r += ZS_STATE_ENTITY_WORDS)
+            if (r[1] && (r[2] < 0 || r[3] < 0 || r[2] >= h->d.W || r[3] >= h->d.H))
+                return fail(ZS_EINVAL, "a present entity's position is outside the map");
+    }
     {  // obstacle life is int32 in HBM; INT32_MIN is the observation kernels' absent mark (ZS_HP_FLOOR)
         const int32_t* hp = buf_host + ZS_STATE_HEADER + ZS_STATE_ENTITY_WORDS * h->d.E + h->d.E;
         for (int o = 0; o < h->d.O; o++)
@@ -1517,9 +1420,10 @@ extern "C" int zs_describe(zs_handle* h, char* buf, int32_t len) {
     snprintf(buf, (size_t)len,
              "{\"envs\": %d, \"entities\": %d, \"lanes_per_env\": %d, \"step_kernel\": \"%s\", \"step_lds\": %zu, "
              "\"step_wgs_per_cu\": %d, \"rng_window\": %d, \"obs_kernel\": \"%s\", \"reset_side_stream\": %d, "
-             "\"reset_lds\": %zu, \"respawn\": \"%s\", \"tick_waves\": %d}",
+             "\"reset_lds\": %zu, \"respawn\": \"%s\", \"tick_waves\": %d, \"rng_step\": %d, \"par_exec\": %d}",
              d.N, d.E, h->G, h->fused ? "k_step" : "k_tick", h->lds, h->resident, d.rw_cap, obs_kernel, h->reset_side,
-             h->reset_lds, d.defer_respawn ? "k_respawn" : "tick", h->fused ? ZS_FUSED_WAVES : h->tick_waves);
+             h->reset_lds, d.defer_respawn ? "k_respawn" : "tick", h->fused ? ZS_FUSED_WAVES : h->tick_waves, d.rw_step,
+             d.par_exec);
     return ZS_OK;
 }
 
@@ -1544,13 +1448,30 @@ extern "C" int zs_debug_lists(zs_handle* h, int32_t* out, void* stream) {
 // ---------------------------------------------------------------------------
 // diagnostic build (-DZS_STAMPS): per-phase k_tick cycle sums since the last read
 // ---------------------------------------------------------------------------
+#ifdef ZS_STAMPS
+// this handle's step-kernel unit (its G)
+static hipError_t stamps_of(int G, unsigned long long* wg, unsigned long long* tl, int clear) {
+    switch (G) {
+    case 1: return stamps_g1(wg, tl, clear);
+    case 2: return stamps_g2(wg, tl, clear);
+    case 4: return stamps_g4(wg, tl, clear);
+    case 8: return stamps_g8(wg, tl, clear);
+    case 16: return stamps_g16(wg, tl, clear);
+    case 32: return stamps_g32(wg, tl, clear);
+    default: return stamps_g64(wg, tl, clear);
+    }
+}
+#endif
+
 // diagnostic build (-DZS_STAMPS): start / end s_memrealtime of the first n workgroups of the last step launch
 extern "C" int zs_debug_timeline(zs_handle* h, uint64_t* out, int32_t n) {
 #ifdef ZS_STAMPS
     if (!h || !out || n < 0 || n > ZS_STAMP_WGS) return fail(ZS_EINVAL, "bad argument");
     HIPCHK(hipSetDevice(h->device));
     HIPCHK(hipDeviceSynchronize());
-    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamp_tl), (size_t)n * 2 * sizeof(unsigned long long)));
+    std::vector<unsigned long long> tl((size_t)ZS_STAMP_WGS * 2);
+    HIPCHK(stamps_of(h->G, nullptr, tl.data(), 0));
+    std::memcpy(out, tl.data(), (size_t)n * 2 * sizeof(unsigned long long));
     return ZS_OK;
 #else
     (void)h; (void)out; (void)n;
@@ -1558,25 +1479,25 @@ extern "C" int zs_debug_timeline(zs_handle* h, uint64_t* out, int32_t n) {
 #endif
 }
 
+// per-phase sums over the step-kernel unit of this handle's G and the reset unit (k_reset's phases)
 extern "C" int zs_debug_stamps(zs_handle* h, uint64_t* sum_out, uint64_t* max_out, int32_t n) {
 #ifdef ZS_STAMPS
     if (!h || !sum_out || n > ZS_NPHASE) return fail(ZS_EINVAL, "bad argument");
     HIPCHK(hipSetDevice(h->device));
     HIPCHK(hipDeviceSynchronize());
-    std::vector<unsigned long long> buf((size_t)ZS_STAMP_WGS * ZS_NPHASE);
-    HIPCHK(hipMemcpyFromSymbol(buf.data(), HIP_SYMBOL(g_stamp_wg), buf.size() * sizeof(unsigned long long)));
+    std::vector<unsigned long long> buf((size_t)ZS_STAMP_WGS * ZS_NPHASE), rb(buf.size());
+    HIPCHK(stamps_of(h->G, buf.data(), nullptr, 1));
+    HIPCHK(stamps_reset(rb.data(), 1));
     for (int k = 0; k < n; k++) {
         sum_out[k] = 0;
         if (max_out) max_out[k] = 0;
     }
     for (size_t w = 0; w < (size_t)ZS_STAMP_WGS; w++)
         for (int k = 0; k < n; k++) {
-            unsigned long long v = buf[w * ZS_NPHASE + k];
+            unsigned long long v = buf[w * ZS_NPHASE + k] + rb[w * ZS_NPHASE + k];
             sum_out[k] += v;
             if (max_out && v > max_out[k]) max_out[k] = v;
         }
-    std::fill(buf.begin(), buf.end(), 0ull);
-    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_wg), buf.data(), buf.size() * sizeof(unsigned long long)));
     return ZS_OK;
 #else
     (void)h; (void)sum_out; (void)max_out; (void)n;

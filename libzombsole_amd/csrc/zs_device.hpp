@@ -96,6 +96,7 @@ struct Dev {
     int rlists_cap;  // the same for the reset work (k_reset has its own LDS budget; = lists_cap when fused)
     int fobs;        // observations are written by the step launch itself (tick and reset work)
     int defer_respawn;  // zombie respawn left to k_respawn (wave per env) instead of the tick's leader
+    int par_exec;       // the env's lanes execute the shuffled actions (zs_tick.hpp grp_execute), else its leader
     ObsLayout obsl;  // one env's observation image (zs_obs.hpp)
     int obs_stat;    // static observation tables staged beside the image (4 * DW words), 0 = none
     int rules, reward_mode, obs_scope, obs_enc, obs_w, obs_dtype, max_steps;
@@ -190,7 +191,9 @@ __device__ __forceinline__ int32_t hp_store_value(const Dev& d, int64_t v) {
             v = ZS_HP_FLOOR;
             f |= ZS_OVF_INT32;
         }
-        atomicOr(d.ovf, f);
+        // one flag word for the handle: skip the atomic once the flags are up (every later hit would
+        // otherwise contend for this address)
+        if ((__hip_atomic_load(d.ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & f) != f) atomicOr(d.ovf, f);
     }
     return (int32_t)v;
 }
@@ -211,7 +214,7 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     return z ^ (z >> 31);
 }
 
-__constant__ int32_t c_discrete[7][3] = {{ZS_ACT_MOVE, 0, 1},  {ZS_ACT_MOVE, -1, 0},       {ZS_ACT_MOVE, 0, -1},
+static __constant__ int32_t c_discrete[7][3] = {{ZS_ACT_MOVE, 0, 1},  {ZS_ACT_MOVE, -1, 0},       {ZS_ACT_MOVE, 0, -1},
                                          {ZS_ACT_MOVE, 1, 0},  {ZS_ACT_ATTACK_CLOSEST, 0, 0}, {ZS_ACT_HEAL, 0, 0},
                                          {ZS_ACT_HEAL_CLOSEST, 0, 0}};
 

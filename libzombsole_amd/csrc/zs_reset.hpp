@@ -67,18 +67,16 @@ __device__ __forceinline__ int wave_spawn(const Dev& d, const ResetLds& L, WaveR
     // k popped cells; the rest only consume their draws.
     const int ndraw = max(n - 1, 0), nswap = min(k, ndraw);
     wave_draws(r, n, 1, ndraw, nswap, [&](int t, uint32_t v) { L.jbuf[t] = v; });
-    if (lane == 0)
-        for (int t = 0; t < nswap; t++) {
-            int i = n - 1 - t, j = (int)L.jbuf[t];
-            uint32_t a = L.cand[i], bb = L.cand[j];
-            L.cand[i] = bb;
-            L.cand[j] = a;
-        }
-    wave_sync();
     int placed = min(k, n);
     for (int m = lane; m < placed; m += 64) {
+        // the m-th popped cell: position n - 1 - m after the first nswap swaps, traced back through them
+        int q = n - 1 - m;
+        for (int t = nswap - 1; t >= 0; t--) {
+            const int i = n - 1 - t, jt = (int)L.jbuf[t];
+            q = q == i ? jt : (q == jt ? i : q);
+        }
         int s = L.lslots[m];
-        int cell = (int)L.cand[n - 1 - m];
+        int cell = (int)L.cand[q];
         L.lpos[s] = pack_xy(cell % d.W, cell / d.W);
         L.lpres[s] = 1;
         __hip_atomic_fetch_or(&L.bm[cell >> 5], 1u << (cell & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -107,9 +105,16 @@ __device__ __forceinline__ void reset_env_wave(const Dev& d, const ResetLds& L, 
     const int lane = threadIdx.x, N = d.N, E = d.E, A = d.A, P = d.P;
     RST_DECL
     RST(0);
-    // the stream state first: the ring staging below waits on it
     const uint32_t st_in = d.rngst[e];
     const int serial0 = d.scal[S_SERIAL * N + e];
+    // the env's ring (both slots, independent of st_in) in the same round of loads as the rows below
+    WaveRng r;
+    r.ring = d.ring + (size_t)e * ZS_RING_WORDS;
+    r.lr = L.tw;
+    uint32_t rv[WR_STAGE_K];
+    wave_rng_fetch(r, rv);
+    // lane l's player (agents [0, A), bots [A, A + P)): its configured weapon / bot type
+    const int wsel = lane < A ? d.agent_weapons[lane] : lane < A + P ? d.bot_types[lane - A] : 0;
     // new World: the map's obstacles (all present, HP carried over), no things, no decoration
     for (int w = lane; w < d.DW; w += 64) {
         L.bm[w] = d.obstbits[w];
@@ -122,22 +127,47 @@ __device__ __forceinline__ void reset_env_wave(const Dev& d, const ResetLds& L, 
         d.obst_present[(size_t)e * d.OW + w] = nb == 32 ? 0xffffffffu : ((1u << nb) - 1u);
         nonpos |= d.obst_nonpos[(size_t)e * d.OW + w] != 0;
     }
-    int odirty = __ballot(nonpos) != 0ull;
     for (int s = lane; s < E; s += 64) {
         L.lpres[s] = 0;
         L.lpos[s] = d.pos[(size_t)s * N + e];
         L.llife[s] = d.life[(size_t)s * N + e];
         L.lweap[s] = d.weapon[(size_t)s * N + e];
     }
-    WaveRng r;
-    r.ring = d.ring + (size_t)e * ZS_RING_WORDS;
-    r.lr = L.tw;
-    wave_rng_stage(r, st_in);
+    const int odirty = __ballot(nonpos) != 0ull;
+    wave_rng_put(r, rv);
     rng_block_load(r, st_in);
     RST(1);
     // players: Player() picks a random weapon unless its module gives one (things.py:113-116);
     // agents: WeaponFactory.create_player_weapon (weapons.py:28-45).  Each random pick is one
     // _randbelow(5), in bots-then-agents order.
+    if (A + P <= 64) {  // one lane per player: the random picks ranked bots first, then agents
+        const bool rnd = lane < A ? wsel == ZS_WEAPON_RANDOM
+                                  : lane < A + P && wsel != ZS_BOT_TERMINATOR && wsel != ZS_BOT_SNIPER;
+        const unsigned long long rb = __ballot(rnd);
+        const unsigned long long bots = ((A + P == 64 ? ~0ull : (1ull << (A + P)) - 1ull) >> A) << A;
+        const int rank = lane >= A ? __popcll(rb & bots & ((1ull << lane) - 1ull))
+                                   : __popcll(rb & bots) + __popcll(rb & ((1ull << lane) - 1ull));
+        const int nrw = __popcll(rb);
+        if (nrw) wave_draws(r, 5, 0, nrw, nrw, [&](int t, uint32_t v) { L.jbuf[t] = v; });
+        if (lane < A + P) {
+            int w;
+            if (lane < A) {  // WeaponFactory: choice([Knife(), Axe(), Gun(), Rifle(), Shotgun()]) when random
+                const int k = rnd ? (int)L.jbuf[rank] : 0;
+                w = !rnd ? wsel : k == 0 ? ZS_WEAPON_KNIFE : k == 1 ? ZS_WEAPON_AXE : k == 2 ? ZS_WEAPON_GUN
+                                : k == 3 ? ZS_WEAPON_RIFLE : ZS_WEAPON_SHOTGUN;
+            } else if (wsel == ZS_BOT_TERMINATOR) {  // terminator.py:40-42
+                w = ZS_WEAPON_SHOTGUN;
+            } else if (wsel == ZS_BOT_SNIPER) {      // sniper.py:22-24
+                w = ZS_WEAPON_RIFLE;
+            } else {                                 // choice([Gun, Shotgun, Rifle, Knife, Axe])
+                const int k = (int)L.jbuf[rank];
+                w = k == 0 ? ZS_WEAPON_GUN : k == 1 ? ZS_WEAPON_SHOTGUN : k == 2 ? ZS_WEAPON_RIFLE
+                    : k == 3 ? ZS_WEAPON_KNIFE : ZS_WEAPON_AXE;
+            }
+            L.lweap[lane] = (uint8_t)w;
+            L.llife[lane] = 100;
+        }
+    } else {
     int nrw = 0;
     for (int p = 0; p < P; p++) nrw += d.bot_types[p] != ZS_BOT_TERMINATOR && d.bot_types[p] != ZS_BOT_SNIPER;
     for (int a = 0; a < A; a++) nrw += d.agent_weapons[a] == ZS_WEAPON_RANDOM;
@@ -164,6 +194,7 @@ __device__ __forceinline__ void reset_env_wave(const Dev& d, const ResetLds& L, 
             L.lweap[a] = (uint8_t)w;
             L.llife[a] = 100;
         }
+    }
     }
     wave_sync();
     int n_order = 0, serial = serial0;
@@ -292,10 +323,13 @@ __device__ __forceinline__ void reset_role(const Dev& d, int list_mode, const in
     }
 }
 
+// the non-template kernels are compiled in k_reset.hip only
+#ifdef ZS_DEFINE_RESET_KERNELS
 __global__ void __launch_bounds__(64, ZS_RESET_WAVES) k_reset(Dev d, int list_mode, const int* list, const int* count,
                                               const uint8_t* mask, int* err_out, void* obs_out) {
     reset_role(d, list_mode, list, count, mask, err_out, blockIdx.x, gridDim.x, obs_out);
 }
+#endif
 
 // ---------------------------------------------------------------------------
 // k_respawn: Game.spawn_zombies_to_maintain_minimum (game.py:196-201) for the envs whose tick
@@ -337,7 +371,7 @@ __device__ __forceinline__ void respawn_env_wave(const Dev& d, const ResetLds& L
     r.ring = d.ring + (size_t)e * ZS_RING_WORDS;
     r.lr = L.tw;
     const uint32_t st_in = d.rngst[e];
-    wave_rng_stage(r, st_in);
+    wave_rng_stage(r);
     rng_block_load(r, st_in);
     // Game.spawn_zombies(count): the deficit's Zombie()s go into the free zombie slots, lowest first
     int nz = 0;
@@ -378,6 +412,7 @@ __device__ __forceinline__ void respawn_env_wave(const Dev& d, const ResetLds& L
     wave_sync();
 }
 
+#ifdef ZS_DEFINE_RESET_KERNELS
 __global__ void __launch_bounds__(64, ZS_STEP_WAVES) k_respawn(Dev d) {
     extern __shared__ __align__(16) uint8_t smem[];
     const int n = min(*d.resp_count, d.N);
@@ -397,3 +432,4 @@ __global__ void __launch_bounds__(256) k_list_filter(const int* src, const int* 
         if (!mask[e]) dst[atomicAdd(dst_count, 1)] = e;
     }
 }
+#endif  // ZS_DEFINE_RESET_KERNELS

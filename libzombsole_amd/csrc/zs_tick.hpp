@@ -27,9 +27,9 @@ enum { K_NONE = 0, K_MOVE = 1, K_ATTACK = 2, K_HEAL = 3, K_DEFER = 4, K_RAISE = 
 // s_memtime ticks each k_tick phase took into its own slot g_stamp_wg[block][phase] (plain
 // stores, no contended atomics); zs_debug_stamps sums / maxes the slots on the host.
 #ifdef ZS_STAMPS
-#define ZS_NPHASE 20
+#define ZS_NPHASE 28
 #define ZS_STAMP_WGS 65536
-__device__ unsigned long long g_stamp_wg[ZS_STAMP_WGS * ZS_NPHASE];
+static __device__ unsigned long long g_stamp_wg[ZS_STAMP_WGS * ZS_NPHASE];
 #define STAMP_DECL unsigned long long _st_prev = 0;
 #define STAMP(k)                                                                          \
     do {                                                                                  \
@@ -45,16 +45,16 @@ __device__ unsigned long long g_stamp_wg[ZS_STAMP_WGS * ZS_NPHASE];
         unsigned long long _t;                                                            \
         asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");      \
         if ((k) > 0 && blockIdx.x < ZS_STAMP_WGS && c.g == 0)                             \
-            g_stamp_wg[blockIdx.x * ZS_NPHASE + 6 + (k)-1] += _t - _sub_prev;             \
+            g_stamp_wg[blockIdx.x * ZS_NPHASE + 7 + (k)-1] += _t - _sub_prev;             \
         _sub_prev = _t;                                                                   \
     } while (0)
-// stage-in splits: SX(1) after the first load round, SX(2) after the RNG window (slots 10, 11)
+// stage-in splits: SX(1) after the first load round, SX(2) after the RNG window (slots 11, 12)
 #define SX(k)                                                                             \
     do {                                                                                  \
         unsigned long long _t;                                                            \
         asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");      \
         if (threadIdx.x == 0 && blockIdx.x < ZS_STAMP_WGS)                                \
-            g_stamp_wg[blockIdx.x * ZS_NPHASE + 9 + (k)] += _t - _st_prev;                \
+            g_stamp_wg[blockIdx.x * ZS_NPHASE + 10 + (k)] += _t - _st_prev;                \
     } while (0)
 #define RST_DECL unsigned long long _r_prev;
 #define RST(k)                                                                            \
@@ -62,12 +62,22 @@ __device__ unsigned long long g_stamp_wg[ZS_STAMP_WGS * ZS_NPHASE];
         unsigned long long _t;                                                            \
         asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");      \
         if ((k) > 0 && blockIdx.x < ZS_STAMP_WGS && threadIdx.x == 0)                     \
-            g_stamp_wg[blockIdx.x * ZS_NPHASE + 12 + (k)-1] += _t - _r_prev;              \
+            g_stamp_wg[blockIdx.x * ZS_NPHASE + 13 + (k)-1] += _t - _r_prev;              \
         _r_prev = _t;                                                                     \
+    } while (0)
+// grp_execute splits (slots 20..26), lane 0 of the workgroup
+#define GX_DECL unsigned long long _g_prev;
+#define GX(k)                                                                             \
+    do {                                                                                  \
+        unsigned long long _t;                                                            \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");      \
+        if ((k) > 0 && threadIdx.x == 0 && blockIdx.x < ZS_STAMP_WGS)                     \
+            g_stamp_wg[blockIdx.x * ZS_NPHASE + 19 + (k)] += _t - _g_prev;                \
+        _g_prev = _t;                                                                     \
     } while (0)
 // workgroup timeline of the last launch: s_memrealtime (100 MHz, one clock for the whole chip) at
 // the workgroup's start and end, g_stamp_tl[block][0 / 1]
-__device__ unsigned long long g_stamp_tl[ZS_STAMP_WGS * 2];
+static __device__ unsigned long long g_stamp_tl[ZS_STAMP_WGS * 2];
 #define TL(k)                                                                             \
     do {                                                                                  \
         unsigned long long _t;                                                            \
@@ -76,6 +86,8 @@ __device__ unsigned long long g_stamp_tl[ZS_STAMP_WGS * 2];
     } while (0)
 #else
 #define TL(k)
+#define GX_DECL
+#define GX(k)
 #define SX(k)
 #define STAMP_DECL
 #define STAMP(k)
@@ -86,8 +98,8 @@ __device__ unsigned long long g_stamp_tl[ZS_STAMP_WGS * 2];
 #endif
 
 // adjacent_positions order (utils.py:34-44)
-__constant__ int c_adj_dx[4] = {0, 0, 1, -1};
-__constant__ int c_adj_dy[4] = {1, -1, 0, 0};
+static __constant__ int c_adj_dx[4] = {0, 0, 1, -1};
+static __constant__ int c_adj_dy[4] = {1, -1, 0, 0};
 
 // LDS footprint of one workgroup (host and device agree on this layout).  The entity columns the
 // observations need (pos, life, weapon, present) sit before `region`; everything in `region` is
@@ -272,13 +284,15 @@ __device__ __forceinline__ bool occupied(const Dev& d, const Grp& c, int x, int 
     return in_bounds(d, x, y) && bm_test(c, y * d.W + x);
 }
 
-// things.get(position): entity slot (>= 0), obstacle -(index+1), or NOTHING
+// things.get(position): entity slot (>= 0), obstacle -(index+1), or NOTHING.  At most one thing stands
+// on a cell, so the entity scan has no early exit: its LDS reads issue back to back.
 __device__ __forceinline__ int thing_at(const Dev& d, const Grp& c, int x, int y) {
     if (!occupied(d, c, x, y)) return NOTHING;
-    int32_t pk = pack_xy(x, y);
-    for (int s = 0; s < d.E; s++)
-        if (LPR(c, s) && LP(c, s) == pk) return s;
-    return -((int)d.cellmap[y * d.W + x] + 1);
+    const int32_t pk = pack_xy(x, y);
+    int hit = -1;
+#pragma unroll 4
+    for (int s = 0; s < d.E; s++) hit = (LPR(c, s) && LP(c, s) == pk) ? s : hit;
+    return hit >= 0 ? hit : -((int)d.cellmap[y * d.W + x] + 1);
 }
 
 __device__ __forceinline__ int32_t target_pos(const Dev& d, const Grp& c, int tgt) {
@@ -307,19 +321,20 @@ __device__ __forceinline__ void set_target_life(const Dev& d, Grp& c, int tgt, i
     c.odirty = 1;
 }
 
-// closest(...) over present slots [s0, s1) \ {excl}: the first minimum in dict order
+// closest(...) over present slots [s0, s1) \ {excl}: the first minimum in dict order (branch-free body:
+// the slots' LDS reads issue back to back)
 __device__ __forceinline__ int closest_in(const Dev& d, const Grp& c, int fx, int fy, int s0, int s1, int excl) {
     int best = -1, bd = 0, br = 0;
+#pragma unroll 4
     for (int s = s0; s < s1; s++) {
-        if (!LPR(c, s) || s == excl) continue;
-        int p = LP(c, s);
-        int dd = d2(fx, fy, unpack_x(p), unpack_y(p));
-        int rk = LR(c, s);
-        if (best < 0 || dd < bd || (dd == bd && rk < br)) {
-            best = s;
-            bd = dd;
-            br = rk;
-        }
+        const bool ok = LPR(c, s) && s != excl;
+        const int p = LP(c, s);
+        const int dd = d2(fx, fy, unpack_x(p), unpack_y(p));
+        const int rk = LR(c, s);
+        const bool better = ok && (best < 0 || dd < bd || (dd == bd && rk < br));
+        best = better ? s : best;
+        bd = better ? dd : bd;
+        br = better ? rk : br;
     }
     return best;
 }
@@ -471,19 +486,28 @@ __device__ __forceinline__ void decide_zombie(const Dev& d, Grp& c, int s, bool 
             tgt = pack_xy(x + c_adj_dx[bk], y + c_adj_dy[bk]);
             return;
         }
-        // blocked: first Box/Wall in sort_by_distance(target, adjacent_positions(self))
-        int dd[4];
+        // blocked: first Box/Wall in sort_by_distance(target, adjacent_positions(self)).  Every neighbour
+        // is occupied (in bounds: an out-of-bounds cell counts as free), so a neighbour no entity stands
+        // on holds a present obstacle; one scan of the entities marks the neighbours they stand on.
+        int dd[4], em = 0;
         for (int k = 0; k < 4; k++) dd[k] = d2(hx, hy, x + c_adj_dx[k], y + c_adj_dy[k]);
+#pragma unroll 4
+        for (int t = 0; t < d.E; t++) {
+            const int pt = LP(c, t);
+            const int ddx = unpack_x(pt) - x, ddy = unpack_y(pt) - y;
+            const bool on = LPR(c, t) && ddx * ddx + ddy * ddy == 1;  // an adjacent_positions cell
+            em |= on ? (ddy == 1 ? 1 : ddy == -1 ? 2 : ddx == 1 ? 4 : 8) : 0;
+        }
         int used = 0;
         for (int r = 0; r < 4; r++) {
             int bk = -1;
             for (int k = 0; k < 4; k++)
                 if (!((used >> k) & 1) && (bk < 0 || dd[k] < dd[bk])) bk = k;
             used |= 1 << bk;
-            int th = thing_at(d, c, x + c_adj_dx[bk], y + c_adj_dy[bk]);
-            if (th != NOTHING && th < 0) {
+            if (!((em >> bk) & 1)) {
+                const int bx = x + c_adj_dx[bk], by = y + c_adj_dy[bk];
                 kind = K_ATTACK;
-                tgt = th;
+                tgt = -((int)d.cellmap[by * d.W + bx] + 1);
                 return;
             }
         }
@@ -714,10 +738,277 @@ __device__ __forceinline__ void rules_check(const Dev& d, const Grp& c, int& end
 }
 
 // ---------------------------------------------------------------------------
-// leader: the order-dependent rest of the tick (gym_env.py:99-145 / multiagent_env.py:111-171)
+// The shuffle and the execution of a tick's actions by the env's G lanes (core.py:76, 103-119).
+//
+// The reference executes the shuffled actions one at a time, so an action sees every earlier one:
+// a move finds its cell taken or freed by earlier moves (core.py:140-166), an attack or heal finds its
+// target where an earlier move put it and draws its randint only when in range (core.py:168-202), and
+// lives change in order (a heal clamps at MAX_LIFE).  The lanes resolve the same sequence in parallel,
+// G actions at a time (a chunk; later chunks see the earlier ones committed):
+//   * shuffle: the n - 1 Fisher-Yates draws _randbelow(n - t) are solved over the env's window of
+//     tempered MT words with ballots (grp_draws, the fixed point of wave_draws), then lane k follows
+//     the element at position k through the swaps;
+//   * moves: lane i finds the earlier valid moves that leave or enter its destination cell (one
+//     shuffle sweep over the chunk); a move with none of them succeeds iff its cell was free at the
+//     chunk's start, the others follow the last earlier successful one of them (freed or taken), in
+//     rounds of ballots until every move is resolved (dependencies point to earlier actions only);
+//   * attacks / heals: the target's position is the one an earlier successful move of the target gave
+//     it, else its chunk-start position; the in-range ones draw their randints in execution order
+//     (grp_draws again, one bound per draw), and the last hitter of each target applies every hit on
+//     it in order (attack: life - damage; heal: min(MAX_LIFE, life + h));
+//   * the chunk's successful moves are committed (occupancy, position, re-insertion at the end of the
+//     dict order in execution order: the movers list LM).
+// LR (the dict ranks, dead once the decisions are taken) holds the draws; movers are marked 255 in LR
+// at the end, as the leader does.  When the window of pre-tempered words cannot hold a chunk's draws,
+// the lanes stop before that chunk and the leader takes over (env_step_leader with shuffled = true).
+// ---------------------------------------------------------------------------
+template <int G>
+__device__ __forceinline__ unsigned long long gbits(const Grp& c, unsigned long long b) {
+    return G == 64 ? b : (b >> (c.g * G)) & ((1ull << G) - 1ull);
+}
+template <int G>
+__device__ __forceinline__ unsigned long long gballot(const Grp& c, bool p) {
+    return gbits<G>(c, __ballot(p));
+}
+
+// draws t = 0..count-1 of _randbelow(bound(t)) (random.py:239-249) from the env's window words pos, pos+1, ...
+// G words per round: the word of lane j serves draw t_j = done + j - H_j (H_j = rejected words of the round
+// before lane j), solved as a fixed point as in wave_draws.  put(t, value) for every accepted draw.  Returns
+// false when the draws need words past the window (wlen); pos then is unspecified.
+template <int G, class Bound, class Put>
+__device__ __forceinline__ bool grp_draws(const Grp& c, int wlen, int& pos, int count, Bound bound, Put put) {
+    const int j = c.j;
+    const unsigned long long below = (1ull << j) - 1ull;
+    int done = 0;
+    while (done < count) {
+        const bool avail = pos + j < wlen;
+        const uint32_t w = avail ? c.rw[IX(c, pos + j)] : 0u;
+        unsigned long long rej = 0ull, prev;
+        int t, b;
+        bool lv, rj;
+        do {
+            prev = rej;
+            t = done + j - __popcll(rej & below);
+            lv = t < count;
+            b = lv ? bound(t) : 1;
+            rj = lv && (w >> (__clz(b))) >= (uint32_t)b;  // getrandbits(bit_length(b)) = w >> (32 - bit_length(b))
+            rej = gballot<G>(c, rj);
+        } while (rej != prev);
+        const unsigned long long live = gballot<G>(c, lv);
+        if (gballot<G>(c, lv && !avail)) return false;
+        if (lv && !rj) put(t, w >> __clz(b));
+        done += __popcll(live) - __popcll(rej);
+        pos += 64 - __clzll((long long)live);
+    }
+    return true;
+}
+
+// random.shuffle of the n actions LPE(0..n) (n <= 2G) from window word pos on; false (nothing written)
+// when the window is too short
+template <int G>
+__device__ __forceinline__ bool grp_shuffle(Grp& c, int n, int wlen, int& pos) {
+    if (n < 2) return true;
+    GX_DECL
+    GX(0);
+    const bool ok = grp_draws<G>(
+        c, wlen, pos, n - 1, [&](int t) { return n - t; }, [&](int t, uint32_t v) { LR(c, t) = (uint8_t)v; });
+    if (!ok) return false;
+    wave_sync();
+    GX(1);
+    // lane j follows the elements at positions j and j + G through the swaps (i = n - 1 - t, j_t)
+    int fin[2] = {-1, -1}, el[2] = {0, 0};
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        const int k = c.j + h * G;
+        if (k < n) {
+            el[h] = LPE(c, k);
+            fin[h] = k;
+        }
+    }
+#pragma unroll 4
+    for (int t = 0; t < n - 1; t++) {
+        const int i = n - 1 - t, jt = LR(c, t);
+#pragma unroll
+        for (int h = 0; h < 2; h++) fin[h] = fin[h] == i ? jt : (fin[h] == jt ? i : fin[h]);
+    }
+    wave_sync();
+#pragma unroll
+    for (int h = 0; h < 2; h++)
+        if (fin[h] >= 0) LPE(c, fin[h]) = (uint8_t)el[h];
+    wave_sync();
+    GX(2);
+    return true;
+}
+
+// execute the shuffled actions LPE(i0..n) chunk by chunk; returns the index of the first action not
+// executed (n when all were; else the leader continues there: the window cannot hold that chunk's draws).
+// Successful movers are appended to LM(nmoved..); odirty is set when an obstacle was hit.
+template <int G>
+__device__ __forceinline__ int grp_execute(const Dev& d, Grp& c, int n, int wlen, int& pos, int& nmoved, int& odirty) {
+    const int j = c.j;
+    const unsigned long long below = (1ull << j) - 1ull;
+    const unsigned long long gfull = G == 64 ? ~0ull : (1ull << G) - 1ull;
+    GX_DECL
+    GX(0);
+    for (int c0 = 0; c0 < n; c0 += G) {
+        const int m = min(G, n - c0);
+        const bool act = j < m;
+        int s = 0, kind = K_NONE, tgt = 0, p = 0, w = 0;
+        if (act) {
+            s = LPE(c, c0 + j);
+            kind = LK(c, s);
+            tgt = LT(c, s);
+            p = LP(c, s);
+            w = LW(c, s);
+        }
+        const int px = unpack_x(p), py = unpack_y(p);
+        // a valid move: in bounds and one step (core.py:140-166); it still fails on an occupied cell
+        bool mv = false;
+        int dcell = 0;
+        if (kind == K_MOVE) {
+            const int tx = unpack_x(tgt), ty = unpack_y(tgt);
+            mv = in_bounds(d, tx, ty) && d2(px, py, tx, ty) <= 1;
+            dcell = ty * d.W + tx;
+        }
+        const bool occ0 = mv && bm_test(c, dcell);
+        const bool hits = kind == K_ATTACK || kind == K_HEAL;
+        const int et = hits && tgt >= 0 ? tgt : -1;  // an entity target may have moved earlier
+        // an obstacle target's position, kind and life: one round of global loads
+        int tp0 = 0, okind = 0, ohp = 0;
+        if (hits && tgt < 0) {
+            tp0 = d.obst_xy[-tgt - 1];
+            okind = d.obst_kind[-tgt - 1];
+            ohp = d.obst_hp[(size_t)c.e * d.O + (-tgt - 1)];
+        } else if (et >= 0) {
+            tp0 = LP(c, et);
+        }
+        GX(3);
+        // earlier valid moves of the chunk that leave (vac) or enter this move's cell, and the target's move
+        unsigned long long dep = 0ull, vac = 0ull;
+        int tmv = -1, tdst = 0;
+        const int sv = mv ? s : -1, mdst = mv ? tgt : 0;
+#pragma unroll 4
+        for (int k = 0; k < m; k++) {
+            const int sk = __shfl(sv, k, G), srck = __shfl(p, k, G), dstk = __shfl(mdst, k, G);
+            if (k < j && sk >= 0) {
+                if (mv && srck == tgt) {
+                    dep |= 1ull << k;
+                    vac |= 1ull << k;
+                } else if (mv && dstk == tgt) {
+                    dep |= 1ull << k;
+                }
+                if (sk == et) {
+                    tmv = k;
+                    tdst = dstk;
+                }
+            }
+        }
+        GX(4);
+        bool res = !mv || dep == 0ull;
+        bool suc = mv && dep == 0ull && !occ0;
+        unsigned long long R = gballot<G>(c, res), S = gballot<G>(c, suc);
+        while (R != gfull) {
+            if (!res && (dep & ~R) == 0ull) {
+                const unsigned long long sd = dep & S;
+                suc = sd ? ((vac >> (63 - __clzll((long long)sd))) & 1ull) != 0ull : !occ0;
+                res = true;
+            }
+            R = gballot<G>(c, res);
+            S = gballot<G>(c, suc);
+        }
+        // attacks / heals: in range at the target's position of the moment (core.py:168-202)
+        bool inr = false;
+        int lo = 0, bnd = 1, ml = 100;
+        if (hits) {
+            ml = tgt >= 0 ? 100 : okind == ZS_THING_BOX ? 10 : 200;  // target_maxlife
+            const int tp = (tgt >= 0 && tmv >= 0 && ((S >> tmv) & 1ull)) ? tdst : tp0;
+            if (kind == K_ATTACK) {
+                inr = d2(px, py, unpack_x(tp), unpack_y(tp)) <= weapon_r2(w);
+                lo = weapon_lo(w);
+                bnd = weapon_hi(w) - lo + 1;
+            } else {
+                inr = d2(px, py, unpack_x(tp), unpack_y(tp)) <= 9;
+                lo = ml / 10;
+                bnd = ml / 4 - lo + 1;
+            }
+        }
+        GX(5);
+        const unsigned long long IR = gballot<G>(c, inr);
+        const int r = __popcll(IR & below);
+        if (inr) LR(c, r) = (uint8_t)bnd;
+        wave_sync();
+        const int pos0 = pos;
+        const bool ok = grp_draws<G>(
+            c, wlen, pos, __popcll(IR), [&](int t) { return (int)LR(c, t); },
+            [&](int t, uint32_t v) { LR(c, t) = (uint8_t)v; });
+        if (!ok) {  // nothing of this chunk is committed: the leader takes over here
+            pos = pos0;
+            return c0;
+        }
+        wave_sync();
+        GX(6);
+        // every hit on a target in execution order; the last hitter stores the result
+        const int hv = inr ? (kind == K_ATTACK ? -(lo + (int)LR(c, r)) : lo + (int)LR(c, r)) : 0;
+        int64_t life = 0;
+        if (inr) life = tgt >= 0 ? (int64_t)LL(c, tgt) : (int64_t)ohp;
+        bool last = inr;
+        uint32_t ovf = 0u;  // an obstacle's life after one of the hits left the int16 / int32 range
+#pragma unroll 4
+        for (int k = 0; k < m; k++) {
+            const int tk = __shfl(tgt, k, G), hk = __shfl(hv, k, G);
+            if (inr && ((IR >> k) & 1ull) && tk == tgt) {
+                if (k <= j) {
+                    life = hk < 0 ? life + hk : min(life + hk, (int64_t)ml);
+                    if (tgt < 0 && life < -32768) {  // hp_store_value of every hit, as the leader stores them
+                        ovf |= ZS_OVF_INT16;
+                        if (life < (int64_t)ZS_HP_FLOOR) {
+                            life = ZS_HP_FLOOR;
+                            ovf |= ZS_OVF_INT32;
+                        }
+                    }
+                } else {
+                    last = false;
+                }
+            }
+        }
+        if (last) {
+            if (tgt >= 0) {
+                LL(c, tgt) = (int)life;
+            } else {  // set_target_life's obstacle path, one lane per obstacle
+                const int oi = -tgt - 1;
+                if (ovf && (__hip_atomic_load(d.ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ovf) != ovf)
+                    atomicOr(d.ovf, ovf);
+                d.obst_hp[(size_t)c.e * d.O + oi] = (int32_t)life;
+                atomicOr(&d.hp_dirty[c.e], 1u << (oi / d.hp_chunk));
+                uint32_t* wp = &d.obst_nonpos[(size_t)c.e * d.OW + (oi >> 5)];
+                if (life <= 0) atomicOr(wp, 1u << (oi & 31));
+                else atomicAnd(wp, ~(1u << (oi & 31)));
+            }
+        }
+        if (gballot<G>(c, inr && tgt < 0)) odirty = 1;
+        // commit the chunk's moves: cells freed before cells taken (a cell is left at most once and
+        // taken at most once per tick, in that order), positions, movers in execution order
+        if (suc) bm_clr(c, py * d.W + px);
+        if (suc) {
+            bm_set(c, dcell);
+            LP(c, s) = tgt;
+            LM(c, nmoved + __popcll(S & below)) = (uint8_t)s;
+        }
+        nmoved += __popcll(S);
+        wave_sync();
+        GX(7);
+    }
+    return n;
+}
+
+// ---------------------------------------------------------------------------
+// leader: the order-dependent rest of the tick (gym_env.py:99-145 / multiagent_env.py:111-171).
+// shuffled: the env's lanes already shuffled the action list and executed its actions before i0
+// (grp_execute; the first nmoved0 movers are in LM), so the leader takes over at action i0.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void env_step_leader(const Dev& d, Grp& c, const int32_t* actions, double* rew, uint8_t* done_out,
-                                uint8_t* trunc_out, uint8_t* listed_out) {
+                                uint8_t* trunc_out, uint8_t* listed_out, bool shuffled = false, int i0 = 0,
+                                int nmoved0 = 0) {
     const int A = d.A;
     SUB_DECL
     SUB(0);
@@ -751,7 +1042,7 @@ __device__ __forceinline__ void env_step_leader(const Dev& d, Grp& c, const int3
         if (LK(c, s) != K_NONE) LPE(c, nact++) = (uint8_t)s;
     }
     // random.shuffle(actions) (core.py:76)
-    for (int i = nact - 1; i >= 1; i--) {
+    for (int i = shuffled ? 0 : nact - 1; i >= 1; i--) {
         int j = rng_below(d, c, i + 1);
         uint8_t tmp = LPE(c, i);
         LPE(c, i) = LPE(c, j);
@@ -760,15 +1051,15 @@ __device__ __forceinline__ void env_step_leader(const Dev& d, Grp& c, const int3
     SUB(1);
     // execute_actions (core.py:103-119).  The next action's actor, kind, target and position are read
     // ahead: nothing this action does changes them (every actor acts once, and only its own action moves it).
-    int nmoved = 0;
+    int nmoved = nmoved0;
     int s_n = 0, kind_n = K_NONE, tgt_n = 0, p_n = 0;
-    if (nact > 0) {
-        s_n = LPE(c, 0);
+    if (i0 < nact) {
+        s_n = LPE(c, i0);
         kind_n = LK(c, s_n);
         tgt_n = LT(c, s_n);
         p_n = LP(c, s_n);
     }
-    for (int i = 0; i < nact; i++) {
+    for (int i = i0; i < nact; i++) {
         const int s = s_n, kind = kind_n, tgt = tgt_n, p = p_n, x = unpack_x(p), y = unpack_y(p);
         if (i + 1 < nact) {
             s_n = LPE(c, i + 1);
@@ -1027,8 +1318,10 @@ __device__ __forceinline__ void coop_refill(const Dev& d, int base, int count, c
 // ---------------------------------------------------------------------------
 // k_tick: one workgroup = one wave = 64/G envs
 // ---------------------------------------------------------------------------
-// envs [env0, env1) of this launch; workgroup wg takes the NE envs from env0 + wg * NE
-template <int G>
+// envs [env0, env1) of this launch; workgroup wg takes the NE envs from env0 + wg * NE.
+// EARLY (the one-round fused launch, whose register budget has room): the RNG window's first 4G words
+// are loaded as soon as the stream state is in, overlapped with the first load round, instead of after it
+template <int G, bool EARLY = false>
 __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* actions, double* rew, uint8_t* done_out,
                                         uint8_t* trunc_out, uint8_t* listed_out, uint8_t* reset_out, int* reset_list,
                                         int* reset_count, void* obs_out, int env0, int env1) {
@@ -1079,7 +1372,20 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
     uint8_t vw[4], vr[4], vo[4];
     int mval = 0, av = 0;
     uint32_t bmv[8], opw = 0u;
+    uint32_t wv[4];  // EARLY: the window's words j, j + G, j + 2G, j + 3G (raw)
+    uint32_t woff = 0, wslot = 0, wready = 0;
     uint64_t pseed = 0, pstep = 0;  // the fused policy's inputs (zs_step_graph)
+    // the window of the stream state st: its first word (off, slot, ready) and length
+    auto window = [&](uint32_t st_, uint32_t& off, uint32_t& slot, uint32_t& ready) {
+        off = st_ & 1023u, slot = (st_ >> 10) & 1u, ready = (st_ >> 11) & 1u;
+        if (off >= ZS_MT_N && ready) {
+            slot ^= 1u;
+            off = 0;
+            ready = 0;
+        }
+        const int maxw = off >= ZS_MT_N ? 0 : (ready ? d.rw_cap : min(d.rw_cap, ZS_MT_N - (int)off));
+        return min(d.rw_step, maxw);
+    };
     const int nmisc = MISC_N + 2 * A;
     if (active) {
         if (d.pol_n) {
@@ -1116,6 +1422,17 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
 #pragma unroll
         for (int u = 0; u < 8; u++) bmv[u] = d.obstbits[min(j + u * G, d.DW - 1)];
         opw = d.obst_present[(size_t)e * d.OW + min(j, d.OW - 1)];
+        if constexpr (EARLY) {
+            if (needs_reset == 0) {  // waits for the first two loads of the round only
+                wlen = window(st, woff, wslot, wready);
+                const uint32_t* ring = d.ring + (size_t)e * ZS_RING_WORDS;
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const uint32_t q = woff + min(j + u * G, max(wlen - 1, 0));
+                    wv[u] = q < ZS_MT_N ? ring[wslot * ZS_MT_N + q] : ring[(wslot ^ 1u) * ZS_MT_N + q - ZS_MT_N];
+                }
+            }
+        }
     }
     stepping = active && needs_reset == 0;
     if (active && d.pol_n) {
@@ -1197,16 +1514,19 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
         if (d.DW > 8 * G)
             stage_in(d.obstbits + 8 * G, d.DW - 8 * G, j, G, c.bm, [&](int w) { return IX(c, w + 8 * G); });
         // RNG window: the next words of this env's stream, tempered
-        uint32_t off = st & 1023u, slot = (st >> 10) & 1u, ready = (st >> 11) & 1u;
-        if (off >= ZS_MT_N && ready) {
-            slot ^= 1u;
-            off = 0;
-            ready = 0;
+        uint32_t off, slot, ready;
+        int b0 = j;
+        if constexpr (EARLY) {
+            off = woff, slot = wslot, ready = wready;
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                if (j + u * G < wlen) c.rw[IX(c, j + u * G)] = mt_temper(wv[u]);
+            b0 = j + 4 * G;
+        } else {
+            wlen = window(st, off, slot, ready);
         }
-        int maxw = off >= ZS_MT_N ? 0 : (ready ? d.rw_cap : min(d.rw_cap, ZS_MT_N - (int)off));
-        wlen = min(d.rw_step, maxw);
         const uint32_t* ring = d.ring + (size_t)e * ZS_RING_WORDS;
-        for (int b = j; b < wlen; b += 8 * G) {
+        for (int b = b0; b < wlen; b += 8 * G) {
             uint32_t v[8];
 #pragma unroll
             for (int u = 0; u < 8; u++) {
@@ -1295,9 +1615,28 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
         d.scal[S_NEEDRESET * N + e] = 0;
         lst[g] = 1u << 11;  // no MT refill for this env here
     }
+    // the shuffle and execution by the env's lanes when no decision was deferred to the leader (grp_execute)
+    bool par = false;
+    int i0 = 0, nm0 = 0, gpos = 0, nact = 0;
+    if (stepping && d.par_exec) {
+        nact = MISC(c, MISC_NMOVED);
+        if (nact >= 0 && nact <= 2 * G) {
+            int pos = 0;
+            if (grp_shuffle<G>(c, nact, wlen, pos)) {
+                int odirty = 0;
+                i0 = grp_execute<G>(d, c, nact, wlen, pos, nm0, odirty);
+                for (int q = j; q < nm0; q += G) LR(c, LM(c, q)) = 255;  // re-inserted at the end of the dict
+                if (odirty && j == 0) MISC(c, MISC_ODIRTY) = 1;
+                par = true;
+                gpos = pos;
+            }
+        }
+    }
+    wave_sync();
+    STAMP(3);
     if (leader && stepping) {
         c.st0 = st0;
-        c.wpos = 0;
+        c.wpos = par ? gpos : 0;
         c.wlen = wlen;
         c.n_order = n_order;
         c.t = MISC(c, MISC_T) + 1;
@@ -1307,7 +1646,12 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
         c.prevzd = MISC(c, MISC_PREVZD);
         c.serial = MISC(c, MISC_SERIAL);
         c.odirty = MISC(c, MISC_ODIRTY);
-        env_step_leader(d, c, actions, rew, done_out, trunc_out, listed_out);
+        if (par && i0 >= nact) {  // every action executed by the lanes: what the leader's part hands on
+            MISC(c, MISC_NMOVED) = nm0;
+            MISC(c, MISC_NORD) = c.n_order;
+        } else {
+            env_step_leader(d, c, actions, rew, done_out, trunc_out, listed_out, par, i0, nm0);
+        }
     }
     wave_sync();
     env_cleanup_group<G>(d, c, stepping);
@@ -1340,7 +1684,7 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
         lst[g] = stf;
     }
     wave_sync();
-    STAMP(3);
+    STAMP(4);
     if (stepping) {
         for (int s = j; s < E; s += G) {
             d.pos[(size_t)s * N + e] = LP(c, s);
@@ -1364,7 +1708,7 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
         }
     }
     wave_sync();
-    STAMP(4);
+    STAMP(5);
     // observations of the envs ticked here (envs reset by this call get theirs from the reset work):
     // the whole wave encodes one env at a time, its image aliasing the dead tick region
     if (d.fobs && obs_out) {
@@ -1385,9 +1729,9 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
         }
     }
     wave_sync();
-    STAMP(5);
-    coop_refill(d, base, min(NE, env1 - base), lst, (lu32*)(smem + L.off_bm));
     STAMP(6);
+    coop_refill(d, base, min(NE, env1 - base), lst, (lu32*)(smem + L.off_bm));
+    STAMP(7);
 }
 
 template <int G, int W = ZS_STEP_WAVES>

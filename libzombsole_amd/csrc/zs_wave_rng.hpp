@@ -22,31 +22,28 @@ struct WaveRng {
     int dirty;            // bit s: LDS slot s was twisted and must be written back
 };
 
-// stage the env's ring into LDS: the current slot, and the next one when it is already twisted
-// (both slots' loads in one round: 10 words per lane each)
-__device__ __forceinline__ void wave_rng_stage(WaveRng& r, uint32_t st) {
-    constexpr int K = (ZS_MT_N + 63) / 64;
-    const uint32_t slot = (st >> 10) & 1u, ready = (st >> 11) & 1u;
+// stage the env's ring into LDS: both slots, whatever the stream state (the slot not yet twisted holds
+// stale words that nothing reads before wave_twist rewrites them), so the loads do not wait for the
+// state word.  wave_rng_fetch issues the 20 loads per lane, wave_rng_put stores them: a caller issues
+// its other loads in between, and the round trips overlap.
+#define WR_STAGE_K ((2 * ZS_MT_N + 63) / 64)
+__device__ __forceinline__ void wave_rng_fetch(const WaveRng& r, uint32_t (&v)[WR_STAGE_K]) {
     const int lane = threadIdx.x;
-    const uint32_t* a = r.ring + slot * ZS_MT_N;
-    const uint32_t* b = r.ring + (slot ^ 1u) * ZS_MT_N;
-    uint32_t va[K], vb[K];
 #pragma unroll
-    for (int u = 0; u < K; u++) va[u] = a[min(lane + 64 * u, ZS_MT_N - 1)];
-    if (ready) {
+    for (int u = 0; u < WR_STAGE_K; u++) v[u] = r.ring[min(lane + 64 * u, 2 * ZS_MT_N - 1)];
+}
+__device__ __forceinline__ void wave_rng_put(WaveRng& r, const uint32_t (&v)[WR_STAGE_K]) {
+    const int lane = threadIdx.x;
 #pragma unroll
-        for (int u = 0; u < K; u++) vb[u] = b[min(lane + 64 * u, ZS_MT_N - 1)];
-    }
-#pragma unroll
-    for (int u = 0; u < K; u++)
-        if (lane + 64 * u < ZS_MT_N) r.lr[slot * ZS_MT_N + lane + 64 * u] = va[u];
-    if (ready) {
-#pragma unroll
-        for (int u = 0; u < K; u++)
-            if (lane + 64 * u < ZS_MT_N) r.lr[(slot ^ 1u) * ZS_MT_N + lane + 64 * u] = vb[u];
-    }
+    for (int u = 0; u < WR_STAGE_K; u++)
+        if (lane + 64 * u < 2 * ZS_MT_N) r.lr[lane + 64 * u] = v[u];
     r.dirty = 0;
     wave_sync();
+}
+__device__ __forceinline__ void wave_rng_stage(WaveRng& r) {
+    uint32_t v[WR_STAGE_K];
+    wave_rng_fetch(r, v);
+    wave_rng_put(r, v);
 }
 
 // next block of the stream (LDS slot ^ 1) from the current one (_randommodule.c genrand_uint32's

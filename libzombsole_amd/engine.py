@@ -24,12 +24,13 @@ class EngineUnavailable(RuntimeError):
 
 
 def load_library(path=None):
-    """Load the engine .so (no device call is made)."""
+    """Load the engine .so (no device call is made).  The product library unless `path` names
+    another build of the same sources; use_library(path) makes such a build the process's engine
+    (diagnostic tools: tools/stamps.py, A/B runs).  No environment variable selects the library."""
     global _lib
     if _lib is not None and path is None:
         return _lib
-    # ZS_ENGINE_LIB selects a diagnostic build of the same sources (tools/stamps.py)
-    p = path or os.environ.get("ZS_ENGINE_LIB") or LIB_PATH
+    p = path or LIB_PATH
     if not os.path.exists(p):
         raise EngineUnavailable("HIP engine library not built: %s (run __graft_entry__.build())" % p)
     # torch ships its own libamdhip64.so.7 / libhsa-runtime64.so.1; load it first so the engine
@@ -58,20 +59,22 @@ def load_library(path=None):
     L.zs_profile_read.argtypes = [vp, C.POINTER(C.c_double)]
     L.zs_debug_stamps.argtypes = [vp, vp, vp, i32]
     L.zs_describe.argtypes = [vp, C.c_char_p, i32]
-    # an older build selected by ZS_ENGINE_LIB for an A/B (tools/ab.sh) may lack newer entry points
-    optional = {"zs_debug_lists", "zs_overflow", "zs_debug_timeline"} if os.environ.get("ZS_ENGINE_LIB") and path is None else set()
+    L.zs_debug_lists.argtypes = [vp, C.POINTER(i32), vp]
+    L.zs_debug_timeline.argtypes = [vp, vp, i32]
     for s in SYMBOLS:
-        if s in optional and not hasattr(L, s):
-            continue
-        if s == "zs_debug_lists":
-            L.zs_debug_lists.argtypes = [vp, C.POINTER(i32), vp]
-        if s == "zs_debug_timeline":
-            L.zs_debug_timeline.argtypes = [vp, vp, i32]
         if s != "zs_last_error":
             getattr(L, s).restype = C.c_int
     if path is None:
         _lib = L
     return L
+
+
+def use_library(path):
+    """Tools only: make the build at `path` (e.g. a -DZS_STAMPS diagnostic build) the library every
+    later Engine of this process binds."""
+    global _lib
+    _lib = load_library(path)
+    return _lib
 
 
 class EngineError(RuntimeError):

@@ -158,6 +158,12 @@ class StepGather(object):
         g = StepGather(eng)
         g.step(lambda out: eng.step_graph(t, 7, out=out))   # per step
         g.obs(), g.rewards(), g.done(), g.truncated()      # the last step's node-wide tensors
+
+    The tensors obs() returns are the exchange buffers themselves when every shard has the same size
+    (no copy): they hold step t's values until the exchange of step t + depth overwrites them, and are
+    ordered on the current stream only (obs(copy=True) returns a copy).  A consumer that reads a step's
+    gathered values on the communication stream instead (a learner overlapping with the next step)
+    passes after=fn to step(): fn(k) runs there right after the collectives that fill set k.
     """
 
     def __init__(self, engine, group=None, depth=2):
@@ -185,9 +191,10 @@ class StepGather(object):
         self.t = 0
         self.last = None
 
-    def step(self, run):
+    def step(self, run, after=None):
         """run(out) issues one engine step into output set `out` on the current stream; the step's
-        exchange follows on the communication stream.  Returns the set used."""
+        exchange follows on the communication stream, then after(k) (if given) on that stream, with
+        g_obs[k] / g_flat[k] holding the step's gathered values.  Returns the set used."""
         torch = self.torch
         k = self.t % self.depth
         out = self.sets[k]
@@ -201,12 +208,16 @@ class StepGather(object):
             with torch.cuda.stream(self.comm):
                 _all_gather_rows(self.g_obs[k], out.obs, self.group)
                 _all_gather_rows(self.g_flat[k], out.flat, self.group)
+                if after is not None:
+                    after(k)
                 ev = torch.cuda.Event()
                 ev.record(self.comm)
             self.pending[k] = ev
         else:
             _all_gather_rows(self.g_obs[k], out.obs, self.group)
             _all_gather_rows(self.g_flat[k], out.flat, self.group)
+            if after is not None:
+                after(k)
         self.last = k
         self.t += 1
         return out
@@ -228,9 +239,11 @@ class StepGather(object):
         m = self.m
         return self.torch.cat([f[r, lo * m:hi * m].view(m, hi - lo)[:s] for r, s in enumerate(self.sizes)], dim=0)
 
-    def obs(self):
+    def obs(self, copy=False):
+        """The last step's node-wide observations (see the class note on their lifetime)."""
         self.wait()
-        return self._rows(self.g_obs[self.last])
+        o = self._rows(self.g_obs[self.last])
+        return o.clone() if copy and o is self.g_obs[self.last] else o
 
     def rewards(self):
         R = self.R

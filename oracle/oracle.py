@@ -45,6 +45,8 @@ def load(path):
     L.zo_rng_draws.argtypes = [C.c_void_p]
     L.zo_poke_life.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int]
     L.zo_poke_obstacle.argtypes = [C.c_void_p, C.c_int, C.c_int]
+    L.zo_poke_dead.argtypes = [C.c_void_p, C.c_int, C.c_int]
+    L.zo_poke_obstacle_gone.argtypes = [C.c_void_p, C.c_int]
     L.zo_run_batch.restype = C.c_int64
     L.zo_run_batch.argtypes = [C.c_void_p, C.c_uint64, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                                C.POINTER(C.c_uint64)]
@@ -145,6 +147,12 @@ class OracleEnv(object):
 
     def poke_obstacle(self, i, life):
         return self.L.zo_poke_obstacle(self.h, i, life)
+
+    def poke_dead(self, x, y):
+        return self.L.zo_poke_dead(self.h, x, y)
+
+    def poke_obstacle_gone(self, i):
+        return self.L.zo_poke_obstacle_gone(self.h, i)
 
 
 def run_batch(builder, seed0, n_envs, steps, n_discrete, threads=1):

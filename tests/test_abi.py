@@ -27,3 +27,27 @@ def test_library_loads_and_exports_all_symbols():
 def test_library_is_gfx950_code_object():
     data = open(engine.LIB_PATH, "rb").read()
     assert b"gfx950" in data
+
+
+def test_struct_layout_matches_header(tmp_path):
+    """The ctypes mirrors of zs_map_desc / zs_launch / zs_config (libzombsole_amd/_abi.py) have the
+    header's sizes and field offsets (gcc on the header itself)."""
+    import subprocess
+
+    from libzombsole_amd import _abi
+    structs = {"zs_map_desc": _abi.zs_map_desc, "zs_launch": _abi.zs_launch, "zs_config": _abi.zs_config}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "zombsole_mi355x.h"', 'int main(void) {']
+    for name, cls in structs.items():
+        lines.append('printf("%s sizeof %%zu\\n", sizeof(%s));' % (name, name))
+        for f in cls._fields_:
+            lines.append('printf("%s %s %%zu\\n", offsetof(%s, %s));' % (name, f[0], name, f[0]))
+    lines.append("return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), "-o", str(exe), str(src)])
+    got = dict((" ".join(l.split()[:2]), int(l.split()[2])) for l in subprocess.check_output([str(exe)]).decode().splitlines())
+    for name, cls in structs.items():
+        assert got["%s sizeof" % name] == ctypes.sizeof(cls), name
+        for f in cls._fields_:
+            assert got["%s %s" % (name, f[0])] == getattr(cls, f[0]).offset, (name, f[0])

@@ -50,6 +50,21 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
+def test_env_range_is_shard_range():
+    """bench.env_range and vector.shard_range give the same ranges for non-divisible totals."""
+    import bench
+    from libzombsole_amd.vector import shard_range
+    for total in (65537, 65536, 8191, 10, 3):
+        for world in (1, 2, 3, 4, 7, 8):
+            covered = 0
+            for rank in range(world):
+                n, env0, kind, tot = bench.env_range(rank, world, total)
+                assert (env0, n) == shard_range(total, rank, world) and kind == "strong" and tot == total
+                assert env0 == covered
+                covered += n
+            assert covered == total
+
+
 def test_bench_two_rank_control_flow():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -65,6 +80,8 @@ def test_bench_two_rank_control_flow():
     # strong scaling: contiguous ranges covering [0, total) exactly, sizes differ by at most one
     assert s0[1] == 0 and s0[1] + s0[0] == s1[1] and s1[1] + s1[0] == 65537
     assert abs(s0[0] - s1[0]) <= 1 and s0[2] == s1[2] == "strong" and s0[3] == s1[3] == 65537
+    # ... and exactly vector.shard_range's partition (the batched API's): the extra env goes to rank 0
+    assert (s0[0], s0[1]) == (32769, 0) and (s1[0], s1[1]) == (32768, 32769)
     # weak scaling: a fixed count per rank, node total = count x ranks
     assert (w0[0], w0[1], w1[1], w0[2], w0[3]) == (8192, 0, 8192, "weak", 16384)
     # exactly W + K steps, the device synced around the warmup and both sides of the timed window

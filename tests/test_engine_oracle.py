@@ -20,12 +20,15 @@ def _rich_triples(seed, step, n_agents):
 
 
 def run_parity(make_builder, n_envs, steps, stream="discrete", seed0=1000, n_discrete=7, check_state_every=25,
-               graph=False):
+               graph=False, launch=None, lanes=0):
     import torch
     from libzombsole_amd.engine import Engine
     from oracle.oracle import OracleEnv
 
-    eng = Engine(make_builder(n_envs))
+    b = make_builder(n_envs).set_launch(launch)
+    if lanes:
+        b.cfg.lanes_per_env = lanes
+    eng = Engine(b)
     kinds = [o[2] for o in eng.builder.map.obstacles]
     seeds = [seed0 + i for i in range(n_envs)]
     eng.seed(seeds)
@@ -122,39 +125,38 @@ def test_multi_bots_survival_rich_int16():
                64, 140, stream="rich")
 
 
-# Alternative kernel paths the engine picks by map / size (or that diagnostics force): each must be
-# bit-exact too.  The variables are read once, when the handle is created.
+# Alternative kernel paths the engine picks by map / size (or that the config's launch overrides force,
+# zs_launch: 1 = on, -1 = off): each must be bit-exact too.
 PATHS = {
-    "unfused": {"ZS_FUSED": "0"},                  # separate k_reset launch
-    "fused": {"ZS_FUSED": "1"},                    # reset work inside the step launch
-    "obs_in_step": {"ZS_FOBS": "1"},               # observations written by the step / reset launches
-    "obs_in_step_unfused": {"ZS_FOBS": "1", "ZS_FUSED": "0"},
-    "obs_k_obs": {"ZS_FOBS": "0", "ZS_OBS_PIPE": "0", "ZS_OBS_GATHER": "0"},  # one-env-per-wave k_obs
-    "obs_gather": {"ZS_FOBS": "0", "ZS_OBS_PIPE": "0"},  # window-only fetches (k_obs_gather)
-    "obs_gather_scell": {"ZS_FOBS": "0", "ZS_OBS_PIPE": "0", "ZS_OBS_GATHER_STAT": "0"},  # ... global static words
-    "obs_pipe_cells": {"ZS_OBS_LDS": "0"},          # k_obs_pipe's per-cell stores instead of k_obs_lds
-    "obs_lds": {"ZS_OBS_LDS": "1"},                 # the LDS-staged store stream at any env count (k_obs_patch)
-    "obs_lds_select": {"ZS_OBS_LDS": "1", "ZS_OBS_PATCH": "0"},  # ... k_obs_lds's per-cell select chain
-    "obs_ring": {"ZS_OBS_LDS": "1", "ZS_OBS_RING": "1"},  # encoder / writer waves through an LDS ring
-    "obs_ring_select": {"ZS_OBS_LDS": "1", "ZS_OBS_RING": "1", "ZS_OBS_RING_PATCH": "0"},  # ... k_obs_lds's encoders
-    "obs_scan": {"ZS_OBS_WIN": "0"},                # per-cell entity scan instead of the window map
-    "obs_scan_in_step": {"ZS_OBS_WIN": "0", "ZS_FOBS": "1"},
-    "obs_scell": {"ZS_OBS_STAT": "0"},              # per-cell static words instead of LDS bitmaps
-    "obs_scell_in_step": {"ZS_OBS_STAT": "0", "ZS_FOBS": "1"},
-    "no_lds_budget": {"ZS_LDS_BUDGET": "0"},        # largest LDS copies instead of occupancy-first
+    "unfused": {"fused": -1},                  # separate k_reset launch
+    "fused": {"fused": 1},                    # reset work inside the step launch
+    "obs_in_step": {"fobs": 1},               # observations written by the step / reset launches
+    "obs_in_step_unfused": {"fobs": 1, "fused": -1},
+    "obs_k_obs": {"fobs": -1, "obs_pipe": -1, "obs_gather": -1},  # one-env-per-wave k_obs
+    "obs_gather": {"fobs": -1, "obs_pipe": -1},  # window-only fetches (k_obs_gather)
+    "obs_gather_scell": {"fobs": -1, "obs_pipe": -1, "obs_gather_stat": -1},  # ... global static words
+    "obs_pipe_cells": {"obs_lds": -1},          # k_obs_pipe's per-cell stores instead of k_obs_lds
+    "obs_lds": {"obs_lds": 1},                 # the LDS-staged store stream at any env count (k_obs_patch)
+    "obs_lds_select": {"obs_lds": 1, "obs_patch": -1},  # ... k_obs_lds's per-cell select chain
+    "obs_ring": {"obs_lds": 1, "obs_ring": 1},  # encoder / writer waves through an LDS ring
+    "obs_ring_select": {"obs_lds": 1, "obs_ring": 1, "obs_ring_patch": -1},  # ... k_obs_lds's encoders
+    "obs_scan": {"obs_win": -1},                # per-cell entity scan instead of the window map
+    "obs_scan_in_step": {"obs_win": -1, "fobs": 1},
+    "obs_scell": {"obs_stat": -1},              # per-cell static words instead of LDS bitmaps
+    "obs_scell_in_step": {"obs_stat": -1, "fobs": 1},
+    "no_lds_budget": {"lds_budget": -1},        # largest LDS copies instead of occupancy-first
+    "serial_exec": {"par_exec": -1},               # the leader's serial shuffle + execution (core.py:76,103-119)
 }
 
 
 @pytest.mark.parametrize("path", sorted(PATHS))
-def test_kernel_paths(path, monkeypatch):
-    for k, v in PATHS[path].items():
-        monkeypatch.setenv(k, v)
-    run_parity(c2, 96, 60, check_state_every=30)
+def test_kernel_paths(path):
+    run_parity(c2, 96, 60, check_state_every=30, launch=PATHS[path])
     run_parity(lambda n: _abi.single_env_config(n, "safehouse", ["terminator"], "city_for_safehouse", "0",
                                                 initial_zombies=20, minimum_zombies=20,
                                                 observation_scope="world", observation_position_encoding="channels",
                                                 max_episode_steps=50),
-               16, 60, check_state_every=30)
+               16, 60, check_state_every=30, launch=PATHS[path])
 
 
 # Zombie respawn in the tick's leader or deferred to k_respawn (wave per env): both bit-exact, on a
@@ -162,29 +164,28 @@ def test_kernel_paths(path, monkeypatch):
 # short list under Extermination, where a respawn decides whether the game ends (boxed: 1 zombie,
 # minimum 1).
 RESPAWN = {
-    "leader": {"ZS_DEFER_RESPAWN": "0"},
-    "deferred": {"ZS_DEFER_RESPAWN": "1"},
-    "deferred_fused": {"ZS_DEFER_RESPAWN": "1", "ZS_FUSED": "1"},
-    "deferred_unfused_serial_reset": {"ZS_DEFER_RESPAWN": "1", "ZS_FUSED": "0", "ZS_RESET_STREAM": "0"},
-    "deferred_unfused_side_reset": {"ZS_DEFER_RESPAWN": "1", "ZS_FUSED": "0"},
+    "leader": {"defer_respawn": -1},
+    "deferred": {"defer_respawn": 1},
+    "deferred_fused": {"defer_respawn": 1, "fused": 1},
+    "deferred_unfused_serial_reset": {"defer_respawn": 1, "fused": -1, "reset_stream": -1},
+    "deferred_unfused_side_reset": {"defer_respawn": 1, "fused": -1},
 }
 
 
 @pytest.mark.parametrize("path", sorted(RESPAWN))
-def test_respawn_paths(path, monkeypatch):
-    for k, v in RESPAWN[path].items():
-        monkeypatch.setenv(k, v)
+def test_respawn_paths(path):
+    lo = RESPAWN[path]
     run_parity(lambda n: _abi.single_env_config(n, "extermination", ["terminator"], "boxed", "0",
                                                 initial_zombies=1, minimum_zombies=1,
                                                 observation_scope="world", observation_position_encoding="channels",
                                                 agent_weapon="shotgun", max_episode_steps=60),
-               64, 100, stream="rich", check_state_every=20)
+               64, 100, stream="rich", check_state_every=20, launch=lo)
     run_parity(lambda n: _abi.multi_env_config(n, "safehouse", [], "city128", ["0", "1", "2", "3"],
                                                initial_zombies=50, minimum_zombies=50),
-               24, 40, check_state_every=20)
+               24, 40, check_state_every=20, launch=lo)
     run_parity(lambda n: _abi.multi_env_config(n, "extermination", [], "city_for_safehouse", ["0", "1"],
                                                initial_zombies=3, minimum_zombies=2, max_episode_steps=40),
-               32, 60, stream="rich", check_state_every=20)
+               32, 60, stream="rich", check_state_every=20, launch=lo)
 
 
 # The bench loop as a replayed hipGraph (zs_step_graph): same trajectories, for both pending-list
@@ -192,59 +193,74 @@ def test_respawn_paths(path, monkeypatch):
 # the side stream, deferred respawn).
 GRAPH = {
     "default": {},
-    "unfused_side_stream": {"ZS_FUSED": "0"},
-    "unfused_serial": {"ZS_FUSED": "0", "ZS_RESET_STREAM": "0"},
+    "unfused_side_stream": {"fused": -1},
+    "unfused_serial": {"fused": -1, "reset_stream": -1},
 }
 
 
 @pytest.mark.parametrize("path", sorted(GRAPH))
-def test_step_graph(path, monkeypatch):
-    for k, v in GRAPH[path].items():
-        monkeypatch.setenv(k, v)
-    run_parity(c2, 128, 80, check_state_every=40, graph=True)
+def test_step_graph(path):
+    run_parity(c2, 128, 80, check_state_every=40, graph=True, launch=GRAPH[path])
     run_parity(lambda n: _abi.multi_env_config(n, "safehouse", [], "city128", ["0", "1", "2", "3"],
                                                initial_zombies=50, minimum_zombies=50),
-               16, 30, check_state_every=15, graph=True)
+               16, 30, check_state_every=15, graph=True, launch=GRAPH[path])
 
 
-@pytest.mark.parametrize("patch", ["0", "1"])
-def test_store_stream_every_phase(patch, monkeypatch):
+@pytest.mark.parametrize("patch", [-1, 1])
+def test_store_stream_every_phase(patch):
     """k_obs_patch / k_obs_lds write each observation block from an LDS slot kept at the destination's
     16-B phase: int16 blocks of 4 agents (2646 B: every even phase), int32 single-agent blocks (5292 B)."""
-    monkeypatch.setenv("ZS_OBS_LDS", "1")
-    monkeypatch.setenv("ZS_OBS_PATCH", patch)
+    lo = {"obs_lds": 1, "obs_patch": patch}
     run_parity(lambda n: _abi.multi_env_config(n, "extermination", [], "bridge64", ["0", "1", "2", "3"],
                                                initial_zombies=20, obs_dtype=_abi.DTYPE_I16, max_episode_steps=200),
-               64, 60, check_state_every=30)
+               64, 60, check_state_every=30, launch=lo)
     run_parity(lambda n: _abi.single_env_config(n, "extermination", [], "bridge64", 0, initial_zombies=10,
                                                 observation_scope="surroundings:21",
                                                 observation_position_encoding="channels", max_episode_steps=200),
-               64, 60, n_discrete=6, check_state_every=30)
+               64, 60, n_discrete=6, check_state_every=30, launch=lo)
 
 
-@pytest.mark.parametrize("stat", ["0", "1"])
-def test_city128_gather_paths(stat, monkeypatch):
+@pytest.mark.parametrize("stat", [-1, 1])
+def test_city128_gather_paths(stat):
     """C4's observation kernel (k_obs_gather): static words from the LDS tables (default) or one
     global load per window cell."""
-    monkeypatch.setenv("ZS_OBS_GATHER_STAT", stat)
     run_parity(lambda n: _abi.multi_env_config(n, "safehouse", [], "city128", ["0", "1", "2", "3"],
                                                initial_zombies=50, minimum_zombies=50),
-               24, 30, check_state_every=15)
+               24, 30, check_state_every=15, launch={"obs_gather_stat": stat})
 
 
-def test_rng_window_reload(monkeypatch):
+@pytest.mark.parametrize("lanes", [4, 8, 16, 32, 64])
+def test_lanes_per_env(lanes):
+    """k_tick / k_step at every lanes-per-env count: the lanes' parallel execution in chunks of G actions
+    (chunks of 4 and 8 on 12-actor envs; more lanes than actions), and the leader's serial loop where an
+    action list exceeds 2G (G = 4); rich actions on a multi-bot map exercise heals, obstacle hits and
+    the deferred (RNG-drawing) decisions that keep the serial path."""
+    run_parity(c2, 64, 60, check_state_every=30, launch=None, lanes=lanes)
+    run_parity(lambda n: _abi.multi_env_config(n, "survival", ["sniper", "terminator", "troll"], "fort",
+                                               ["0", "1", "2"], initial_zombies=12, minimum_zombies=8,
+                                               agent_weapons=["shotgun", "gun", "axe"], max_episode_steps=60,
+                                               lanes_per_env=lanes),
+               48, 80, stream="rich", check_state_every=40)
+
+
+def test_rng_window_reload():
     """A 32-word RNG window on 54-actor envs (median 82 draws per step): the tick's leader runs its
     window dry and reloads it from the ring several times per step (core.py:76 shuffle, :168-202
     attack / heal draws), bit-exact."""
-    monkeypatch.setenv("ZS_RW_NEED", "32")
     run_parity(lambda n: _abi.multi_env_config(n, "safehouse", [], "city128", ["0", "1", "2", "3"],
                                                initial_zombies=50, minimum_zombies=50),
-               24, 30, check_state_every=15)
-    run_parity(c2, 128, 60, check_state_every=30, graph=True)
+               24, 30, check_state_every=15, launch={"rw_need": 32})
+    run_parity(c2, 128, 60, check_state_every=30, graph=True, launch={"rw_need": 32})
+    # 24 actors (C5's shape) on a 32-word window: the lanes' shuffle fits, a chunk's damage draws often
+    # do not, and the leader takes over mid-list from the window's next word
+    run_parity(lambda n: _abi.multi_env_config(n, "extermination", [], "bridge64", ["0", "1", "2", "3"],
+                                               initial_zombies=20, obs_dtype=_abi.DTYPE_I16, max_episode_steps=200),
+               64, 80, check_state_every=40, launch={"rw_need": 32})
 
 
-@pytest.mark.parametrize("fused", ["0", "1"])
-def test_masked_reset_of_pending_envs(fused, monkeypatch):
+@pytest.mark.parametrize("graph", [False, True])
+@pytest.mark.parametrize("fused", [-1, 1])
+def test_masked_reset_of_pending_envs(fused, graph):
     """Next-step autoreset, reset work on the side stream (unfused) or inside the step launch: between
     calls a pending env still shows its terminal world (state records against the oracle's, which resets
     only at the next call); a masked zs_reset of pending and running envs alike resets each once (the
@@ -253,14 +269,13 @@ def test_masked_reset_of_pending_envs(fused, monkeypatch):
     import torch
     from libzombsole_amd.engine import Engine
     from oracle.oracle import OracleEnv
-    monkeypatch.setenv("ZS_FUSED", fused)
 
     def b(n):
         return _abi.multi_env_config(n, "extermination", [], "bridge64", ["0", "1"], initial_zombies=10,
                                      minimum_zombies=0, max_episode_steps=6)
     n, steps = 256, 30
-    eng = Engine(b(n))
-    assert eng.describe()["reset_side_stream"] == (fused == "0")
+    eng = Engine(b(n).set_launch({"fused": fused}))
+    assert eng.describe()["reset_side_stream"] == (fused < 0)
     kinds = [o[2] for o in eng.builder.map.obstacles]
     eng.seed([700 + i for i in range(n)])
     eng.reset()
@@ -280,9 +295,12 @@ def test_masked_reset_of_pending_envs(fused, monkeypatch):
                 assert np.array_equal(obs[k], refs[k].reset()), ("masked reset obs", k, t)
                 masked_pending += need[k]
                 need[k] = False
-        eng.gen_actions(t, 7)
+        if graph:  # replayed step graphs between masked resets (the reset flips the list parity)
+            eng.step_graph(t, 7)
+        else:
+            eng.gen_actions(t, 7)
+            eng.step()
         acts = eng.actions.cpu().numpy()
-        eng.step()
         torch.cuda.synchronize()
         obs = eng.obs.cpu().numpy()
         rew = eng.rewards.cpu().numpy()

@@ -67,14 +67,14 @@ def oracle_state(make_builder, seed, steps, nd, twice):
     return o.state()
 
 
-def run_full(make_builder, n, steps, nd=7, seed0=0, graph=True, twice=0, min_resets=1):
+def run_full(make_builder, n, steps, nd=7, seed0=0, graph=True, twice=0, min_resets=1, launch=None, after=None):
     import torch
 
     from libzombsole_amd.engine import Engine
     from oracle.oracle import run_hashes
     from parity_hash import StepHasher
 
-    eng = Engine(make_builder(n))
+    eng = Engine(make_builder(n).set_launch(launch))
     eng.seed([seed0 + i for i in range(n)])
     eng.reset()
     if twice:  # a masked reset of every twice-th env (zs_reset mask mode over the whole grid)
@@ -101,6 +101,8 @@ def run_full(make_builder, n, steps, nd=7, seed0=0, graph=True, twice=0, min_res
     for e in spot_envs(n):
         exp_state = oracle_state(make_builder, seed0 + e, steps, nd, twice and e % twice == 1)
         assert eng.get_state(e).canonical(kinds) == exp_state, ("state", e)
+    if after:
+        after(eng)
     eng.close()
     return resets
 
@@ -121,61 +123,53 @@ def test_c2_4096_graph():
     run_full(c3, 4096, 60, seed0=4242)
 
 
-def test_c2_4096_one_obs_workgroup_per_cu(monkeypatch):
-    """ZS_OBS_WGS=1: the persistent observation kernel (k_obs_lds, the int64 ring off) at 1 workgroup
+def test_c2_4096_one_obs_workgroup_per_cu():
+    """obs_wgs = 1: the persistent observation kernel (k_obs_lds, the int64 ring off) at 1 workgroup
     per CU walks 4 envs per wave at 4 096."""
-    monkeypatch.setenv("ZS_OBS_WGS", "1")
-    monkeypatch.setenv("ZS_OBS_LDS", "1")
-    monkeypatch.setenv("ZS_OBS_RING", "0")
-    run_full(c3, 4096, 40, seed0=99)
+    run_full(c3, 4096, 40, seed0=99, launch={"obs_wgs": 1, "obs_lds": 1, "obs_ring": -1})
 
 
-def test_c2_4096_ring(monkeypatch):
+def test_c2_4096_ring():
     """k_obs_ring (encoder / writer waves through an LDS ring; C3's default) at 4 096 envs: 16 envs per
     workgroup, every ring slot reused."""
-    monkeypatch.setenv("ZS_OBS_LDS", "1")
-    monkeypatch.setenv("ZS_OBS_RING", "1")
-    run_full(c3, 4096, 40, seed0=1234)
+    run_full(c3, 4096, 40, seed0=1234, launch={"obs_lds": 1, "obs_ring": 1})
 
 
-def test_c5_65536_int16_ring(monkeypatch):
+def test_c5_65536_int16_ring():
     """k_obs_ring on C5's int16 blocks of 4 agents (10 584-B envs, two 16-B phases)."""
-    monkeypatch.setenv("ZS_OBS_RING", "1")
-    run_full(c5, 65536, 12, min_resets=0)
+    run_full(c5, 65536, 12, min_resets=0, launch={"obs_ring": 1})
 
 
-def test_c5_odd_int16_ring_pairs(monkeypatch):
+def test_c5_odd_int16_ring_pairs():
     """k_obs_ring's two-env units (C5's int16 envs end on 16-B boundaries in pairs) over an odd env
     count: one workgroup's last unit holds a single env."""
-    monkeypatch.setenv("ZS_OBS_RING", "1")
-    run_full(c5, 4097, 24, seed0=555, min_resets=0)
+    run_full(c5, 4097, 24, seed0=555, min_resets=0, launch={"obs_ring": 1})
 
 
-def test_c2_4096_ring_select_encoders(monkeypatch):
+def test_c2_4096_ring_select_encoders():
     """k_obs_ring with k_obs_lds's select-chain encoders instead of the padded-table ones."""
-    monkeypatch.setenv("ZS_OBS_LDS", "1")
-    monkeypatch.setenv("ZS_OBS_RING", "1")
-    monkeypatch.setenv("ZS_OBS_RING_PATCH", "0")
-    run_full(c3, 4096, 40, seed0=4321)
+    run_full(c3, 4096, 40, seed0=4321, launch={"obs_lds": 1, "obs_ring": 1, "obs_ring_patch": -1})
 
 
-def test_c2_4096_one_obs_workgroup_per_cu_cells(monkeypatch):
+def test_c2_4096_one_obs_workgroup_per_cu_cells():
     """The same walk through k_obs_pipe's per-cell stores."""
-    monkeypatch.setenv("ZS_OBS_WGS", "1")
-    monkeypatch.setenv("ZS_OBS_LDS", "0")
-    run_full(c3, 4096, 40, seed0=7)
+    run_full(c3, 4096, 40, seed0=7, launch={"obs_wgs": 1, "obs_lds": -1})
 
 
 def test_c5_65536_int16_graph():
     """C5's engine side: 4 agents + 20 zombies, int16 observations (the gathered form); k_obs_ring
-    with the padded-table encoders."""
-    run_full(c5, 65536, 32, min_resets=0)
+    with the padded-table encoders; episodes ending (extermination) and their autoresets at full size."""
+    run_full(c5, 65536, 40, min_resets=1)
 
 
-def test_c5_65536_int16_patch(monkeypatch):
+def test_c5_8192_int16_shard_graph():
+    """C5's per-GPU shard at N=8 (8 192 envs, int16, rank 5's env range): the fused step launch."""
+    run_full(c5, 8192, 48, seed0=5 * 8192, min_resets=1)
+
+
+def test_c5_65536_int16_patch():
     """C5 through k_obs_patch (the padded-table encoder with per-wave flushes)."""
-    monkeypatch.setenv("ZS_OBS_RING", "0")
-    run_full(c5, 65536, 32, seed0=77, min_resets=0)
+    run_full(c5, 65536, 32, seed0=77, min_resets=0, launch={"obs_ring": -1})
 
 
 def test_c5_65536_int16_truncation_waves():
@@ -185,10 +179,30 @@ def test_c5_65536_int16_truncation_waves():
 
 
 def test_c4_16384_graph():
-    """C4: city128 safehouse, 4 agents + 50 zombies (minimum 50): k_obs_gather and k_respawn."""
-    run_full(c4, 16384, 30, min_resets=0)
+    """C4: city128 safehouse, 4 agents + 50 zombies (minimum 50): k_obs_gather, k_respawn after zombie deaths
+    and safehouse / all-dead autoresets, at full size."""
+    def respawned(eng):
+        # every zombie death leaves a deficit under minimum 50 that the same step's respawn fills
+        zd = sum(eng.get_state(e).zombie_deaths for e in range(0, 16384, 97))
+        assert zd > 0, "no zombie died in the sampled envs: k_respawn untested"
+        assert eng.describe()["respawn"] == "k_respawn"
+    run_full(c4, 16384, 80, min_resets=1, after=respawned)
 
 
 def test_c3_8192_shard_eager():
     """The N=8 shard size (8 192 envs per GPU) through per-kernel launches (zs_step), env range of rank 3."""
     run_full(c3, 8192, 40, seed0=3 * 8192, graph=False)
+
+
+def test_c3_8192_shard_graph():
+    """The N=8 headline's per-GPU run as bench.py times it: graph replay, the policy and the reset work
+    inside the fused step launch (k_step), the lanes' parallel execution; env range of rank 6."""
+    def fused(eng):
+        desc = eng.describe()
+        assert desc["step_kernel"] == "k_step" and desc["par_exec"] == 1, desc
+    run_full(c3, 8192, 60, seed0=6 * 8192, after=fused)
+
+
+def test_c3_8192_shard_serial_exec():
+    """The same shard with the leader's serial execution (zs_launch.par_exec = -1)."""
+    run_full(c3, 8192, 40, seed0=2 * 8192, launch={"par_exec": -1})

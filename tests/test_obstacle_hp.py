@@ -58,27 +58,25 @@ def _poke_all(eng, pokes):
 
 # observation kernels: the engine's pick for the size (int16: k_obs_ring, int32: k_obs_patch), the
 # store streams forced at 64 envs (int64 too: k_obs_patch, k_obs_ring), and k_obs_lds's select chain
-OBS_PATHS = {"default": {}, "patch": {"ZS_OBS_LDS": "1", "ZS_OBS_RING": "0"},
-             "ring": {"ZS_OBS_LDS": "1", "ZS_OBS_RING": "1"},
-             "lds_select": {"ZS_OBS_LDS": "1", "ZS_OBS_PATCH": "0", "ZS_OBS_RING": "0"}}
+OBS_PATHS = {"default": {}, "patch": {"obs_lds": 1, "obs_ring": -1},
+             "ring": {"obs_lds": 1, "obs_ring": 1},
+             "lds_select": {"obs_lds": 1, "obs_patch": -1, "obs_ring": -1}}
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("path", sorted(OBS_PATHS))
 @pytest.mark.parametrize("dtype", [_abi.DTYPE_I64, _abi.DTYPE_I32, _abi.DTYPE_I16])
-def test_engine_matches_oracle_across_resets(dtype, path, monkeypatch):
+def test_engine_matches_oracle_across_resets(dtype, path):
     """64 envs x 160 calls (80 episodes), every call's obs / rewards / flags and the obstacle state
     against the oracle; int16 observations saturate like the oracle's int16 form and raise
     ZS_OVF_INT16, never ZS_OVF_INT32.  The 5 x 4 map puts most of every 21 x 21 window out of bounds,
     and the walls the agents shoot are damaged, destroyed and re-spawned at negative life."""
-    for k, v in OBS_PATHS[path].items():
-        monkeypatch.setenv(k, v)
     import torch
     from libzombsole_amd.engine import Engine
     from oracle.oracle import OracleEnv
     n, calls = 64, 160
     pokes = [(5, -32700), (6, -32720), (7, -32760)]
-    eng = Engine(_builder(n, dtype))
+    eng = Engine(_builder(n, dtype).set_launch(OBS_PATHS[path]))
     kinds = [o[2] for o in eng.builder.map.obstacles]
     seeds = [500 + i for i in range(n)]
     eng.seed(seeds)
@@ -176,6 +174,15 @@ def test_set_state_refuses_pending_flag_change():
         eng.set_state(2, st)
     assert np.array_equal(eng.get_state(2).buf, before)
     eng.set_state(2, eng.get_state(2))  # the engine's own record round-trips
+    # a present thing placed outside the map is refused (the kernels index the map by its cell)
+    st = eng.get_state(1)
+    before = st.buf.copy()
+    s0 = int(np.nonzero(st.ent[:, 1])[0][0])
+    for x, y in ((-1, 0), (0, -1), (st.W, 0), (0, st.H)):
+        st.ent[s0, 2], st.ent[s0, 3] = x, y
+        with pytest.raises(ValueError):
+            eng.set_state(1, st)
+    assert np.array_equal(eng.get_state(1).buf, before)
     eng.close()
 
 
@@ -215,42 +222,55 @@ def test_raise_kind_only_in_debug_envs():
         eng.close()
 
 
+ENCODERS = {"k_obs_patch": {"obs_lds": 1, "obs_ring": -1, "obs_patch": 1},
+            "k_obs_lds": {"obs_lds": 1, "obs_ring": -1, "obs_patch": -1},
+            "k_obs_ring": {"obs_lds": 1, "obs_ring": 1}}
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("dtype", [_abi.DTYPE_I16, _abi.DTYPE_I64])
-def test_patch_encoder_against_select_chain(dtype, monkeypatch):
-    """k_obs_patch (padded static table + per-env patches) against k_obs_lds's per-cell select chain
-    (itself pinned to the oracle) on the same poked states of bridge64 with 4 agents: 40 to 900
-    dead-body cells per env (more than PATCH_DEAD_CAP = 256 cells takes the per-word scan), bodies
-    under map obstacles, damaged and cleaned-up obstacles, a life below the int16 range."""
-    import torch
+@pytest.mark.parametrize("dtype,kernel", [(_abi.DTYPE_I16, k) for k in sorted(ENCODERS)] +
+                         [(_abi.DTYPE_I64, "k_obs_lds"), (_abi.DTYPE_I64, "k_obs_patch")])
+def test_observation_encoders_on_poked_states(dtype, kernel):
+    """The store-stream observation kernels (the padded-table encoder of k_obs_patch and k_obs_ring,
+    k_obs_lds's per-cell select chain) against the oracle's encoder (gym/observation.py:57-173) on the
+    same poked states of bridge64 with 4 agents: 40 to 900 dead-body cells per env (more than
+    PATCH_DEAD_CAP = 256 cells takes the per-word scan), bodies under map obstacles and under things,
+    damaged and cleaned-up obstacles, lives below the int16 range (int16 saturates in both).  (k_obs_ring's
+    LDS ring does not fit four int64 blocks: the engine does not pick it there.)"""
     from libzombsole_amd.engine import Engine
+    from oracle.oracle import OracleEnv
     n = 64
 
     def cfg(k):
         return _abi.multi_env_config(k, "extermination", [], "bridge64", ["0", "1", "2", "3"], initial_zombies=20,
                                      obs_dtype=dtype)
 
-    obs = {}
-    for patch in ("1", "0"):
-        monkeypatch.setenv("ZS_OBS_LDS", "1")
-        monkeypatch.setenv("ZS_OBS_RING", "0")
-        monkeypatch.setenv("ZS_OBS_PATCH", patch)
-        eng = Engine(cfg(n))
-        eng.seed([900 + i for i in range(n)])
-        eng.reset()
-        rng = np.random.default_rng(11)
-        cells = eng.get_state(0).W * eng.get_state(0).H
-        for e in range(n):
-            st = eng.get_state(e)
-            dw = st.dead_words.view(np.uint32)  # writes through to the record
-            for c in rng.choice(cells, size=(40, 200, 300, 900)[e % 4], replace=False):
-                dw[int(c) >> 5] |= np.uint32(1 << (int(c) & 31))
-            for i in rng.choice(st.O, size=12, replace=False):
-                st.obst_life[i] = int(rng.integers(-40000, 199))
-                if st.obst_life[i] <= 0 and rng.integers(2):
-                    st.obst_present[i] = 0
-            eng.set_state(e, st)
-        obs[patch] = eng.observe().cpu().numpy().copy()
-        assert eng.describe()["obs_kernel"] == ("k_obs_patch" if patch == "1" else "k_obs_lds")
-        eng.close()
-    assert np.array_equal(obs["1"], obs["0"])
+    eng = Engine(cfg(n).set_launch(ENCODERS[kernel]))
+    assert eng.describe()["obs_kernel"] == kernel
+    eng.seed([900 + i for i in range(n)])
+    eng.reset()
+    rng = np.random.default_rng(11)
+    W = eng.get_state(0).W
+    cells = W * eng.get_state(0).H
+    refs = []
+    for e in range(n):
+        o = OracleEnv(cfg(1))
+        o.seed(900 + e)
+        o.reset()
+        st = eng.get_state(e)
+        dw = st.dead_words.view(np.uint32)  # writes through to the record
+        for c in rng.choice(cells, size=(40, 200, 300, 900)[e % 4], replace=False):
+            dw[int(c) >> 5] |= np.uint32(1 << (int(c) & 31))
+            o.poke_dead(int(c) % W, int(c) // W)
+        for i in rng.choice(st.O, size=12, replace=False):
+            st.obst_life[i] = int(rng.integers(-40000, 199))
+            o.poke_obstacle(int(i), int(st.obst_life[i]))
+            if st.obst_life[i] <= 0 and rng.integers(2):
+                st.obst_present[i] = 0
+                o.poke_obstacle_gone(int(i))
+        eng.set_state(e, st)
+        refs.append(o)
+    got = eng.observe().cpu().numpy()
+    for e, o in enumerate(refs):
+        assert np.array_equal(got[e], o.obs()), ("obs", kernel, e)
+    eng.close()

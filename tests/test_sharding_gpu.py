@@ -98,3 +98,62 @@ def test_rccl_world1_gather():
         eng.close()
     finally:
         dist.destroy_process_group()
+
+
+def test_rccl_world1_gather_in_flight():
+    """C5's exchange with steps in flight: 8 gathered steps issued back to back with no host sync and no
+    wait on the caller's stream, so step t + 1 computes while step t's collectives run, and a set is
+    written again only after the collectives of two steps earlier.  A consumer on the communication stream
+    (StepGather.step(after=...)) hashes every step's gathered observations, rewards and flags there; the
+    hashes, and the last two sets' gathered tensors, equal those of a reference engine stepped alone
+    (gym/multiagent_env.py:111-171)."""
+    import torch
+    import torch.distributed as dist
+
+    from libzombsole_amd.engine import Engine
+    from libzombsole_amd.vector import StepGather
+
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % _free_port(), rank=0, world_size=1,
+                            device_id=dev)
+    try:
+        n, steps = 8192, 8
+        eng = Engine(_c5(n))
+        eng.seed(list(range(n)))
+        eng.reset()
+        g = StepGather(eng)
+        hashes = torch.zeros((steps, 2), dtype=torch.int64, device=dev)
+        wts = torch.arange(1, g.g_obs[0].numel() + 1, dtype=torch.int64, device=dev) % 1000003
+
+        def hash_into(t):
+            def after(k):  # runs on the communication stream, after the collectives filling set k
+                hashes[t - 1, 0] = (g.g_obs[k].reshape(-1).to(torch.int64) * wts).sum()
+                hashes[t - 1, 1] = (g.g_flat[k].to(torch.int64) * wts[:g.g_flat[k].numel()]).sum()
+            return after
+
+        for t in range(1, steps + 1):
+            g.step(lambda o: eng.step_graph(t, 7, out=o), after=hash_into(t))
+        ref = Engine(_c5(n))
+        ref.seed(list(range(n)))
+        ref.reset()
+        exp = torch.zeros_like(hashes)
+        last = {}
+        for t in range(1, steps + 1):
+            ref.step_graph(t, 7)
+            exp[t - 1, 0] = (ref.obs.reshape(-1).to(torch.int64) * wts).sum()
+            exp[t - 1, 1] = (ref.out.flat.to(torch.int64) * wts[:ref.out.flat.numel()]).sum()
+            if t > steps - 2:
+                last[t] = (ref.obs.clone(), ref.rewards.clone(), ref.done.clone(), ref.trunc.clone())
+        torch.cuda.synchronize()
+        g.wait()
+        torch.cuda.synchronize()
+        assert torch.equal(hashes, exp), (hashes - exp).abs().sum(dim=1).tolist()
+        for t in (steps - 1, steps):
+            k = (t - 1) % g.depth
+            assert torch.equal(g.g_obs[k], last[t][0]), t
+            assert torch.equal(g.g_flat[k], torch.cat([last[t][1].view(-1).view(torch.uint8), last[t][2], last[t][3]])), t
+        assert torch.equal(g.obs(copy=True), last[steps][0])
+        ref.close()
+        eng.close()
+    finally:
+        dist.destroy_process_group()

@@ -3,26 +3,31 @@
 reports, per phase, the mean and max s_memtime cycles per workgroup launch for the bench
 workload at several lanes-per-env settings.  Never used by the product or the bench."""
 import os
-import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 SO = os.path.join(ROOT, "libzombsole_amd", "_build", "libzombsole_mi355x_stamps.so")
-PHASES = ["stage-in", "decide", "leader", "stage-out", "obs-write", "mt-refill",
+PHASES = ["stage-in", "decide", "grp-exec", "leader", "stage-out", "obs-write", "mt-refill",
           "  L:defer+shuffle", "  L:execute", "  L:order+cleanup", "  L:reward+rules", "  S:to round 1", "  S:to window",
-          "R:setup+rng", "R:weapons", "R:spawn p+a", "R:zombie lives", "R:spawn z", "R:twist+out"]
+          "R:setup+rng", "R:weapons", "R:spawn p+a", "R:zombie lives", "R:spawn z", "R:twist+out", "-",
+          "  G:shuffle draws", "  G:shuffle track", "  G:chunk loads", "  G:chunk scan", "  G:resolve+range",
+          "  G:damage draws", "  G:lives+commit"]
 
 
 def main():
     import __graft_entry__ as ge
     if not os.path.exists(SO) or "--rebuild" in sys.argv:
-        subprocess.check_call([ge._hipcc()] + ge.HIPCC_FLAGS + ["-DZS_STAMPS", "-o", SO,
-                                                                 os.path.join(ge.CSRC, "engine.hip")])
-    os.environ["ZS_ENGINE_LIB"] = SO
+        ge.build_engine(extra=["-DZS_STAMPS"], out=SO, tag="stamps")
+    if "--build-only" in sys.argv:
+        return
     import torch
     from libzombsole_amd import _abi
+    from libzombsole_amd import engine as engine_mod
     from libzombsole_amd.engine import Engine
+    engine_mod.use_library(SO)
+    # launch overrides of the run, 'field=v,...' (zs_launch fields)
+    launch = dict((kv.split("=")[0], int(kv.split("=")[1])) for kv in os.environ.get("LAUNCH", "").split(",") if kv)
     n_envs = int(os.environ.get("N_ENVS", "8192"))
     for G in [int(g) for g in os.environ.get("GS", "1,2,4,8,16").split(",")]:
         A = int(os.environ.get("AGENTS", "2"))
@@ -30,7 +35,7 @@ def main():
                                   os.environ.get("MAP", "bridge64"), [str(i) for i in range(A)],
                                   initial_zombies=int(os.environ.get("ZOMBIES", "10")),
                                   minimum_zombies=int(os.environ.get("MINZ", "0")), max_episode_steps=1000,
-                                  lanes_per_env=G)
+                                  lanes_per_env=G).set_launch(launch)
         eng = Engine(b)
         eng.seed(list(range(n_envs)))
         eng.reset()
@@ -66,7 +71,7 @@ def main():
         if desc.get("step_kernel") == "k_step":
             # workgroup timeline of one more fused step launch (s_memrealtime, 10 ns)
             import numpy as np
-            n_reset = min(n_envs, int(os.environ.get("ZS_RESET_WGS", "256")))
+            n_reset = min(n_envs, launch.get("reset_wgs", 256))
             eng.gen_actions(31 + steps, 7)
             eng.step()
             torch.cuda.synchronize()

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Run bench.py once per variant and print one summary line each.  Variants are arguments of the
 # form 'label;ENV=v ENV2=v;bench args' (env and args may be empty), e.g.
-#   bash tools/sweep.sh 'base;;' 'side0;ZS_RESET_STREAM=0;' 'w2;ZS_ENGINE_LIB=libzombsole_amd/_build/libzombsole_mi355x_w2.so;'
+#   bash tools/sweep.sh 'base;;' 'side0;;--launch reset_stream=-1' 'w2;;--engine-lib libzombsole_amd/_build/libzombsole_mi355x_w2.so'
 # Stops at the first failing run (crash, timeout).
 cd "$(dirname "$0")/.." || exit 2
 mkdir -p gpurun_out/sweep
