@@ -285,6 +285,9 @@ int zs_debug_stamps(zs_handle* h, uint64_t* sum_out, uint64_t* max_out, int32_t 
 /* Diagnostic builds only: out[2w], out[2w + 1] = start / end s_memrealtime (100 MHz) of workgroup w
  * of the last fused step launch (k_step), w < n. */
 int zs_debug_timeline(zs_handle* h, uint64_t* out, int32_t n);
+/* Diagnostic builds only: out[w * n_phase + k] = cycles of phase k of workgroup w of the step launches
+ * since the last zs_debug_stamps / zs_debug_stamps_wg call (the step kernel's slots only), w < n_wgs. */
+int zs_debug_stamps_wg(zs_handle* h, uint64_t* out, int32_t n_wgs, int32_t n_phase);
 
 /* Flat state record, int32 words:
  *   [0]  t (World.t)          [1] deaths            [2] zombie_deaths

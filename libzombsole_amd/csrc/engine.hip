@@ -118,23 +118,23 @@ __global__ void k_get_state(Dev d, int e, int32_t* buf) {
     b[9] = d.H;
     b[10] = d.scal[S_PREVZD * N + e];
     int nz = 0;
-    for (int s = d.A + d.P; s < E; s++) nz += d.present[(size_t)s * N + e];
+    for (int s = d.A + d.P; s < E; s++) nz += d.present[EIX(d, s, e)];
     b[11] = nz;
     b[12] = d.scal[S_SERIAL * N + e];
     b[13] = b[14] = b[15] = 0;
     int32_t* r = b + ZS_STATE_HEADER;
     for (int s = 0; s < E; s++, r += ZS_STATE_ENTITY_WORDS) {
-        int32_t p = d.pos[(size_t)s * N + e];
+        int32_t p = d.pos[EIX(d, s, e)];
         r[0] = s < d.A ? ZS_THING_AGENT : (s < d.A + d.P ? ZS_THING_PLAYER : ZS_THING_ZOMBIE);
-        r[1] = d.present[(size_t)s * N + e];
+        r[1] = d.present[EIX(d, s, e)];
         r[2] = unpack_x(p);
         r[3] = unpack_y(p);
-        r[4] = d.life[(size_t)s * N + e];
-        r[5] = d.weapon[(size_t)s * N + e];
+        r[4] = d.life[EIX(d, s, e)];
+        r[5] = d.weapon[EIX(d, s, e)];
         r[6] = s < d.A ? s : (s < d.A + d.P ? s - d.A : 0);
-        r[7] = (int32_t)d.serial[(size_t)s * N + e];
+        r[7] = (int32_t)d.serial[EIX(d, s, e)];
     }
-    for (int s = 0; s < E; s++) *r++ = d.order[(size_t)s * N + e];
+    for (int s = 0; s < E; s++) *r++ = d.order[EIX(d, s, e)];
     for (int o = 0; o < d.O; o++) *r++ = d.obst_hp[(size_t)e * d.O + o];
     for (int o = 0; o < d.O; o++) *r++ = (d.obst_present[(size_t)e * d.OW + (o >> 5)] >> (o & 31)) & 1u;
     for (int a = 0; a < d.A; a++) *r++ = d.prev_life[(size_t)a * N + e];
@@ -162,13 +162,13 @@ __global__ void k_set_state(Dev d, int e, const int32_t* buf, int* err) {
     d.scal[S_SERIAL * N + e] = b[12];
     const int32_t* r = b + ZS_STATE_HEADER;
     for (int s = 0; s < E; s++, r += ZS_STATE_ENTITY_WORDS) {
-        d.present[(size_t)s * N + e] = (uint8_t)r[1];
-        d.pos[(size_t)s * N + e] = pack_xy(r[2], r[3]);
-        d.life[(size_t)s * N + e] = r[4];
-        d.weapon[(size_t)s * N + e] = (uint8_t)r[5];
-        d.serial[(size_t)s * N + e] = (uint32_t)r[7];
+        d.present[EIX(d, s, e)] = (uint8_t)r[1];
+        d.pos[EIX(d, s, e)] = pack_xy(r[2], r[3]);
+        d.life[EIX(d, s, e)] = r[4];
+        d.weapon[EIX(d, s, e)] = (uint8_t)r[5];
+        d.serial[EIX(d, s, e)] = (uint32_t)r[7];
     }
-    for (int s = 0; s < E; s++) d.order[(size_t)s * N + e] = (uint8_t)*r++;
+    for (int s = 0; s < E; s++) d.order[EIX(d, s, e)] = (uint8_t)*r++;
     int any_nonpos = 0;
     for (int o = 0; o < d.O; o++) {
         int v = *r++;
@@ -807,6 +807,9 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
         const int obs_b = d.fobs ? d.obsl.bytes + 4 * d.obs_stat : 0;
         TRY(choose_layout(h, cfg->lanes_per_env, true, obs_b));
         h->fused = h->ov.fused ? h->ov.fused > 0 : h->resident >= h->want;
+        // the fused launch loads its window's first 4G words with its first load round (zs_tick.hpp EARLY): a
+        // window that size costs no round trip, and the lanes' draws then reload it less often
+        if (h->fused && h->ov.rw_need <= 0) d.rw_step = std::min(d.rw_cap, std::max(d.rw_step, 4 * h->G));
         if (!h->fused) {
             TRY(choose_layout(h, cfg->lanes_per_env, false, obs_b));
             // k_tick's register budget: 5 waves per SIMD (96 VGPRs, 20 B of scratch per lane) unless 6 (80
@@ -1475,6 +1478,23 @@ extern "C" int zs_debug_timeline(zs_handle* h, uint64_t* out, int32_t n) {
     return ZS_OK;
 #else
     (void)h; (void)out; (void)n;
+    return fail(ZS_ESTATE, "not a ZS_STAMPS diagnostic build");
+#endif
+}
+
+extern "C" int zs_debug_stamps_wg(zs_handle* h, uint64_t* out, int32_t n_wgs, int32_t n_phase) {
+#ifdef ZS_STAMPS
+    if (!h || !out || n_wgs < 0 || n_wgs > ZS_STAMP_WGS || n_phase < 1 || n_phase > ZS_NPHASE)
+        return fail(ZS_EINVAL, "bad argument");
+    HIPCHK(hipSetDevice(h->device));
+    HIPCHK(hipDeviceSynchronize());
+    std::vector<unsigned long long> buf((size_t)ZS_STAMP_WGS * ZS_NPHASE);
+    HIPCHK(stamps_of(h->G, buf.data(), nullptr, 1));
+    for (int w = 0; w < n_wgs; w++)
+        for (int k = 0; k < n_phase; k++) out[(size_t)w * n_phase + k] = buf[(size_t)w * ZS_NPHASE + k];
+    return ZS_OK;
+#else
+    (void)h; (void)out; (void)n_wgs; (void)n_phase;
     return fail(ZS_ESTATE, "not a ZS_STAMPS diagnostic build");
 #endif
 }

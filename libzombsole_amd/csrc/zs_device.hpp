@@ -1,9 +1,10 @@
 // zs_device.hpp — device-side data layout and primitives of the MI355X zombsole engine.
 //
 // Layout in HBM (N envs, E = A + P + Z entity slots, O obstacles, W x H map, DW = ceil(W*H/32)):
-//   * entity SoA, env-minor [slot][N]: pos (x | y << 16, int16 each), life (int32),
+//   * entity arrays, env-major [N][E] (EIX): pos (x | y << 16, int16 each), life (int32),
 //     weapon (u8), present (u8), serial (u32), order (u8 dict-order list)
-//       -> lanes touching the same slot of consecutive envs issue coalesced accesses.
+//       -> the lanes of an env group (one lane per slot) read one env's contiguous row: a wave of
+//          4 envs x 12 slots touches 3 lines per int32 array instead of one line per slot.
 //   * per-env scalars [k][N] (World.t, deaths, zombie_deaths, ...), agent tracker [a][N].
 //   * env-major per-env blocks (a lane group walks its own env):
 //       dead     [N][DW] u32       dead-body decoration bitmap
@@ -40,6 +41,9 @@
 #define ZS_MT_N 624
 #define ZS_MT_M 397
 #define ZS_RING_WORDS (2 * ZS_MT_N)
+
+// entity slot s of env e in the env-major entity arrays [N][E] (pos, life, weapon, present, order, serial)
+#define EIX(d, s, e) ((size_t)(e) * (d).E + (s))
 
 // per-env scalar rows
 enum {

@@ -28,6 +28,7 @@
 typedef unsigned int zs_v4u __attribute__((ext_vector_type(4)));
 typedef unsigned int zs_v2u __attribute__((ext_vector_type(2)));
 typedef int zs_v2i __attribute__((ext_vector_type(2)));
+typedef int zs_v4i __attribute__((ext_vector_type(4)));
 
 // observations per env
 __host__ __device__ inline int obs_count(int scope, int reward_mode, int A) {
@@ -465,12 +466,11 @@ __global__ void __launch_bounds__(256) k_obs(Dev d, T* out, const uint8_t* mask,
     if (e >= d.N) return;
     if (mask && !mask[e]) return;
     lu8* img = (lu8*)(smem + stat_words * 4 + wave * L.bytes);
-    const int N = d.N;
     obs_build(d, L, img, e, [&](int s, int& p, int& lf, int& wp, int& pr) {
-        p = d.pos[(size_t)s * N + e];
-        lf = d.life[(size_t)s * N + e];
-        wp = d.weapon[(size_t)s * N + e];
-        pr = d.present[(size_t)s * N + e];
+        p = d.pos[EIX(d, s, e)];
+        lf = d.life[EIX(d, s, e)];
+        wp = d.weapon[EIX(d, s, e)];
+        pr = d.present[EIX(d, s, e)];
     });
     obs_stream(d, L, stat_words ? st : nullptr, img, out, e);
 }
@@ -508,16 +508,16 @@ __device__ __forceinline__ zs_v2u obs_dirty(const Dev& d, int e) { return zs_v2u
 // chunk reads hp_init instead of the env's row, a clean dead-body chunk reads dead_zero, and the address
 // selects wait on nothing in flight.
 __device__ __forceinline__ void obs_prefetch_env(const Dev& d, int e, zs_v2u dirty, ObsPrefetch& f) {
-    const int lane = threadIdx.x & 63, N = d.N;
+    const int lane = threadIdx.x & 63;
     const int s = lane < d.E ? lane : d.E - 1;
 #ifndef ZS_OBS_DIAG
 #define ZS_OBS_DIAG 0
 #endif
     const int ee = (ZS_OBS_DIAG & 4) ? 0 : e, ed = (ZS_OBS_DIAG & 2) ? 0 : e, eh = (ZS_OBS_DIAG & 1) ? 0 : e;
-    f.pos = d.pos[(size_t)s * N + ee];
-    f.life = d.life[(size_t)s * N + ee];
-    f.wp = d.weapon[(size_t)s * N + ee];
-    f.pr = d.present[(size_t)s * N + ee];
+    f.pos = d.pos[EIX(d, s, ee)];
+    f.life = d.life[EIX(d, s, ee)];
+    f.wp = d.weapon[EIX(d, s, ee)];
+    f.pr = d.present[EIX(d, s, ee)];
     const uint32_t* dr = d.dead + (size_t)ed * d.DW;
 #pragma unroll
     for (int i = 0; i < OBS_PF_D; i++) {
@@ -749,16 +749,16 @@ __global__ void __launch_bounds__(256) k_obs_gather(Dev d, T* out, const uint8_t
     if (!stat && !act) return;
     const lv4u* st4 = (const lv4u*)smem;
     lu8* img = (lu8*)(smem + (stat ? 16 * d.DW : 0) + wave * L.bytes);
-    const int N = d.N, W = d.W, H = d.H;
+    const int W = d.W, H = d.H;
     if (stat) obs_stage_static4(d, (lv4u*)smem, threadIdx.x, blockDim.x);
     uint32_t hpd = 0;  // arrives with obs_build's loads, used one load round later
     if (act) {
         hpd = d.hp_dirty[e];
         obs_build(d, L, img, e, [&](int s, int& p, int& lf, int& wp, int& pr) {
-            p = d.pos[(size_t)s * N + e];
-            lf = d.life[(size_t)s * N + e];
-            wp = d.weapon[(size_t)s * N + e];
-            pr = d.present[(size_t)s * N + e];
+            p = d.pos[EIX(d, s, e)];
+            lf = d.life[EIX(d, s, e)];
+            wp = d.weapon[EIX(d, s, e)];
+            pr = d.present[EIX(d, s, e)];
         });
     }
     if (stat) __syncthreads();

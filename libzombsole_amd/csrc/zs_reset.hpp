@@ -81,7 +81,7 @@ __device__ __forceinline__ int wave_spawn(const Dev& d, const ResetLds& L, WaveR
         L.lpres[s] = 1;
         __hip_atomic_fetch_or(&L.bm[cell >> 5], 1u << (cell & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         L.lorder[n_order + m] = (uint8_t)s;
-        d.serial[(size_t)s * d.N + e] = (uint32_t)(serial + m + 1);
+        d.serial[EIX(d, s, e)] = (uint32_t)(serial + m + 1);
     }
     n_order += placed;
     serial += placed;
@@ -129,9 +129,9 @@ __device__ __forceinline__ void reset_env_wave(const Dev& d, const ResetLds& L, 
     }
     for (int s = lane; s < E; s += 64) {
         L.lpres[s] = 0;
-        L.lpos[s] = d.pos[(size_t)s * N + e];
-        L.llife[s] = d.life[(size_t)s * N + e];
-        L.lweap[s] = d.weapon[(size_t)s * N + e];
+        L.lpos[s] = d.pos[EIX(d, s, e)];
+        L.llife[s] = d.life[EIX(d, s, e)];
+        L.lweap[s] = d.weapon[EIX(d, s, e)];
     }
     const int odirty = __ballot(nonpos) != 0ull;
     wave_rng_put(r, rv);
@@ -233,11 +233,11 @@ __device__ __forceinline__ void reset_env_wave(const Dev& d, const ResetLds& L, 
     const uint32_t stf = wave_rng_finish(r);
     // write the new world back
     for (int s = lane; s < E; s += 64) {
-        d.pos[(size_t)s * N + e] = L.lpos[s];
-        d.life[(size_t)s * N + e] = L.llife[s];
-        d.weapon[(size_t)s * N + e] = L.lweap[s];
-        d.present[(size_t)s * N + e] = L.lpres[s];
-        d.order[(size_t)s * N + e] = L.lorder[s];
+        d.pos[EIX(d, s, e)] = L.lpos[s];
+        d.life[EIX(d, s, e)] = L.llife[s];
+        d.weapon[EIX(d, s, e)] = L.lweap[s];
+        d.present[EIX(d, s, e)] = L.lpres[s];
+        d.order[EIX(d, s, e)] = L.lorder[s];
     }
     for (int a = lane; a < A; a += 64) {  // reward_tracker.reset / env.agents = possible_agents
         d.prev_life[(size_t)a * N + e] = L.llife[a];
@@ -342,11 +342,11 @@ __device__ __forceinline__ void respawn_env_wave(const Dev& d, const ResetLds& L
     const int lane = threadIdx.x, N = d.N, E = d.E, Z0 = d.A + d.P;
     for (int w = lane; w < d.DW; w += 64) L.bm[w] = d.obstbits[w];
     for (int s = lane; s < E; s += 64) {
-        L.lpos[s] = d.pos[(size_t)s * N + e];
-        L.llife[s] = d.life[(size_t)s * N + e];
-        L.lweap[s] = d.weapon[(size_t)s * N + e];
-        L.lpres[s] = d.present[(size_t)s * N + e];
-        L.lorder[s] = d.order[(size_t)s * N + e];
+        L.lpos[s] = d.pos[EIX(d, s, e)];
+        L.llife[s] = d.life[EIX(d, s, e)];
+        L.lweap[s] = d.weapon[EIX(d, s, e)];
+        L.lpres[s] = d.present[EIX(d, s, e)];
+        L.lorder[s] = d.order[EIX(d, s, e)];
     }
     // occupancy (as k_tick rebuilds it): the map's obstacle cells minus the lost obstacles, then the
     // present things
@@ -398,12 +398,12 @@ __device__ __forceinline__ void respawn_env_wave(const Dev& d, const ResetLds& L
     const uint32_t stf = wave_rng_finish(r);
     for (int m = lane; m < k; m += 64) {  // the new zombies (dropped ones keep their drawn life)
         const int s = L.lslots[m];
-        d.pos[(size_t)s * N + e] = L.lpos[s];
-        d.life[(size_t)s * N + e] = L.llife[s];
-        d.weapon[(size_t)s * N + e] = L.lweap[s];
-        d.present[(size_t)s * N + e] = L.lpres[s];
+        d.pos[EIX(d, s, e)] = L.lpos[s];
+        d.life[EIX(d, s, e)] = L.llife[s];
+        d.weapon[EIX(d, s, e)] = L.lweap[s];
+        d.present[EIX(d, s, e)] = L.lpres[s];
     }
-    for (int m = n0 + lane; m < n0 + placed; m += 64) d.order[(size_t)m * N + e] = L.lorder[m];
+    for (int m = n0 + lane; m < n0 + placed; m += 64) d.order[EIX(d, m, e)] = L.lorder[m];
     if (lane == 0) {
         d.scal[S_NORDER * N + e] = n_order;
         d.scal[S_SERIAL * N + e] = serial;

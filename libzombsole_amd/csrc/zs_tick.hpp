@@ -75,6 +75,8 @@ static __device__ unsigned long long g_stamp_wg[ZS_STAMP_WGS * ZS_NPHASE];
             g_stamp_wg[blockIdx.x * ZS_NPHASE + 19 + (k)] += _t - _g_prev;                \
         _g_prev = _t;                                                                     \
     } while (0)
+// slot 27: envs of the workgroup whose actions the leader executed (serial path or window fallback)
+#define XEV(k) atomicAdd(&g_stamp_wg[blockIdx.x * ZS_NPHASE + 27], (unsigned long long)(k))
 // workgroup timeline of the last launch: s_memrealtime (100 MHz, one clock for the whole chip) at
 // the workgroup's start and end, g_stamp_tl[block][0 / 1]
 static __device__ unsigned long long g_stamp_tl[ZS_STAMP_WGS * 2];
@@ -86,6 +88,7 @@ static __device__ unsigned long long g_stamp_tl[ZS_STAMP_WGS * 2];
     } while (0)
 #else
 #define TL(k)
+#define XEV(k)
 #define GX_DECL
 #define GX(k)
 #define SX(k)
@@ -112,7 +115,7 @@ struct TickLayout {
     int off_lst;
     int off_pos, off_life, off_weap, off_pres;
     int off_region;                          // = off_bm
-    int off_bm, off_rw, off_cand, off_tgt, off_act, off_order, off_rank, off_kind, off_perm, off_moved;
+    int off_bm, off_rw, off_cand, off_tgt, off_act, off_order, off_rank, off_kind, off_perm, off_moved, off_xs;
     int bytes;
 };
 
@@ -162,6 +165,8 @@ __host__ __device__ inline TickLayout tick_layout(int ne, int E, int DW, int rw_
     L.off_moved = o;
     o += E * ne;
     o = ((o + 15) / 16) * 16;
+    L.off_xs = o;  // grp_execute's two tables of 64 words (G per env)
+    o += 2 * 64 * 4;
     // the MT twist buffer (2 x 624 words) and one env's observation image alias the region
     if (o - region < 2 * ZS_MT_N * 4) o = region + 2 * ZS_MT_N * 4;
     if (o - region < obs_bytes) o = region + obs_bytes;
@@ -188,6 +193,7 @@ struct Grp {
     lu8* lperm;
     lu8* lmoved;
     li32* lact;  // agent a's action triple at 3a..3a+2
+    li32* xs;    // grp_execute's tables: table k of this env at xs + 64 k + g G
     // leader registers
     uint32_t st0;  // ring state at the start of the LDS window
     int wpos, wlen;
@@ -348,7 +354,7 @@ __device__ __forceinline__ void place(const Dev& d, Grp& c, int s, int cell) {
     bm_set(c, cell);
     LO(c, c.n_order) = (uint8_t)s;
     c.n_order++;
-    d.serial[(size_t)s * d.N + c.e] = (uint32_t)(++c.serial);
+    d.serial[EIX(d, s, c.e)] = (uint32_t)(++c.serial);
 }
 
 // entry i of the player (which = 0) or zombie (which = 1) spawn list, packed x | y << 16
@@ -771,17 +777,54 @@ __device__ __forceinline__ unsigned long long gballot(const Grp& c, bool p) {
     return gbits<G>(c, __ballot(p));
 }
 
+// The window ran out at position pos (every word before it consumed): the G lanes load the stream's next
+// rw_step words into it, one round trip, as rng_reload does for the leader.  A block the words cross into
+// is twisted first when it is not ready (by lane 0, serially); the refill at the end of every tick and
+// reset leaves the next block ready, and a tick draws far fewer than 624 words, so that does not happen
+// in practice.
+template <int G>
+__device__ __forceinline__ void grp_reload(const Dev& d, Grp& c, int& pos) {
+    const uint32_t st = st_advance(c.st0, (uint32_t)pos);
+    uint32_t off = st & 1023u, slot = (st >> 10) & 1u, ready = (st >> 11) & 1u;
+    uint32_t* ring = d.ring + (size_t)c.e * ZS_RING_WORDS;
+    const int n = d.rw_step;
+    bool twist = false;
+    if (off >= ZS_MT_N) {
+        twist = !ready;
+        if (twist && c.j == 0) mt_twist_serial(ring + (slot ^ 1u) * ZS_MT_N, ring + slot * ZS_MT_N);
+        slot ^= 1u;
+        off = 0;
+        ready = 0;
+    }
+    if ((int)off + n > ZS_MT_N && !ready) {
+        if (c.j == 0) mt_twist_serial(ring + (slot ^ 1u) * ZS_MT_N, ring + slot * ZS_MT_N);
+        twist = true;
+        ready = 1;
+    }
+    if (twist) __threadfence();  // lane 0's block before the lanes' loads
+    wave_sync();
+    for (int k = c.j; k < n; k += G) {
+        const uint32_t q = off + k;
+        c.rw[IX(c, k)] = mt_temper(q < ZS_MT_N ? ring[slot * ZS_MT_N + q] : ring[(slot ^ 1u) * ZS_MT_N + q - ZS_MT_N]);
+    }
+    wave_sync();
+    c.st0 = st_pack(off, slot, ready);
+    c.wlen = n;
+    pos = 0;
+}
+
 // draws t = 0..count-1 of _randbelow(bound(t)) (random.py:239-249) from the env's window words pos, pos+1, ...
 // G words per round: the word of lane j serves draw t_j = done + j - H_j (H_j = rejected words of the round
-// before lane j), solved as a fixed point as in wave_draws.  put(t, value) for every accepted draw.  Returns
-// false when the draws need words past the window (wlen); pos then is unspecified.
+// before lane j), solved as a fixed point as in wave_draws; a round ends at the window's end, and an empty
+// window is reloaded (grp_reload).  put(t, value) for every accepted draw.
 template <int G, class Bound, class Put>
-__device__ __forceinline__ bool grp_draws(const Grp& c, int wlen, int& pos, int count, Bound bound, Put put) {
+__device__ __forceinline__ void grp_draws(const Dev& d, Grp& c, int& pos, int count, Bound bound, Put put) {
     const int j = c.j;
     const unsigned long long below = (1ull << j) - 1ull;
     int done = 0;
     while (done < count) {
-        const bool avail = pos + j < wlen;
+        if (pos >= c.wlen) grp_reload<G>(d, c, pos);
+        const bool avail = pos + j < c.wlen;
         const uint32_t w = avail ? c.rw[IX(c, pos + j)] : 0u;
         unsigned long long rej = 0ull, prev;
         int t, b;
@@ -789,33 +832,31 @@ __device__ __forceinline__ bool grp_draws(const Grp& c, int wlen, int& pos, int 
         do {
             prev = rej;
             t = done + j - __popcll(rej & below);
-            lv = t < count;
+            lv = avail && t < count;
             b = lv ? bound(t) : 1;
             rj = lv && (w >> (__clz(b))) >= (uint32_t)b;  // getrandbits(bit_length(b)) = w >> (32 - bit_length(b))
             rej = gballot<G>(c, rj);
         } while (rej != prev);
         const unsigned long long live = gballot<G>(c, lv);
-        if (gballot<G>(c, lv && !avail)) return false;
         if (lv && !rj) put(t, w >> __clz(b));
         done += __popcll(live) - __popcll(rej);
         pos += 64 - __clzll((long long)live);
     }
-    return true;
 }
 
-// random.shuffle of the n actions LPE(0..n) (n <= 2G) from window word pos on; false (nothing written)
-// when the window is too short
+// random.shuffle of the n actions LPE(0..n) (n <= 2G) from window word pos on.  The draws go to the
+// env's first table as bytes (4G of them).
 template <int G>
-__device__ __forceinline__ bool grp_shuffle(Grp& c, int n, int wlen, int& pos) {
-    if (n < 2) return true;
+__device__ __forceinline__ void grp_shuffle(const Dev& d, Grp& c, int n, int& pos) {
+    if (n < 2) return;
     GX_DECL
     GX(0);
-    const bool ok = grp_draws<G>(
-        c, wlen, pos, n - 1, [&](int t) { return n - t; }, [&](int t, uint32_t v) { LR(c, t) = (uint8_t)v; });
-    if (!ok) return false;
+    lu8* jt8 = (lu8*)(c.xs + c.g * G);
+    grp_draws<G>(d, c, pos, n - 1, [&](int t) { return n - t; }, [&](int t, uint32_t v) { jt8[t] = (uint8_t)v; });
     wave_sync();
     GX(1);
-    // lane j follows the elements at positions j and j + G through the swaps (i = n - 1 - t, j_t)
+    // lane j follows the elements at positions j and j + G through the swaps (i = n - 1 - t, j_t), the
+    // draws read 16 at a time
     int fin[2] = {-1, -1}, el[2] = {0, 0};
 #pragma unroll
     for (int h = 0; h < 2; h++) {
@@ -825,11 +866,16 @@ __device__ __forceinline__ bool grp_shuffle(Grp& c, int n, int wlen, int& pos) {
             fin[h] = k;
         }
     }
-#pragma unroll 4
-    for (int t = 0; t < n - 1; t++) {
-        const int i = n - 1 - t, jt = LR(c, t);
+    const lv4u* jv = (const lv4u*)jt8;
+    for (int t0 = 0; t0 < n - 1; t0 += 16) {
+        const zs_v4u q = jv[t0 >> 4];
 #pragma unroll
-        for (int h = 0; h < 2; h++) fin[h] = fin[h] == i ? jt : (fin[h] == jt ? i : fin[h]);
+        for (int b = 0; b < 16; b++) {
+            const int t = t0 + b, i = n - 1 - t, jt = (int)((q[b >> 2] >> (8 * (b & 3))) & 0xffu);
+            const bool live = t < n - 1;
+#pragma unroll
+            for (int h = 0; h < 2; h++) fin[h] = !live ? fin[h] : fin[h] == i ? jt : (fin[h] == jt ? i : fin[h]);
+        }
     }
     wave_sync();
 #pragma unroll
@@ -837,17 +883,21 @@ __device__ __forceinline__ bool grp_shuffle(Grp& c, int n, int wlen, int& pos) {
         if (fin[h] >= 0) LPE(c, fin[h]) = (uint8_t)el[h];
     wave_sync();
     GX(2);
-    return true;
 }
 
-// execute the shuffled actions LPE(i0..n) chunk by chunk; returns the index of the first action not
-// executed (n when all were; else the leader continues there: the window cannot hold that chunk's draws).
-// Successful movers are appended to LM(nmoved..); odirty is set when an obstacle was hit.
+// execute the shuffled actions LPE(0..n) chunk by chunk.  Successful movers are appended to LM(nmoved..);
+// odirty is set when an obstacle was hit.  The lanes
+// exchange their actions through the env's two tables (t0, t1: one word per lane), read back four
+// words at a time.
 template <int G>
-__device__ __forceinline__ int grp_execute(const Dev& d, Grp& c, int n, int wlen, int& pos, int& nmoved, int& odirty) {
+__device__ __forceinline__ void grp_execute(const Dev& d, Grp& c, int n, int& pos, int& nmoved, int& odirty) {
     const int j = c.j;
     const unsigned long long below = (1ull << j) - 1ull;
     const unsigned long long gfull = G == 64 ? ~0ull : (1ull << G) - 1ull;
+    li32* t0 = c.xs + c.g * G;
+    li32* t1 = c.xs + 64 + c.g * G;
+    const ZS_LDS zs_v4i* t0v = (const ZS_LDS zs_v4i*)t0;
+    const ZS_LDS zs_v4i* t1v = (const ZS_LDS zs_v4i*)t1;
     GX_DECL
     GX(0);
     for (int c0 = 0; c0 < n; c0 += G) {
@@ -870,6 +920,9 @@ __device__ __forceinline__ int grp_execute(const Dev& d, Grp& c, int n, int wlen
             mv = in_bounds(d, tx, ty) && d2(px, py, tx, ty) <= 1;
             dcell = ty * d.W + tx;
         }
+        t0[j] = mv ? tgt : -1;  // valid moves' destinations (packed, >= 0) and sources
+        t1[j] = p;
+        if (act) LR(c, s) = (uint8_t)j;  // the chunk position of each actor (dict ranks are dead by now)
         const bool occ0 = mv && bm_test(c, dcell);
         const bool hits = kind == K_ATTACK || kind == K_HEAL;
         const int et = hits && tgt >= 0 ? tgt : -1;  // an entity target may have moved earlier
@@ -882,25 +935,28 @@ __device__ __forceinline__ int grp_execute(const Dev& d, Grp& c, int n, int wlen
         } else if (et >= 0) {
             tp0 = LP(c, et);
         }
+        wave_sync();
         GX(3);
-        // earlier valid moves of the chunk that leave (vac) or enter this move's cell, and the target's move
+        // earlier valid moves of the chunk that leave (vac) or enter (dep) this move's cell
         unsigned long long dep = 0ull, vac = 0ull;
+        constexpr int UNR = G <= 16 ? G / 4 : 2;  // whole scans up to 16 lanes; wider groups by halves of 8
+#pragma unroll UNR
+        for (int k0 = 0; k0 < G; k0 += 4) {
+            const zs_v4i dv = t0v[k0 >> 2], sv = t1v[k0 >> 2];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const bool e = mv && k0 + u < j && dv[u] >= 0;
+                vac |= (unsigned long long)(e && sv[u] == tgt) << (k0 + u);
+                dep |= (unsigned long long)(e && (sv[u] == tgt || dv[u] == tgt)) << (k0 + u);
+            }
+        }
+        // the target's own move earlier in the chunk
         int tmv = -1, tdst = 0;
-        const int sv = mv ? s : -1, mdst = mv ? tgt : 0;
-#pragma unroll 4
-        for (int k = 0; k < m; k++) {
-            const int sk = __shfl(sv, k, G), srck = __shfl(p, k, G), dstk = __shfl(mdst, k, G);
-            if (k < j && sk >= 0) {
-                if (mv && srck == tgt) {
-                    dep |= 1ull << k;
-                    vac |= 1ull << k;
-                } else if (mv && dstk == tgt) {
-                    dep |= 1ull << k;
-                }
-                if (sk == et) {
-                    tmv = k;
-                    tdst = dstk;
-                }
+        if (et >= 0) {
+            const int k = LR(c, et);
+            if (k < j && LPE(c, c0 + k) == et) {
+                tdst = t0[k];
+                tmv = tdst >= 0 ? k : -1;
             }
         }
         GX(4);
@@ -921,7 +977,7 @@ __device__ __forceinline__ int grp_execute(const Dev& d, Grp& c, int n, int wlen
         int lo = 0, bnd = 1, ml = 100;
         if (hits) {
             ml = tgt >= 0 ? 100 : okind == ZS_THING_BOX ? 10 : 200;  // target_maxlife
-            const int tp = (tgt >= 0 && tmv >= 0 && ((S >> tmv) & 1ull)) ? tdst : tp0;
+            const int tp = (tmv >= 0 && ((S >> tmv) & 1ull)) ? tdst : tp0;
             if (kind == K_ATTACK) {
                 inr = d2(px, py, unpack_x(tp), unpack_y(tp)) <= weapon_r2(w);
                 lo = weapon_lo(w);
@@ -935,40 +991,40 @@ __device__ __forceinline__ int grp_execute(const Dev& d, Grp& c, int n, int wlen
         GX(5);
         const unsigned long long IR = gballot<G>(c, inr);
         const int r = __popcll(IR & below);
-        if (inr) LR(c, r) = (uint8_t)bnd;
+        wave_sync();  // the scans' table reads before the bounds overwrite t1
+        if (inr) t1[r] = bnd;
         wave_sync();
-        const int pos0 = pos;
-        const bool ok = grp_draws<G>(
-            c, wlen, pos, __popcll(IR), [&](int t) { return (int)LR(c, t); },
-            [&](int t, uint32_t v) { LR(c, t) = (uint8_t)v; });
-        if (!ok) {  // nothing of this chunk is committed: the leader takes over here
-            pos = pos0;
-            return c0;
-        }
+        grp_draws<G>(d, c, pos, __popcll(IR), [&](int t) { return (int)t1[t]; }, [&](int t, uint32_t v) { t1[t] = (int)v; });
         wave_sync();
         GX(6);
         // every hit on a target in execution order; the last hitter stores the result
-        const int hv = inr ? (kind == K_ATTACK ? -(lo + (int)LR(c, r)) : lo + (int)LR(c, r)) : 0;
-        int64_t life = 0;
-        if (inr) life = tgt >= 0 ? (int64_t)LL(c, tgt) : (int64_t)ohp;
+        const int hv = inr ? (kind == K_ATTACK ? -(lo + t1[r]) : lo + t1[r]) : 0;
+        wave_sync();
+        t0[j] = inr ? tgt : 0x7fffffff;  // hit targets (0x7fffffff: no hit) and signed hit values
+        t1[j] = hv;
+        wave_sync();
+        int life = 0;
+        if (inr) life = tgt >= 0 ? LL(c, tgt) : ohp;
         bool last = inr;
         uint32_t ovf = 0u;  // an obstacle's life after one of the hits left the int16 / int32 range
-#pragma unroll 4
-        for (int k = 0; k < m; k++) {
-            const int tk = __shfl(tgt, k, G), hk = __shfl(hv, k, G);
-            if (inr && ((IR >> k) & 1ull) && tk == tgt) {
-                if (k <= j) {
-                    life = hk < 0 ? life + hk : min(life + hk, (int64_t)ml);
-                    if (tgt < 0 && life < -32768) {  // hp_store_value of every hit, as the leader stores them
-                        ovf |= ZS_OVF_INT16;
-                        if (life < (int64_t)ZS_HP_FLOOR) {
-                            life = ZS_HP_FLOOR;
-                            ovf |= ZS_OVF_INT32;
-                        }
-                    }
-                } else {
-                    last = false;
+#pragma unroll UNR
+        for (int k0 = 0; k0 < G; k0 += 4) {
+            const zs_v4i tv = t0v[k0 >> 2], hvv = t1v[k0 >> 2];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int k = k0 + u;
+                const bool app = inr && tv[u] == tgt && k <= j;
+                const int hk = hvv[u];
+                // a hit is at most 100: life + hk leaves int32 only below ZS_HP_FLOOR, where an obstacle's life
+                // saturates (hp_store_value of every hit, as the leader stores them); a heal clamps at MAX_LIFE
+                const bool sat = hk < 0 && life < ZS_HP_FLOOR - hk;
+                const int nl = sat ? ZS_HP_FLOOR : (hk < 0 ? life + hk : min(life + hk, ml));
+                if (tgt < 0) {
+                    ovf |= (app && nl < -32768) ? ZS_OVF_INT16 : 0u;
+                    ovf |= (app && sat) ? ZS_OVF_INT32 : 0u;
                 }
+                life = app ? nl : life;
+                last = last && !(inr && tv[u] == tgt && k > j);
             }
         }
         if (last) {
@@ -998,17 +1054,14 @@ __device__ __forceinline__ int grp_execute(const Dev& d, Grp& c, int n, int wlen
         wave_sync();
         GX(7);
     }
-    return n;
 }
 
 // ---------------------------------------------------------------------------
-// leader: the order-dependent rest of the tick (gym_env.py:99-145 / multiagent_env.py:111-171).
-// shuffled: the env's lanes already shuffled the action list and executed its actions before i0
-// (grp_execute; the first nmoved0 movers are in LM), so the leader takes over at action i0.
+// leader: the order-dependent rest of the tick (gym_env.py:99-145 / multiagent_env.py:111-171), where the
+// env's lanes did not execute the actions (a decision deferred to the leader, or more than 2G actions)
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void env_step_leader(const Dev& d, Grp& c, const int32_t* actions, double* rew, uint8_t* done_out,
-                                uint8_t* trunc_out, uint8_t* listed_out, bool shuffled = false, int i0 = 0,
-                                int nmoved0 = 0) {
+                                uint8_t* trunc_out, uint8_t* listed_out) {
     const int A = d.A;
     SUB_DECL
     SUB(0);
@@ -1042,7 +1095,7 @@ __device__ __forceinline__ void env_step_leader(const Dev& d, Grp& c, const int3
         if (LK(c, s) != K_NONE) LPE(c, nact++) = (uint8_t)s;
     }
     // random.shuffle(actions) (core.py:76)
-    for (int i = shuffled ? 0 : nact - 1; i >= 1; i--) {
+    for (int i = nact - 1; i >= 1; i--) {
         int j = rng_below(d, c, i + 1);
         uint8_t tmp = LPE(c, i);
         LPE(c, i) = LPE(c, j);
@@ -1051,15 +1104,15 @@ __device__ __forceinline__ void env_step_leader(const Dev& d, Grp& c, const int3
     SUB(1);
     // execute_actions (core.py:103-119).  The next action's actor, kind, target and position are read
     // ahead: nothing this action does changes them (every actor acts once, and only its own action moves it).
-    int nmoved = nmoved0;
+    int nmoved = 0;
     int s_n = 0, kind_n = K_NONE, tgt_n = 0, p_n = 0;
-    if (i0 < nact) {
-        s_n = LPE(c, i0);
+    if (nact > 0) {
+        s_n = LPE(c, 0);
         kind_n = LK(c, s_n);
         tgt_n = LT(c, s_n);
         p_n = LP(c, s_n);
     }
-    for (int i = i0; i < nact; i++) {
+    for (int i = 0; i < nact; i++) {
         const int s = s_n, kind = kind_n, tgt = tgt_n, p = p_n, x = unpack_x(p), y = unpack_y(p);
         if (i + 1 < nact) {
             s_n = LPE(c, i + 1);
@@ -1353,6 +1406,7 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
     c.lperm = (lu8*)(smem + L.off_perm);
     c.lmoved = (lu8*)(smem + L.off_moved);
     c.lact = (li32*)(smem + L.off_act);
+    c.xs = (li32*)(smem + L.off_xs);
     c.lists = (li32*)(smem + L.off_lists);
     if (d.lists_cap)  // the static spawn lists, staged once per workgroup
         for (int i = lane; i < d.nps + d.nzs; i += 64) c.lists[i] = i < d.nps ? d.pspawn[i] : d.zspawn[i - d.nps];
@@ -1399,12 +1453,14 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
         st = d.rngst[e];
 #pragma unroll
         for (int u = 0; u < 4; u++) {
-            const int s = min(j + u * G, E - 1);
-            vp[u] = d.pos[(size_t)s * N + e];
-            vl[u] = d.life[(size_t)s * N + e];
-            vw[u] = d.weapon[(size_t)s * N + e];
-            vr[u] = d.present[(size_t)s * N + e];
-            vo[u] = d.order[(size_t)s * N + e];
+            const int s = j + u * G;
+            if (s < E) {  // slots past E issue nothing (an all-lanes-false batch is skipped)
+                vp[u] = d.pos[EIX(d, s, e)];
+                vl[u] = d.life[EIX(d, s, e)];
+                vw[u] = d.weapon[EIX(d, s, e)];
+                vr[u] = d.present[EIX(d, s, e)];
+                vo[u] = d.order[EIX(d, s, e)];
+            }
         }
         const int f = min(j, nmisc - 1);
         if (f == MISC_T) mval = d.scal[S_T * N + e];
@@ -1468,19 +1524,18 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
         // the rest of the entity table (E > 4G) (SoA [slot][N]: this env's column)
         {
             auto ix = [&](int s) { return IX(c, s); };
-            const int32_t* pcol = d.pos + e;
-            const int32_t* lcol = d.life + e;
+
             for (int b = j + 4 * G; b < E; b += 4 * G) {
                 int32_t vp[4], vl[4];
                 uint8_t vw[4], vr[4], vo[4];
 #pragma unroll
                 for (int u = 0; u < 4; u++) {
                     int s = min(b + u * G, E - 1);
-                    vp[u] = pcol[(size_t)s * N];
-                    vl[u] = lcol[(size_t)s * N];
-                    vw[u] = d.weapon[(size_t)s * N + e];
-                    vr[u] = d.present[(size_t)s * N + e];
-                    vo[u] = d.order[(size_t)s * N + e];
+                    vp[u] = d.pos[EIX(d, s, e)];
+                    vl[u] = d.life[EIX(d, s, e)];
+                    vw[u] = d.weapon[EIX(d, s, e)];
+                    vr[u] = d.present[EIX(d, s, e)];
+                    vo[u] = d.order[EIX(d, s, e)];
                 }
 #pragma unroll
                 for (int u = 0; u < 4; u++) {
@@ -1571,26 +1626,19 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
     wave_sync();
     STAMP(1);
     if (stepping) {
-        // decisions (start-of-tick state), the group's lanes over the actors
-        for (int k = j; k < n_order; k += G) {
-            int s = LO(c, k), kind, tgt;
-            decide(d, c, s, actions, false, kind, tgt);
-            LK(c, s) = (uint8_t)kind;
-            LT(c, s) = tgt;
-        }
-    }
-    wave_sync();
-    if (stepping) {
-        // the action list of get_actions (core.py:80-101) in dict order, compacted by the group when no
-        // decision was deferred to the leader (RNG-drawing) or raises: MISC_NMOVED = its length, else -1
+        // decisions (start-of-tick state), the group's lanes over the actors in dict order, and the action
+        // list of get_actions (core.py:80-101) compacted from them in the same pass when no decision was
+        // deferred to the leader (RNG-drawing) or raises: MISC_NMOVED = its length, else -1
         int nact = 0;
         unsigned long long special = 0ull;
         for (int b0 = 0; b0 < n_order; b0 += G) {
             const int k = b0 + j;
-            int s = 0, kk = K_NONE;
+            int s = 0, kk = K_NONE, tgt = 0;
             if (k < n_order) {
                 s = LO(c, k);
-                kk = LK(c, s);
+                decide(d, c, s, actions, false, kk, tgt);
+                LK(c, s) = (uint8_t)kk;
+                LT(c, s) = tgt;
             }
             const bool keep = kk == K_MOVE || kk == K_ATTACK || kk == K_HEAL;
             const unsigned long long sb = __ballot(kk == K_DEFER || kk == K_RAISE);
@@ -1615,29 +1663,28 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
         d.scal[S_NEEDRESET * N + e] = 0;
         lst[g] = 1u << 11;  // no MT refill for this env here
     }
+    // the stream window, in every lane of a stepping env (the lanes' draws and the leader's continue it)
+    c.st0 = st0;
+    c.wpos = 0;
+    c.wlen = wlen;
     // the shuffle and execution by the env's lanes when no decision was deferred to the leader (grp_execute)
     bool par = false;
-    int i0 = 0, nm0 = 0, gpos = 0, nact = 0;
+    int nm0 = 0;
     if (stepping && d.par_exec) {
-        nact = MISC(c, MISC_NMOVED);
+        const int nact = MISC(c, MISC_NMOVED);
         if (nact >= 0 && nact <= 2 * G) {
-            int pos = 0;
-            if (grp_shuffle<G>(c, nact, wlen, pos)) {
-                int odirty = 0;
-                i0 = grp_execute<G>(d, c, nact, wlen, pos, nm0, odirty);
-                for (int q = j; q < nm0; q += G) LR(c, LM(c, q)) = 255;  // re-inserted at the end of the dict
-                if (odirty && j == 0) MISC(c, MISC_ODIRTY) = 1;
-                par = true;
-                gpos = pos;
-            }
+            int pos = 0, odirty = 0;
+            grp_shuffle<G>(d, c, nact, pos);
+            grp_execute<G>(d, c, nact, pos, nm0, odirty);
+            for (int q = j; q < nm0; q += G) LR(c, LM(c, q)) = 255;  // re-inserted at the end of the dict
+            if (odirty && j == 0) MISC(c, MISC_ODIRTY) = 1;
+            c.wpos = pos;
+            par = true;
         }
     }
     wave_sync();
     STAMP(3);
     if (leader && stepping) {
-        c.st0 = st0;
-        c.wpos = par ? gpos : 0;
-        c.wlen = wlen;
         c.n_order = n_order;
         c.t = MISC(c, MISC_T) + 1;
         c.deaths = MISC(c, MISC_DEATHS);
@@ -1646,11 +1693,12 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
         c.prevzd = MISC(c, MISC_PREVZD);
         c.serial = MISC(c, MISC_SERIAL);
         c.odirty = MISC(c, MISC_ODIRTY);
-        if (par && i0 >= nact) {  // every action executed by the lanes: what the leader's part hands on
+        if (par) {  // every action executed by the lanes: what the leader's part hands on
             MISC(c, MISC_NMOVED) = nm0;
             MISC(c, MISC_NORD) = c.n_order;
         } else {
-            env_step_leader(d, c, actions, rew, done_out, trunc_out, listed_out, par, i0, nm0);
+            XEV(1);
+            env_step_leader(d, c, actions, rew, done_out, trunc_out, listed_out);
         }
     }
     wave_sync();
@@ -1687,11 +1735,11 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
     STAMP(4);
     if (stepping) {
         for (int s = j; s < E; s += G) {
-            d.pos[(size_t)s * N + e] = LP(c, s);
-            d.life[(size_t)s * N + e] = LL(c, s);
-            d.weapon[(size_t)s * N + e] = LW(c, s);
-            d.present[(size_t)s * N + e] = LPR(c, s);
-            d.order[(size_t)s * N + e] = LO(c, s);
+            d.pos[EIX(d, s, e)] = LP(c, s);
+            d.life[EIX(d, s, e)] = LL(c, s);
+            d.weapon[EIX(d, s, e)] = LW(c, s);
+            d.present[EIX(d, s, e)] = LPR(c, s);
+            d.order[EIX(d, s, e)] = LO(c, s);
         }
         for (int f = j; f < MISC_N + 2 * A; f += G) {
             int v = MISC(c, f);

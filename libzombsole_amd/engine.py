@@ -14,7 +14,7 @@ from . import _abi
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_build", "libzombsole_mi355x.so")
 SYMBOLS = ["zs_last_error", "zs_create", "zs_destroy", "zs_obs_shape", "zs_seed", "zs_reset", "zs_step", "zs_observe",
            "zs_gen_actions", "zs_step_graph", "zs_state_size", "zs_get_state", "zs_set_state", "zs_get_rng", "zs_set_rng", "zs_overflow", "zs_profile", "zs_profile_read", "zs_describe",
-           "zs_debug_stamps", "zs_debug_timeline", "zs_debug_lists"]
+           "zs_debug_stamps", "zs_debug_stamps_wg", "zs_debug_timeline", "zs_debug_lists"]
 
 _lib = None
 
@@ -61,6 +61,7 @@ def load_library(path=None):
     L.zs_describe.argtypes = [vp, C.c_char_p, i32]
     L.zs_debug_lists.argtypes = [vp, C.POINTER(i32), vp]
     L.zs_debug_timeline.argtypes = [vp, vp, i32]
+    L.zs_debug_stamps_wg.argtypes = [vp, vp, i32, i32]
     for s in SYMBOLS:
         if s != "zs_last_error":
             getattr(L, s).restype = C.c_int
@@ -228,6 +229,15 @@ class Engine(object):
         if rc:
             _raise(self.L, rc, "zs_debug_stamps")
         return ssum, smax
+
+    def debug_stamps_wg(self, n_wgs, n_phase):
+        """Per-workgroup phase cycles of the step launches since the last stamps read, shape [n_wgs, n_phase]
+        (diagnostic -DZS_STAMPS build only)."""
+        out = np.zeros((n_wgs, n_phase), dtype=np.uint64)
+        rc = self.L.zs_debug_stamps_wg(self.h, C.c_void_p(out.ctypes.data), n_wgs, n_phase)
+        if rc:
+            _raise(self.L, rc, "zs_debug_stamps_wg")
+        return out
 
     def debug_timeline(self, n):
         """Start / end s_memrealtime (100 MHz) of the first n workgroups of the last fused step launch,

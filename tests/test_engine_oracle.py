@@ -244,15 +244,15 @@ def test_lanes_per_env(lanes):
 
 
 def test_rng_window_reload():
-    """A 32-word RNG window on 54-actor envs (median 82 draws per step): the tick's leader runs its
-    window dry and reloads it from the ring several times per step (core.py:76 shuffle, :168-202
-    attack / heal draws), bit-exact."""
+    """A 32-word RNG window on 54-actor envs (median 82 draws per step): the tick runs its window dry and
+    reloads it from the ring several times per step (core.py:76 shuffle, :168-202 attack / heal draws),
+    by the env's lanes or its leader, bit-exact."""
     run_parity(lambda n: _abi.multi_env_config(n, "safehouse", [], "city128", ["0", "1", "2", "3"],
                                                initial_zombies=50, minimum_zombies=50),
                24, 30, check_state_every=15, launch={"rw_need": 32})
     run_parity(c2, 128, 60, check_state_every=30, graph=True, launch={"rw_need": 32})
-    # 24 actors (C5's shape) on a 32-word window: the lanes' shuffle fits, a chunk's damage draws often
-    # do not, and the leader takes over mid-list from the window's next word
+    # 24 actors (C5's shape) on a 32-word window: the lanes' shuffle and damage draws run the window dry
+    # and reload it themselves (grp_reload) mid-shuffle and mid-chunk
     run_parity(lambda n: _abi.multi_env_config(n, "extermination", [], "bridge64", ["0", "1", "2", "3"],
                                                initial_zombies=20, obs_dtype=_abi.DTYPE_I16, max_episode_steps=200),
                64, 80, check_state_every=40, launch={"rw_need": 32})

@@ -12,7 +12,7 @@ PHASES = ["stage-in", "decide", "grp-exec", "leader", "stage-out", "obs-write", 
           "  L:defer+shuffle", "  L:execute", "  L:order+cleanup", "  L:reward+rules", "  S:to round 1", "  S:to window",
           "R:setup+rng", "R:weapons", "R:spawn p+a", "R:zombie lives", "R:spawn z", "R:twist+out", "-",
           "  G:shuffle draws", "  G:shuffle track", "  G:chunk loads", "  G:chunk scan", "  G:resolve+range",
-          "  G:damage draws", "  G:lives+commit"]
+          "  G:damage draws", "  G:lives+commit", "  leader-exec envs"]
 
 
 def main():
@@ -72,6 +72,7 @@ def main():
             # workgroup timeline of one more fused step launch (s_memrealtime, 10 ns)
             import numpy as np
             n_reset = min(n_envs, launch.get("reset_wgs", 256))
+            eng.debug_stamps(len(PHASES))  # clears: the next read is this one launch's
             eng.gen_actions(31 + steps, 7)
             eng.step()
             torch.cuda.synchronize()
@@ -86,6 +87,22 @@ def main():
             print("     tick wg life   %s" % q(dur[n_reset:]))
             if n_reset:
                 print("     reset wg end   %s" % q(en[:n_reset]))
+            # phase cycles of that launch's slowest 1 % tick workgroups against its median ones
+            ph = eng.debug_stamps_wg(n_reset + wgs, len(PHASES)).astype(np.float64)[n_reset:]
+            life = dur[n_reset:]
+            order = np.argsort(life)
+            slow = order[-max(1, len(order) // 100):]
+            mid = order[len(order) // 2 - len(order) // 20: len(order) // 2 + len(order) // 20]
+            print("     phases of the slowest 1%% (%d wgs, life %.1f us) vs the median 10%% (life %.1f us):" % (
+                len(slow), life[slow].mean(), life[mid].mean()))
+            top = order[-3:][::-1]
+            print("       %-18s %9s  %9s  | slowest three: %s us" % ("", "slowest1%", "median", " ".join("%.1f" % life[w] for w in top)))
+            for k, name in enumerate(PHASES):
+                if name == "-" or name.startswith("R:"):
+                    continue
+                a, b = ph[slow, k].mean(), ph[mid, k].mean()
+                if a or b:
+                    print("       %-18s %9.0f  %9.0f  | %s" % (name.strip(), a, b, " ".join("%9.0f" % ph[w, k] for w in top)))
         eng.close()
 
 
