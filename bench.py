@@ -217,6 +217,11 @@ def max_over_ranks(elapsed, device):
 
 def main():
     args = parse()
+    # ONE JSON line on stdout: anything else the process prints there (RCCL's version banner at its first
+    # communicator, library notices) goes to stderr; the line itself is written to the saved stdout
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     import torch
     import torch.distributed as dist
 
@@ -402,7 +407,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args, builder)
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
     eng.close()
     if distributed:
         dist.destroy_process_group()

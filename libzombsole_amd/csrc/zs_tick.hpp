@@ -142,6 +142,8 @@ __host__ __device__ inline TickLayout tick_layout(int ne, int E, int DW, int rw_
     o += E * ne;
     L.off_pres = o;
     o += E * ne;
+    L.off_order = o;  // the dict order is stored out after the MT refill, whose buffer aliases the region
+    o += E * ne;
     o = ((o + 15) / 16) * 16;
     const int region = o;
     L.off_region = L.off_bm = o;
@@ -154,8 +156,6 @@ __host__ __device__ inline TickLayout tick_layout(int ne, int E, int DW, int rw_
     o += 3 * A * ne * 4;
     L.off_cand = o;
     o += ((cand_cap * ne * 2 + 3) / 4) * 4;
-    L.off_order = o;
-    o += E * ne;
     L.off_rank = o;
     o += E * ne;
     L.off_kind = o;
@@ -226,7 +226,10 @@ __device__ __forceinline__ void rng_reload(const Dev& d, Grp& c) {
     uint32_t off = st & 1023u, slot = (st >> 10) & 1u, ready = (st >> 11) & 1u;
     uint32_t* ring = d.ring + (size_t)c.e * ZS_RING_WORDS;
     if (off >= ZS_MT_N) {
-        if (!ready) mt_twist_serial(ring + (slot ^ 1u) * ZS_MT_N, ring + slot * ZS_MT_N);
+        if (!ready) {
+            mt_twist_serial(ring + (slot ^ 1u) * ZS_MT_N, ring + slot * ZS_MT_N);
+            __threadfence();  // the block's stores before any later read of it (coop_refill's loads)
+        }
         slot ^= 1u;
         off = 0;
         ready = 0;
@@ -234,6 +237,7 @@ __device__ __forceinline__ void rng_reload(const Dev& d, Grp& c) {
     int n = d.rw_step;  // a multiple of 4 (32 .. 512)
     if ((int)off + n > ZS_MT_N && !ready) {
         mt_twist_serial(ring + (slot ^ 1u) * ZS_MT_N, ring + slot * ZS_MT_N);
+        __threadfence();
         ready = 1;
     }
     for (int i0 = 0; i0 < n; i0 += 4) {  // 4 loads in flight (a wider batch costs every caller registers)
@@ -1338,31 +1342,39 @@ __device__ __forceinline__ void env_step_leader_b(const Dev& d, Grp& c, double* 
 }
 
 // ---------------------------------------------------------------------------
-// wave-cooperative MT19937 refill: every env of the workgroup whose next block is not ready
-// gets it twisted by all 64 lanes (3 dependency phases over the 624-word block).
+// wave-cooperative MT19937 refill: every env of the workgroup whose next block is not ready gets it
+// twisted by all 64 lanes (3 dependency phases over the 624-word block): one round of 10 loads per
+// lane, the phases in LDS, the stores.  No workgroup barrier: nothing this wave stored earlier is read
+// (a serial twist of the tick is followed by its own fence), so the loads do not wait for its stores.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void coop_refill(const Dev& d, int base, int count, const lu32* lst, lu32* tw) {
-    const int tid = threadIdx.x, nt = blockDim.x;
+    constexpr int K = (ZS_MT_N + 63) / 64;
+    const int tid = threadIdx.x;
     for (int i = 0; i < count; i++) {
-        uint32_t st = lst[i];
+        const uint32_t st = lst[i];
         if ((st >> 11) & 1u) continue;
-        __syncthreads();  // the leader's stores (incl. a serial twist of this block) are complete
-        uint32_t slot = (st >> 10) & 1u;
+        const uint32_t slot = (st >> 10) & 1u;
         uint32_t* ring = d.ring + (size_t)(base + i) * ZS_RING_WORDS;
         const uint32_t* src = ring + slot * ZS_MT_N;
         uint32_t* dst = ring + (slot ^ 1u) * ZS_MT_N;
-        stage_in(src, ZS_MT_N, tid, nt, tw, [](int k) { return k; });
+        uint32_t v[K];
+#pragma unroll
+        for (int u = 0; u < K; u++) v[u] = src[min(tid + 64 * u, ZS_MT_N - 1)];
+        wave_sync();
+#pragma unroll
+        for (int u = 0; u < K; u++)
+            if (tid + 64 * u < ZS_MT_N) tw[tid + 64 * u] = v[u];
         wave_sync();
         lu32* nw = tw + ZS_MT_N;
-        for (int k = tid; k < ZS_MT_N - ZS_MT_M; k += nt) nw[k] = mt_f(tw[k], tw[k + 1], tw[k + ZS_MT_M]);
+        for (int k = tid; k < ZS_MT_N - ZS_MT_M; k += 64) nw[k] = mt_f(tw[k], tw[k + 1], tw[k + ZS_MT_M]);
         wave_sync();
-        for (int k = (ZS_MT_N - ZS_MT_M) + tid; k < 2 * (ZS_MT_N - ZS_MT_M); k += nt)
+        for (int k = (ZS_MT_N - ZS_MT_M) + tid; k < 2 * (ZS_MT_N - ZS_MT_M); k += 64)
             nw[k] = mt_f(tw[k], tw[k + 1], nw[k + ZS_MT_M - ZS_MT_N]);
         wave_sync();
-        for (int k = 2 * (ZS_MT_N - ZS_MT_M) + tid; k < ZS_MT_N; k += nt)
+        for (int k = 2 * (ZS_MT_N - ZS_MT_M) + tid; k < ZS_MT_N; k += 64)
             nw[k] = mt_f(tw[k], k + 1 < ZS_MT_N ? tw[k + 1] : nw[0], nw[k + ZS_MT_M - ZS_MT_N]);
         wave_sync();
-        for (int k = tid; k < ZS_MT_N; k += nt) dst[k] = nw[k];
+        for (int k = tid; k < ZS_MT_N; k += 64) dst[k] = nw[k];
         if (tid == 0) d.rngst[base + i] = st | (1u << 11);
         wave_sync();
     }
@@ -1733,6 +1745,9 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
     }
     wave_sync();
     STAMP(4);
+    // the MT refill first: its loads do not wait behind the stage-out's stores (one vmcnt for both)
+    coop_refill(d, base, min(NE, env1 - base), lst, (lu32*)(smem + L.off_bm));
+    STAMP(5);
     if (stepping) {
         for (int s = j; s < E; s += G) {
             d.pos[EIX(d, s, e)] = LP(c, s);
@@ -1756,7 +1771,7 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
         }
     }
     wave_sync();
-    STAMP(5);
+    STAMP(6);
     // observations of the envs ticked here (envs reset by this call get theirs from the reset work):
     // the whole wave encodes one env at a time, its image aliasing the dead tick region
     if (d.fobs && obs_out) {
@@ -1776,9 +1791,6 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
             wave_sync();
         }
     }
-    wave_sync();
-    STAMP(6);
-    coop_refill(d, base, min(NE, env1 - base), lst, (lu32*)(smem + L.off_bm));
     STAMP(7);
 }
 

@@ -158,10 +158,11 @@ class Engine(object):
             _raise(self.L, rc, "zs_reset")
         return self.obs
 
-    def outputs(self, rows=None):
+    def outputs(self, rows=None, obs=None, flat=None):
         """A set of step output buffers (StepOutputs) with `rows` >= N rows; the engine writes the
-        first N.  Steps may alternate between sets (double-buffered outputs, vector.StepGather)."""
-        return StepOutputs(self, self.N if rows is None else max(int(rows), self.N))
+        first N.  Steps may alternate between sets (double-buffered outputs, vector.StepGather).  obs / flat,
+        when given, are the storage to use (e.g. this rank's slice of a gather buffer)."""
+        return StepOutputs(self, self.N if rows is None else max(int(rows), self.N), obs, flat)
 
     def step(self, actions=None, out=None):
         """One tick for all envs; `actions` int32 [N, A, 3] device tensor (default: self.actions);
@@ -320,16 +321,21 @@ class StepOutputs(object):
     tensor (`flat`: float64 rewards [rows][R], then done [rows], then truncated [rows]) so a per-step
     exchange moves them in one collective."""
 
-    def __init__(self, eng, rows):
+    def __init__(self, eng, rows, obs=None, flat=None):
         torch = eng.torch
         kw = dict(device=eng.device)
         R = eng.A if eng.multi else 1
         self.rows = rows
-        self.obs = torch.zeros((rows,) + eng.obs_shape, dtype=eng.obs_dtype, **kw)
-        self.flat = torch.zeros(rows * (8 * R + 2), dtype=torch.uint8, **kw)
+        if obs is not None:
+            assert obs.shape == (rows,) + tuple(eng.obs_shape) and obs.dtype == eng.obs_dtype and obs.is_contiguous()
+        if flat is not None:
+            assert flat.dim() == 1 and flat.numel() >= rows * (8 * R + 2) and flat.dtype == torch.uint8
+            assert flat.is_contiguous() and flat.storage_offset() % 8 == 0
+        self.obs = obs if obs is not None else torch.zeros((rows,) + eng.obs_shape, dtype=eng.obs_dtype, **kw)
+        self.flat = flat if flat is not None else torch.zeros(rows * (8 * R + 2), dtype=torch.uint8, **kw)
         self.rewards = self.flat[:8 * R * rows].view(torch.float64).view(rows, R)
         self.done = self.flat[8 * R * rows:(8 * R + 1) * rows]
-        self.trunc = self.flat[(8 * R + 1) * rows:]
+        self.trunc = self.flat[(8 * R + 1) * rows:(8 * R + 2) * rows]
         self.listed = torch.zeros((rows, eng.A), dtype=torch.uint8, **kw)
         self.was_reset = torch.zeros(rows, dtype=torch.uint8, **kw)
 

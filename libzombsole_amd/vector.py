@@ -147,9 +147,11 @@ class StepGather(object):
     step's compute.
 
     Every rank's observation shard plus its rewards / done / truncated are all-gathered into node-wide
-    tensors.  The engine writes each step into one of `depth` output sets (Engine.outputs), padded to
-    the longest shard, so the exchange copies nothing: the observations are one collective and
-    rewards / done / truncated (one flat byte tensor per set, engine.StepOutputs) a second.  Step t
+    tensors.  The engine writes each step into one of `depth` output sets (Engine.outputs) whose storage
+    is this rank's slice of that set's gather buffers, padded to the longest shard, so the exchange copies
+    nothing: the collectives run in place (a rank receives the other ranks' slices only), the observations
+    one collective and rewards / done / truncated (one flat byte tensor per set, engine.StepOutputs) a
+    second.  Step t
     writes set t % depth on the caller's stream; its collectives are issued on a communication stream
     that waits for that step only, so they run while step t + 1 computes into the next set; before a
     set is written again the caller's stream waits for the collectives that read it.  With gloo (CPU
@@ -178,13 +180,16 @@ class StepGather(object):
         self.m = max(self.sizes)
         self.R = engine.A if engine.multi else 1
         self.depth = int(depth)
-        self.sets = [engine.outputs(rows=self.m) for _ in range(self.depth)]
-        shape = tuple(self.sets[0].obs.shape[1:])
         dev = engine.device
-        self.g_obs = [torch.empty((self.world * self.m,) + shape, dtype=self.sets[0].obs.dtype, device=dev)
+        rank = dist.get_rank(group)
+        shape = tuple(engine.obs_shape)
+        nflat = (self.m * (8 * self.R + 2) + 15) // 16 * 16  # a rank's segment; the float64 rewards 8-B aligned
+        self.g_obs = [torch.zeros((self.world * self.m,) + shape, dtype=engine.obs_dtype, device=dev)
                       for _ in range(self.depth)]
-        self.g_flat = [torch.empty(self.world * self.sets[0].flat.numel(), dtype=torch.uint8, device=dev)
-                       for _ in range(self.depth)]
+        self.g_flat = [torch.zeros(self.world * nflat, dtype=torch.uint8, device=dev) for _ in range(self.depth)]
+        # the engine's output sets are this rank's slices of the gather buffers (in-place collectives)
+        self.sets = [engine.outputs(rows=self.m, obs=self.g_obs[k][rank * self.m:(rank + 1) * self.m],
+                                    flat=self.g_flat[k][rank * nflat:(rank + 1) * nflat]) for k in range(self.depth)]
         cuda = dev.type == "cuda"
         self.comm = torch.cuda.Stream(device=dev) if cuda else None
         self.pending = [None] * self.depth  # per set: event after the collectives that read it

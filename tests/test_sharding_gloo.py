@@ -58,8 +58,8 @@ def _worker(rank, world, port, q):
             N, A, multi, obs_shape, obs_dtype, device, torch = n, 2, True, (2, 3, 5, 5), torch.int32, \
                 torch.device("cpu"), torch
 
-            def outputs(self, rows=None):
-                return StepOutputs(self, max(rows or n, n))
+            def outputs(self, rows=None, obs=None, flat=None):
+                return StepOutputs(self, max(rows or n, n), obs, flat)
 
         def run(t):
             def fill(out):
@@ -71,6 +71,8 @@ def _worker(rank, world, port, q):
 
         sg = StepGather(Fake())
         ok = torch.equal(g, g2) and len(sg.sets) == 2 and all(s.obs.shape[0] == 13 for s in sg.sets)
+        # the output sets are this rank's slices of the gather buffers (in-place collectives)
+        ok = ok and all(s.obs.data_ptr() == sg.g_obs[k][13 * rank:].data_ptr() for k, s in enumerate(sg.sets))
         ga = torch.arange(TOTAL)
         for t in range(5):
             used = sg.step(run(t))

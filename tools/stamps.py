@@ -8,7 +8,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 SO = os.path.join(ROOT, "libzombsole_amd", "_build", "libzombsole_mi355x_stamps.so")
-PHASES = ["stage-in", "decide", "grp-exec", "leader", "stage-out", "obs-write", "mt-refill",
+PHASES = ["stage-in", "decide", "grp-exec", "leader", "mt-refill", "stage-out", "obs-write",
           "  L:defer+shuffle", "  L:execute", "  L:order+cleanup", "  L:reward+rules", "  S:to round 1", "  S:to window",
           "R:setup+rng", "R:weapons", "R:spawn p+a", "R:zombie lives", "R:spawn z", "R:twist+out", "-",
           "  G:shuffle draws", "  G:shuffle track", "  G:chunk loads", "  G:chunk scan", "  G:resolve+range",
