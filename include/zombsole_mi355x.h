@@ -111,6 +111,9 @@ extern "C" {
 #define ZS_FLAG_AUTORESET 1u /* next-step autoreset: an env that ended is reset by the next zs_step */
 #define ZS_FLAG_DEBUG 2u     /* debug=True envs (core.py:96-99, 115-119): action kind ZS_ACT_RAISE
                               * stops World.step; without the flag kinds >= 7 are unknown (idle) */
+#define ZS_FLAG_DEATH_LOG 4u /* keep, per env, the things its last step's clean_dead_things removed, in
+                              * removal order (zs_death_log; the drop-in views' decoration order and
+                              * the final values of a removed zombie whose slot a respawn reuses) */
 
 /* ---- range flags (zs_overflow) -------------------------------------------
  * The reference's obstacle life is an unbounded Python int that carries over resets
@@ -279,6 +282,11 @@ int zs_describe(zs_handle* h, char* buf, int32_t len);
 /* Diagnostics: out[0], out[1] = the two pending-reset list counts, out[2] = the deferred-respawn
  * count (after everything queued on stream), out[3] = the list parity the next step drains. */
 int zs_debug_lists(zs_handle* h, int32_t out[4], void* stream);
+/* The things env's last zs_step removed in World.clean_dead_things (core.py:121-138), in removal order
+ * (the dict order at the cleanup): per thing {slot, serial, x, y, life} (its entity record's values at
+ * removal), at most cap entries into out_host; *n_out = how many the step removed.  Needs
+ * ZS_FLAG_DEATH_LOG; an env reset by that step reports none. */
+int zs_death_log(zs_handle* h, int32_t env, int32_t* out_host, int32_t cap, int32_t* n_out, void* stream);
 /* Diagnostic builds compiled with -DZS_STAMPS only (the product .so returns ZS_ESTATE):
  * per-phase k_tick cycle sums / maxima over all workgroup launches since the last call. */
 int zs_debug_stamps(zs_handle* h, uint64_t* sum_out, uint64_t* max_out, int32_t n);

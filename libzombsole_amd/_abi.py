@@ -28,6 +28,7 @@ ENC_SIMPLE, ENC_CHANNELS = 0, 1
 DTYPE_I32, DTYPE_I64, DTYPE_I16 = 0, 1, 2
 FLAG_AUTORESET = 1
 FLAG_DEBUG = 2
+FLAG_DEATH_LOG = 4  # zs_death_log: the drop-in views' decoration order and removed zombies' final values
 OVF_INT16, OVF_INT32 = 1, 2  # zs_overflow range flags
 STATE_HEADER, STATE_ENTITY_WORDS = 16, 8
 

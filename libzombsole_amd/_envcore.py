@@ -22,6 +22,8 @@ from .game import GameView
 class EnvCore(object):
     def __init__(self, builder, map_, rules_name, player_names, agent_ids, agent_weapons, initial_zombies,
                  minimum_zombies, debug, device=None):
+        # the per-step death log feeds the views' decoration order and removed things (game.py)
+        builder.cfg.flags |= _abi.FLAG_DEATH_LOG
         self.engine = Engine(builder, device=device)
         self.torch = self.engine.torch
         self.debug = debug
@@ -78,6 +80,7 @@ class EnvCore(object):
         finally:
             eng.store_python_random(0)
             self.game.invalidate()
+        self.game.after_step()
         if raising is not None:
             raise raising.args[0]
         obs = eng.obs[0].cpu().numpy()

@@ -247,6 +247,8 @@ struct zs_handle {
     int obs_lds = 0;       // k_obs_pipe's walk with LDS-staged 16-B stores (k_obs_lds), channels encoding
     int obs_ring = 0;      // k_obs_ring: encoder and writer waves through an LDS ring (zs_launch.obs_ring)
     size_t obs_ring_bytes = 0;
+    int obs_bring = 0;     // k_obs_bring: its unit slots (0: not used)
+    size_t obs_bring_bytes = 0;
     size_t obs_lds_bytes = 0;
     int obs_patch = 0;     // k_obs_lds's walk with the padded-table encoder (k_obs_patch, zs_launch.obs_patch)
     size_t obs_patch_bytes = 0;
@@ -654,6 +656,7 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
         d.hp_init = p_init;
         d.hp_chunk = std::max(1, (d.O + 31) / 32);
         d.hp_chunk_m = (uint32_t)(((1u << 20) + d.hp_chunk - 1) / d.hp_chunk);
+        d.hp_chunk_m32 = (uint32_t)(((1ull << 32) + d.hp_chunk - 1) / d.hp_chunk);
         std::vector<uint32_t> full(std::max(d.OW, 1), 0u);
         for (int w = 0; w < d.OW; w++) full[w] = d.O - 32 * w >= 32 ? 0xffffffffu : ((1u << (d.O - 32 * w)) - 1u);
         uint32_t* p_full;
@@ -671,6 +674,7 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
         d.dead_zero = p_zero;
         d.dead_chunk = std::max(1, (d.DW + 31) / 32);
         d.dead_chunk_m = (uint32_t)(((1u << 20) + d.dead_chunk - 1) / d.dead_chunk);
+        d.dead_chunk_m32 = (uint32_t)(((1ull << 32) + d.dead_chunk - 1) / d.dead_chunk);
         // exact for every cell when cells * (w_m * W - 2^20) < 2^20 (w_m * W - 2^20 < W)
         d.w_m = (long)d.W * d.H * d.W < (1L << 20) ? (uint32_t)(((1u << 20) + d.W - 1) / d.W) : 0u;
     }
@@ -686,6 +690,10 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
     TRY(dalloc(h, &h->d_rlist[1], N));
     TRY(dalloc(h, &h->d_rcount, 2));
     TRY(dalloc(h, &d.resp_list, N));
+    if (d.flags & ZS_FLAG_DEATH_LOG) {
+        TRY(dalloc(h, &d.dlog, (size_t)N * E * 5));
+        TRY(dalloc(h, &d.dlog_n, N));
+    }
     TRY(dalloc(h, &d.resp_count, 1));
     {
         // observation images: k_obs (four envs per workgroup when their images fit 64 KiB, else one;
@@ -790,6 +798,19 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
                 h->obs_gather_stat = d.obs_stat && gb + 16 * (size_t)d.DW <= 64 * 1024 && h->ov.obs_gather_stat >= 0;
             }
         }
+        // k_obs_bring: k_obs_gather's window-only fetches as the encoders of a k_obs_ring-style ring, when
+        // the dead-body and present rows fit the encoders' load rounds and two unit slots fit beside the
+        // static tables and the encoder images.  zs_launch.obs_ring = -1 keeps k_obs_gather.
+        if (h->obs_gather && d.obs_stat && d.obs_enc == ZS_ENC_CHANNELS && d.E <= 64 && d.DW <= 64 * BRING_D &&
+            d.OW <= 64 * BRING_O && h->ov.obs_ring >= 0) {
+            const int ts = d.obs_dtype == ZS_DTYPE_I64 ? 8 : d.obs_dtype == ZS_DTYPE_I32 ? 4 : 2;
+            const int us = bring_slots(d.DW, h->obs_gl.bytes, ts, nobs, 160 * 1024);
+            const size_t bb = (size_t)bring_fixed_bytes(d.DW, h->obs_gl.bytes) + (size_t)us * bring_unit_bytes(ts, nobs);
+            if (us >= 2 && obs_attr(d.obs_dtype, OBSK_BRING, nobs, 0, (int)bb) == hipSuccess) {
+                h->obs_bring = us;
+                h->obs_bring_bytes = bb;
+            }
+        }
         // with the store-stream kernel available the observations are its job (measured faster than
         // writing them from the tick workgroups at both 8192 and 65536 envs); zs_launch.fobs forces them
         // into the step launch
@@ -797,6 +818,13 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
         d.fobs = L.bytes + 4 * d.obs_stat <= 16 * 1024 && h->ov.fobs >= 0;
         if (h->obs_pipe && h->ov.fobs <= 0) d.fobs = 0;
         if (d.defer_respawn) d.fobs = 0;  // the observations must see k_respawn's zombies
+        // the tick's part of them by k_obs_pipe's walk over its own envs (zs_tick.hpp fobs_pipe) for the
+        // shape k_obs_pipe serves, else the generic per-cell encoder
+        d.fobs_pipe = d.fobs && !world && d.obs_w == 21 && (nobs == 1 || nobs == 2 || nobs == 4) && d.obs_stat &&
+                              L.hp_cap && L.win && d.O > 0 && d.E <= 64 && d.DW <= 64 * OBS_PF_D &&
+                              d.O <= 64 * OBS_PF_H && d.OW <= 64
+                          ? nobs
+                          : 0;
     }
     // Fused step launch (reset work + tick in one) when the whole launch is resident at once: then
     // the step is one latency-bound round and the reset work hides under the ticks (measured: 8192
@@ -945,6 +973,16 @@ static int launch_obs(zs_handle* h, void* obs, const uint8_t* mask, hipStream_t 
         o.grid = (unsigned)std::min((env1 - env0 + 3) / 4, 256 * h->obs_pipe_wgs);
         o.block = 256;
         o.lds = h->obs_lds ? h->obs_lds_bytes : (size_t)d.obs_stat * 4 + 4 * (size_t)h->obs_l.bytes;
+    } else if (!mask && h->obs_bring) {  // every env of [env0, env1): window-only encoders, writer waves
+        const int ts = d.obs_dtype == ZS_DTYPE_I64 ? 8 : d.obs_dtype == ZS_DTYPE_I32 ? 4 : 2;
+        const int pair = ring_pair(ts, h->obs_gather);
+        o.kind = OBSK_BRING;
+        o.nobs = h->obs_gather;
+        o.grid = (unsigned)std::min((env1 - env0 + pair - 1) / pair, 256);
+        o.block = 64 * (BRING_ENC + BRING_WRT);
+        o.lds = h->obs_bring_bytes;
+        o.L = h->obs_gl;
+        o.us = h->obs_bring;
     } else if (h->obs_gather) {  // one env per wave, four per workgroup, window-only fetches
         o.kind = OBSK_GATHER;
         o.nobs = h->obs_gather;
@@ -1419,7 +1457,7 @@ extern "C" int zs_describe(zs_handle* h, char* buf, int32_t len) {
     const Dev& d = h->d;
     const char* obs_kernel = d.fobs ? "step launch"
                              : h->obs_pipe ? (h->obs_ring ? "k_obs_ring" : h->obs_patch ? "k_obs_patch" : h->obs_lds ? "k_obs_lds" : "k_obs_pipe")
-                             : h->obs_gather ? "k_obs_gather" : "k_obs";
+                             : h->obs_bring ? "k_obs_bring" : h->obs_gather ? "k_obs_gather" : "k_obs";
     snprintf(buf, (size_t)len,
              "{\"envs\": %d, \"entities\": %d, \"lanes_per_env\": %d, \"step_kernel\": \"%s\", \"step_lds\": %zu, "
              "\"step_wgs_per_cu\": %d, \"rng_window\": %d, \"obs_kernel\": \"%s\", \"reset_side_stream\": %d, "
@@ -1427,6 +1465,26 @@ extern "C" int zs_describe(zs_handle* h, char* buf, int32_t len) {
              d.N, d.E, h->G, h->fused ? "k_step" : "k_tick", h->lds, h->resident, d.rw_cap, obs_kernel, h->reset_side,
              h->reset_lds, d.defer_respawn ? "k_respawn" : "tick", h->fused ? ZS_FUSED_WAVES : h->tick_waves, d.rw_step,
              d.par_exec);
+    return ZS_OK;
+}
+
+extern "C" int zs_death_log(zs_handle* h, int32_t env, int32_t* out_host, int32_t cap, int32_t* n_out, void* stream) {
+    if (!h || !n_out || (cap > 0 && !out_host)) return fail(ZS_EINVAL, "null argument");
+    if (!h->d.dlog) return fail(ZS_EINVAL, "the handle was created without ZS_FLAG_DEATH_LOG");
+    if (env < 0 || env >= h->d.N) return fail(ZS_EINVAL, "env out of range");
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(hipSetDevice(h->device));
+    int32_t n = 0;
+    HIPCHK(hipMemcpyAsync(&n, h->d.dlog_n + env, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    n = std::max(0, std::min(n, h->d.E));
+    const int k = std::min(n, std::max(0, (int)cap));
+    if (k > 0) {
+        HIPCHK(hipMemcpyAsync(out_host, h->d.dlog + (size_t)env * h->d.E * 5, sizeof(int32_t) * 5 * k,
+                              hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+    }
+    *n_out = n;
     return ZS_OK;
 }
 

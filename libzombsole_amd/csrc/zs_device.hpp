@@ -99,6 +99,7 @@ struct Dev {
     int lists_cap;   // static spawn-list entries staged in LDS per workgroup (0 = read from global)
     int rlists_cap;  // the same for the reset work (k_reset has its own LDS budget; = lists_cap when fused)
     int fobs;        // observations are written by the step launch itself (tick and reset work)
+    int fobs_pipe;   // ... by the tick's k_obs_pipe walk (zs_tick.hpp fobs_pipe): observations per env, else 0
     int defer_respawn;  // zombie respawn left to k_respawn (wave per env) instead of the tick's leader
     int par_exec;       // the env's lanes execute the shuffled actions (zs_tick.hpp grp_execute), else its leader
     ObsLayout obsl;  // one env's observation image (zs_obs.hpp)
@@ -148,6 +149,7 @@ struct Dev {
     const int32_t* hp_init;  // [O] Box / Wall MAX_LIFE
     int hp_chunk;            // ceil(O / 32)
     uint32_t hp_chunk_m;     // ceil(2^20 / hp_chunk): o / hp_chunk = (o * hp_chunk_m) >> 20 for o < 2^16 / hp_chunk
+    uint32_t hp_chunk_m32;   // ceil(2^32 / hp_chunk): o / hp_chunk = umulhi(o, hp_chunk_m32) for every o < 2^32 / hp_chunk
     // [N]: bit k set once a dead-body word of chunk k (words k * dead_chunk .. + dead_chunk - 1) may be
     // non-zero (tick cleanup, zs_set_state; k_reset clears it with the row): the prefetching observation
     // kernels read a clean chunk from dead_zero, so an env with few bodies reads few dead words
@@ -155,6 +157,7 @@ struct Dev {
     const uint32_t* dead_zero;  // [DW] zeros
     int dead_chunk;             // ceil(DW / 32)
     uint32_t dead_chunk_m;      // ceil(2^20 / dead_chunk), as hp_chunk_m
+    uint32_t dead_chunk_m32;    // ceil(2^32 / dead_chunk), as hp_chunk_m32
     const uint32_t* opres_full;  // [OW] every obstacle present (the row of an env with no HP chunk dirty)
     uint32_t w_m;               // ceil(2^20 / W): c / W = (c * w_m) >> 20 for every cell c (0: not exact, divide)
     uint32_t* obst_present;
@@ -176,6 +179,10 @@ struct Dev {
     int32_t* cand;
     int* resp_list;   // envs whose respawn the tick deferred to k_respawn [N]
     int* resp_count;
+    // ZS_FLAG_DEATH_LOG: per env, the things its last tick's cleanup removed, {slot, serial, x, y, life}
+    // each in removal order ([N][E][5]), and their count ([N]); null = not kept
+    int32_t* dlog;
+    int32_t* dlog_n;
     // sticky range flags of the handle (zs_overflow): ZS_OVF_INT16 once an obstacle's life went below
     // the int16 range (int16 observations then saturate it), ZS_OVF_INT32 once one saturated at
     // ZS_HP_FLOOR (the engine then differs from the reference's unbounded int)

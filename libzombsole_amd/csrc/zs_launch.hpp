@@ -42,7 +42,7 @@ ZS_TICK_DECL(64)
 #undef ZS_TICK_DECL
 
 // observation kernels
-enum { OBSK_OBS = 0, OBSK_GATHER, OBSK_PIPE, OBSK_LDS, OBSK_PATCH, OBSK_RING };
+enum { OBSK_OBS = 0, OBSK_GATHER, OBSK_PIPE, OBSK_LDS, OBSK_PATCH, OBSK_RING, OBSK_BRING };
 struct ObsLaunch {
     int kind;         // OBSK_*
     int nobs;         // 1, 2 or 4 (k_obs: any)
@@ -55,6 +55,7 @@ struct ObsLaunch {
     ObsLayout L;
     int env0, env1;
     int stat;         // k_obs: static words staged; k_obs_gather: static words from LDS tables
+    int us;           // k_obs_bring: unit slots of the ring
 };
 #define ZS_OBS_DECL(T)                                                              \
     hipError_t launch_obs_##T(const ObsLaunch& o, hipStream_t s, const Dev& d); \

@@ -1167,6 +1167,7 @@ __device__ __forceinline__ void env_step_leader(const Dev& d, Grp& c, const int3
 template <int G>
 __device__ __forceinline__ void env_cleanup_group(const Dev& d, Grp& c, bool run) {
     const int A = d.A, j = c.j;
+    const bool stepping_ = run;
     const int nm = run ? MISC(c, MISC_NMOVED) : -1;
     run = run && nm >= 0;  // nm < 0: this step re-raised an agent's exception (debug) and ended there
     const int K = run ? MISC(c, MISC_NORD) : 0;
@@ -1190,7 +1191,7 @@ __device__ __forceinline__ void env_cleanup_group(const Dev& d, Grp& c, bool run
     }
     const int total = run ? K + nm : 0;
     uint32_t* deadbits = d.dead + (size_t)c.e * d.DW;
-    int kept = 0;
+    int kept = 0, nlog = 0;
     for (int b0 = 0; b0 < total; b0 += G) {
         const int idx = b0 + j;
         int s = 0;
@@ -1218,7 +1219,23 @@ __device__ __forceinline__ void env_cleanup_group(const Dev& d, Grp& c, bool run
         const unsigned long long gb = G == 64 ? bal : (bal >> (c.g * G)) & ((1ull << G) - 1ull);
         if (keep) LO(c, kept + __popcll(gb & ((1ull << j) - 1ull))) = (uint8_t)s;
         kept += __popcll(gb);
+        if (d.dlog) {  // ZS_FLAG_DEATH_LOG: the removed things in dict order
+            const bool gone = idx < total && (idx >= K || LR(c, s) != 255) && !keep;
+            const unsigned long long db = __ballot(gone);
+            const unsigned long long gd = G == 64 ? db : (db >> (c.g * G)) & ((1ull << G) - 1ull);
+            if (gone) {
+                int32_t* en = d.dlog + ((size_t)c.e * d.E + nlog + __popcll(gd & ((1ull << j) - 1ull))) * 5;
+                const int32_t p = LP(c, s);
+                en[0] = s;
+                en[1] = (int32_t)d.serial[EIX(d, s, c.e)];
+                en[2] = unpack_x(p);
+                en[3] = unpack_y(p);
+                en[4] = LL(c, s);
+            }
+            nlog += __popcll(gd);
+        }
     }
+    if (d.dlog && stepping_ && j == 0) d.dlog_n[c.e] = nlog;
     // what the leader's respawn and rules read, from the cleaned-up table: present zombies, any player
     // alive (Rules.players_alive), any agent alive, an alive player off the objectives (Safehouse)
     int nz = 0;
@@ -1347,36 +1364,151 @@ __device__ __forceinline__ void env_step_leader_b(const Dev& d, Grp& c, double* 
 // lane, the phases in LDS, the stores.  No workgroup barrier: nothing this wave stored earlier is read
 // (a serial twist of the tick is followed by its own fence), so the loads do not wait for its stores.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void coop_refill(const Dev& d, int base, int count, const lu32* lst, lu32* tw) {
+// env e's next block (slot ^ 1 of the stream state st) twisted by one wave through tw (2 x 624 LDS
+// words of that wave), then marked ready in the env's stream state
+__device__ __forceinline__ void wave_refill(const Dev& d, int e, uint32_t st, lu32* tw, int lane) {
     constexpr int K = (ZS_MT_N + 63) / 64;
-    const int tid = threadIdx.x;
+    const uint32_t slot = (st >> 10) & 1u;
+    uint32_t* ring = d.ring + (size_t)e * ZS_RING_WORDS;
+    const uint32_t* src = ring + slot * ZS_MT_N;
+    uint32_t* dst = ring + (slot ^ 1u) * ZS_MT_N;
+    uint32_t v[K];
+#pragma unroll
+    for (int u = 0; u < K; u++) v[u] = src[min(lane + 64 * u, ZS_MT_N - 1)];
+    wave_sync();
+#pragma unroll
+    for (int u = 0; u < K; u++)
+        if (lane + 64 * u < ZS_MT_N) tw[lane + 64 * u] = v[u];
+    wave_sync();
+    lu32* nw = tw + ZS_MT_N;
+    for (int k = lane; k < ZS_MT_N - ZS_MT_M; k += 64) nw[k] = mt_f(tw[k], tw[k + 1], tw[k + ZS_MT_M]);
+    wave_sync();
+    for (int k = (ZS_MT_N - ZS_MT_M) + lane; k < 2 * (ZS_MT_N - ZS_MT_M); k += 64)
+        nw[k] = mt_f(tw[k], tw[k + 1], nw[k + ZS_MT_M - ZS_MT_N]);
+    wave_sync();
+    for (int k = 2 * (ZS_MT_N - ZS_MT_M) + lane; k < ZS_MT_N; k += 64)
+        nw[k] = mt_f(tw[k], k + 1 < ZS_MT_N ? tw[k + 1] : nw[0], nw[k + ZS_MT_M - ZS_MT_N]);
+    wave_sync();
+    for (int k = lane; k < ZS_MT_N; k += 64) dst[k] = nw[k];
+    if (lane == 0) d.rngst[e] = st | (1u << 11);
+    wave_sync();
+}
+
+__device__ __forceinline__ void coop_refill(const Dev& d, int base, int count, const lu32* lst, lu32* tw) {
     for (int i = 0; i < count; i++) {
         const uint32_t st = lst[i];
-        if ((st >> 11) & 1u) continue;
-        const uint32_t slot = (st >> 10) & 1u;
-        uint32_t* ring = d.ring + (size_t)(base + i) * ZS_RING_WORDS;
-        const uint32_t* src = ring + slot * ZS_MT_N;
-        uint32_t* dst = ring + (slot ^ 1u) * ZS_MT_N;
-        uint32_t v[K];
+        if (!((st >> 11) & 1u)) wave_refill(d, base + i, st, tw, threadIdx.x);
+    }
+}
+
+
+// ---------------------------------------------------------------------------
+// Observations written by the step launch itself (Dev::fobs_pipe, zs_launch.fobs), for the registered
+// shape k_obs_pipe serves (surroundings of width 21, static tables, staged HP, window map): the tick
+// wave, right after its stage-out, runs k_obs_pipe's walk over its own stepping envs.  The entity
+// tables come from the tick's LDS, the dead-body / present / HP words are loaded one env ahead (a clean
+// chunk from the shared rows), the compact image and the static tables alias the dead tick region, and
+// the cells go out as per-cell stores (obs_cell_lds, obs_store).  The step's stores then start as each
+// workgroup finishes its tick instead of after the slowest one, and the separate observation launch
+// (its dispatch, first load round and drain) is gone.
+// ---------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ void fobs_pipe_env(const Dev& d, const ObsLayout& L, const lv4u* st4, const lu8* img, T* out,
+                                              int e, int nobs, int lane) {
+    constexpr int WW = 21, PLANE = WW * WW, PER = (PLANE + 63) / 64;
+    const li32* pos = (const li32*)(img + L.off_pos);
+    const bool ch = d.obs_enc == ZS_ENC_CHANNELS;
+    const int C = ch ? 3 : 1;
+#pragma unroll 1
+    for (int a = 0; a < nobs; a++) {
+        const int32_t ap = pos[a];
+        const int ox = unpack_x(ap) - WW / 2, oy = unpack_y(ap) - WW / 2;
+        const lu8* wm = img + a * PLANE;
+        T* o = out + ((size_t)e * nobs + a) * C * PLANE;
 #pragma unroll
-        for (int u = 0; u < K; u++) v[u] = src[min(tid + 64 * u, ZS_MT_N - 1)];
-        wave_sync();
+        for (int i = 0; i < PER; i++) {
+            const int cell = lane + 64 * i;
+            const int cc = cell < PLANE ? cell : PLANE - 1;
+            const int r = cc / WW, q = cc - r * WW;
+            int code, lf, weapon;
+            obs_cell_lds(d, L, st4, img, wm, cc, ox + q, oy + r, code, lf, weapon);
+            if (cell < PLANE) obs_store(o, PLANE, cell, ch, code, lf, weapon);
+        }
+    }
+}
+
+template <int NE>
+__device__ __forceinline__ void fobs_pipe(const Dev& d, const Grp& c, uint8_t* region, unsigned long long stepmask,
+                                          int G, int base, void* obs_out) {
+    constexpr int WW = 21, PLANE = WW * WW;
+    const int lane = threadIdx.x;
+    const ObsLayout& L = d.obsl;
+    lv4u* st4 = (lv4u*)region;
+    lu8* img = (lu8*)(region + 16 * d.DW);
+    const int nobs = d.fobs_pipe;
+    const int code_s = lane < d.A ? (d.obs_enc == ZS_ENC_CHANNELS ? d.agent_codes[lane < d.A ? lane : 0] : ZS_THING_AGENT)
+                                  : (lane < d.A + d.P ? ZS_THING_PLAYER : ZS_THING_ZOMBIE);
+    obs_stage_static4(d, st4, lane, 64);
+    // Every word this launch wrote (the tick's HP stores, its dead-body and dirty-mask atomics) is read
+    // with device-scope loads, which bypass the CU's L1: a line the tick loaded earlier may be there.
+    auto ld = [](const void* p) { return __hip_atomic_load((const uint32_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    // the envs' dirty masks (lane g: env base + g; a lane past the stepping envs reads env base)
+    const int gl = lane < NE && ((stepmask >> (lane * G)) & 1ull) ? lane : 0;
+    const uint32_t hdl = ld(d.hp_dirty + base + gl), ddl = ld(d.dead_dirty + base + gl);
+    // obs_prefetch_env's dead-body / present / HP words of env e (the entity slots come from LDS)
+    auto prefetch = [&](int g, ObsPrefetch& f) {
+        const int e = base + g;
+        const uint32_t hd = (uint32_t)__builtin_amdgcn_readlane((int)hdl, g), dd = (uint32_t)__builtin_amdgcn_readlane((int)ddl, g);
+        const uint32_t* dr = d.dead + (size_t)e * d.DW;
 #pragma unroll
-        for (int u = 0; u < K; u++)
-            if (tid + 64 * u < ZS_MT_N) tw[tid + 64 * u] = v[u];
+        for (int i = 0; i < OBS_PF_D; i++) {
+            const int w = min(lane + 64 * i, d.DW - 1);
+            f.dead[i] = ld((((dd >> ((w * d.dead_chunk_m) >> 20)) & 1u) ? dr : d.dead_zero) + w);
+        }
+        f.opres = ld((hd ? d.obst_present + (size_t)e * d.OW : d.opres_full) + min(lane, d.OW - 1));
+        const int32_t* hr = d.obst_hp + (size_t)e * d.O;
+#pragma unroll
+        for (int i = 0; i < OBS_PF_H; i++) {
+            const int o = min(lane + 64 * i, d.O - 1);
+            f.hp[i] = (int32_t)ld((((hd >> ((o * d.hp_chunk_m) >> 20)) & 1u) ? hr : d.hp_init) + o);
+        }
+    };
+    int g2 = stepmask ? (__ffsll((long long)stepmask) - 1) / G : NE;
+    ObsPrefetch f;
+    if (g2 < NE) prefetch(g2, f);
+    while (g2 < NE) {
+        // this env's entity slots from the tick's LDS tables (lane s: slot s), then its image
+        const int s = lane < d.E ? lane : 0;
+        f.pos = c.lpos[s * NE + g2];
+        f.life = c.llife[s * NE + g2];
+        f.wp = c.lweap[s * NE + g2];
+        f.pr = c.lpres[s * NE + g2];
+        obs_build_compact(d, L, img, f, code_s, lane);
+        // the next stepping env's words, issued ahead of this env's stores
+        const unsigned long long rest = stepmask & ~((2ull << (g2 * G)) - 1ull);
+        const int gn = rest ? (__ffsll((long long)rest) - 1) / G : NE;
+        if (gn < NE) prefetch(gn, f);
         wave_sync();
-        lu32* nw = tw + ZS_MT_N;
-        for (int k = tid; k < ZS_MT_N - ZS_MT_M; k += 64) nw[k] = mt_f(tw[k], tw[k + 1], tw[k + ZS_MT_M]);
+        {  // window maps: every present entity's slot + 1 in each agent's window
+            const li32* pos = (const li32*)(img + L.off_pos);
+            const lv2i* ent = (const lv2i*)(img + L.off_life);
+            if (lane < d.E && ((ent[lane].x >> 16) & 1)) {
+                const int32_t p = pos[lane];
+                const int x = unpack_x(p), y = unpack_y(p);
+                for (int a = 0; a < nobs; a++) {
+                    const int32_t ap = pos[a];
+                    const int dx = x - (unpack_x(ap) - WW / 2), dy = y - (unpack_y(ap) - WW / 2);
+                    if (dx >= 0 && dy >= 0 && dx < WW && dy < WW) img[a * PLANE + dy * WW + dx] = (uint8_t)(lane + 1);
+                }
+            }
+        }
         wave_sync();
-        for (int k = (ZS_MT_N - ZS_MT_M) + tid; k < 2 * (ZS_MT_N - ZS_MT_M); k += 64)
-            nw[k] = mt_f(tw[k], tw[k + 1], nw[k + ZS_MT_M - ZS_MT_N]);
+        const int e = base + g2;
+        if (d.obs_dtype == ZS_DTYPE_I64) fobs_pipe_env(d, L, st4, img, (int64_t*)obs_out, e, nobs, lane);
+        else if (d.obs_dtype == ZS_DTYPE_I32) fobs_pipe_env(d, L, st4, img, (int32_t*)obs_out, e, nobs, lane);
+        else fobs_pipe_env(d, L, st4, img, (int16_t*)obs_out, e, nobs, lane);
         wave_sync();
-        for (int k = 2 * (ZS_MT_N - ZS_MT_M) + tid; k < ZS_MT_N; k += 64)
-            nw[k] = mt_f(tw[k], k + 1 < ZS_MT_N ? tw[k + 1] : nw[0], nw[k + ZS_MT_M - ZS_MT_N]);
-        wave_sync();
-        for (int k = tid; k < ZS_MT_N; k += 64) dst[k] = nw[k];
-        if (tid == 0) d.rngst[base + i] = st | (1u << 11);
-        wave_sync();
+        g2 = gn;
     }
 }
 
@@ -1774,7 +1906,9 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
     STAMP(6);
     // observations of the envs ticked here (envs reset by this call get theirs from the reset work):
     // the whole wave encodes one env at a time, its image aliasing the dead tick region
-    if (d.fobs && obs_out) {
+    if (d.fobs && obs_out && d.fobs_pipe) {
+        fobs_pipe<NE>(d, c, smem + L.off_region, __ballot(stepping && leader), G, base, obs_out);
+    } else if (d.fobs && obs_out) {
         const unsigned long long stepmask = __ballot(stepping && leader);  // bit g * G per stepping env
         lu8* img = (lu8*)(smem + L.off_region);
         lu32* st = d.obs_stat ? (lu32*)(smem + L.off_region + d.obsl.bytes) : nullptr;

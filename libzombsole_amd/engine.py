@@ -14,7 +14,7 @@ from . import _abi
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_build", "libzombsole_mi355x.so")
 SYMBOLS = ["zs_last_error", "zs_create", "zs_destroy", "zs_obs_shape", "zs_seed", "zs_reset", "zs_step", "zs_observe",
            "zs_gen_actions", "zs_step_graph", "zs_state_size", "zs_get_state", "zs_set_state", "zs_get_rng", "zs_set_rng", "zs_overflow", "zs_profile", "zs_profile_read", "zs_describe",
-           "zs_debug_stamps", "zs_debug_stamps_wg", "zs_debug_timeline", "zs_debug_lists"]
+           "zs_debug_stamps", "zs_debug_stamps_wg", "zs_debug_timeline", "zs_debug_lists", "zs_death_log"]
 
 _lib = None
 
@@ -60,6 +60,7 @@ def load_library(path=None):
     L.zs_debug_stamps.argtypes = [vp, vp, vp, i32]
     L.zs_describe.argtypes = [vp, C.c_char_p, i32]
     L.zs_debug_lists.argtypes = [vp, C.POINTER(i32), vp]
+    L.zs_death_log.argtypes = [vp, i32, C.POINTER(i32), i32, C.POINTER(i32), vp]
     L.zs_debug_timeline.argtypes = [vp, vp, i32]
     L.zs_debug_stamps_wg.argtypes = [vp, vp, i32, i32]
     for s in SYMBOLS:
@@ -119,6 +120,8 @@ class Engine(object):
         self.obs_shape = tuple(int(v) for v in shp)
         self.N = builder.cfg.num_envs
         self.A = builder.num_agents
+        c = builder.cfg
+        self.E = self.A + builder.num_bots + max(c.initial_zombies, c.minimum_zombies)  # entity slots (zs_create)
         self.multi = builder.cfg.reward_mode == _abi.REWARD_MULTI
         dt = {_abi.DTYPE_I32: torch.int32, _abi.DTYPE_I64: torch.int64, _abi.DTYPE_I16: torch.int16}
         self.obs_dtype = dt[builder.cfg.obs_dtype]
@@ -256,6 +259,16 @@ class Engine(object):
         if rc:
             _raise(self.L, rc, "zs_debug_lists")
         return tuple(int(v) for v in out)
+
+    def death_log(self, env):
+        """The things env's last step removed in clean_dead_things (core.py:121-138), in removal order:
+        a list of (slot, serial, x, y, life).  Needs a config with FLAG_DEATH_LOG."""
+        out = (C.c_int32 * (5 * max(1, self.E)))()
+        n = C.c_int32(0)
+        rc = self.L.zs_death_log(self.h, int(env), out, int(self.E), C.byref(n), self._stream())
+        if rc:
+            _raise(self.L, rc, "zs_death_log")
+        return [tuple(int(v) for v in out[5 * k:5 * k + 5]) for k in range(min(n.value, self.E))]
 
     def get_state(self, env):
         buf = np.zeros(self.state_words, dtype=np.int32)

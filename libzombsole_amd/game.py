@@ -35,7 +35,10 @@ class MapView(object):
 class WorldView(object):
     """`core.World` attributes read by user code: size, t, deaths, zombie_deaths, things,
     decoration (core.py:12-22).  `things` is a fresh dict in the reference's insertion
-    order: present obstacles in map-file order, then dynamic things in dict order."""
+    order: present obstacles in map-file order, then dynamic things in dict order.
+    `decoration` is in the reference's insertion order too: the map's objectives, then every
+    cell in the order a body first landed on it (core.py:24-31,121-128), the value the last body
+    placed there; the order comes from the engine's per-step death log (ZS_FLAG_DEATH_LOG)."""
 
     def __init__(self, game):
         self._game = game
@@ -64,14 +67,17 @@ class WorldView(object):
     def decoration(self):
         g = self._game
         st = g._state()
-        dead = set(st.dead_cells())
         W = self.size[0]
+        dead = set(st.dead_cells())
         out = {}
-        for (x, y) in g.map.objectives:
-            c = y * W + x
-            out[(x, y)] = DeadBody("dead body", (x, y)) if c in dead else ObjectiveLocation((x, y))
+        for p, name in g._deco.items():
+            c = p[1] * W + p[0]
+            if name is None:  # an objective no body has landed on
+                out[p] = ObjectiveLocation(p)
+            elif c in dead:
+                out[p] = DeadBody(name, p)
             dead.discard(c)
-        for c in sorted(dead):
+        for c in sorted(dead):  # bodies the log did not see (zs_set_state pokes)
             p = (c % W, c // W)
             out[p] = DeadBody("dead body", p)
         return out
@@ -222,6 +228,9 @@ class GameView(object):
         """Fresh objects after a reset (the reference builds a new World and new players,
         game.py:151-169)."""
         self._cache = None
+        # World.decoration's keys in insertion order -> the name of the body on the cell (None: the
+        # objective spawned there by the map, game.py:151-155)
+        self._deco = {tuple(p): None for p in self.map.objectives}
         A = len(self.agent_ids)
         self.agents = [Agent(self, i, self.agent_ids[i]) for i in range(A)]
         self.players = [Player(self, A + j, self.player_names[j]) for j in range(len(self.player_names))]
@@ -231,6 +240,17 @@ class GameView(object):
         for j, p in enumerate(self.players):
             self._views[A + j] = p
         self.world = WorldView(self)
+
+    def after_step(self):
+        """Book-keeping of a step the env took (EnvCore.tick): the bodies its cleanup left, in the
+        order it removed the things (core.py:121-128), and the final values of the removed things
+        into their views (a removed zombie's slot may be reused by the same step's respawn)."""
+        for slot, serial, x, y, life in self.engine.death_log(self.env):
+            v = self._views.get(slot)
+            if v is not None and v._serial == serial:
+                v._finalize(x, y, life)
+            # things.py:64,118 (agents and bots always have a view; a zombie slot may have none)
+            self._deco[(x, y)] = ("dead " + v.name) if isinstance(v, Player) else "zombie remains"
 
     def _entity(self, slot):
         v = self._views.get(slot)

@@ -12,8 +12,10 @@ reference (`isinstance(thing, Zombie)`, `thing.life`, `agent.position`,
   * `life` is writable (the tests' pokes, `tests/test_game.py:55,105`,
     `tests/test_multiagent_env.py:108`) and goes to the device through `zs_set_state`.
 
-A view of a zombie whose slot is later reused by a respawned zombie keeps reporting the
-values it last saw (the reference object would simply no longer be in the world).
+A thing removed by a step's cleanup keeps its values at removal, as the reference object does once
+it is out of the world: the drop-in env hands each step's removals (the engine's death log) to the
+views, so a zombie view reports its final position and life even when the same step's respawn
+reuses its slot (GameView.after_step).
 """
 from . import _abi
 
@@ -134,12 +136,22 @@ class _EntityView(object):
         self._slot = slot
         self._serial = int(game._state().ent[slot][7])
         self._last = None
+        self._gone = False
 
     def _row(self):
+        if self._gone:
+            return self._last
         r = self._game._state().ent[self._slot]
         if int(r[7]) == self._serial:
             self._last = [int(v) for v in r]
         return self._last
+
+    def _finalize(self, x, y, life):
+        """Removed from the world with these values (core.py:121-138)."""
+        r = list(self._row())
+        r[1], r[2], r[3], r[4] = 0, int(x), int(y), int(life)
+        self._last = r
+        self._gone = True
 
     @property
     def position(self):
@@ -157,6 +169,10 @@ class _EntityView(object):
 
     @life.setter
     def life(self, value):
+        if self._gone:  # no longer in the world: the reference object just holds the value
+            self._last = list(self._last)
+            self._last[4] = int(value)
+            return
         self._game._poke_entity(self._slot, int(value))
         self._last = None
 
@@ -177,7 +193,7 @@ class Zombie(_EntityView, FightingThing):
 
     @property
     def dead_decoration(self):
-        return DeadBody("dead zombie", self.position)
+        return DeadBody("zombie remains", self.position)  # things.py:64
 
 
 class Player(_EntityView, FightingThing):

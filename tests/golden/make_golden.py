@@ -132,6 +132,17 @@ CONFIGS = [
      {"poke_obstacles": [[5, -32700], [6, -32720], [7, -32760]],
       "actions": [{"action_type": "attack", "parameter": [1, 0]},
                   {"action_type": "attack", "parameter": [-1, 0]}]}),
+    # env.game views (golden_driver.ViewTracker): World.decoration in insertion order (bodies over
+    # objectives and over earlier bodies), zombie identity across respawns, the values a removed zombie
+    # keeps; respawns under a minimum count reuse the dead zombies' slots in the same step
+    ("views_multi_bridge_a4_z20_respawn", "multi", "rich",
+     dict(rules_name="extermination", player_names=["terminator"], map_name="bridge",
+          agent_ids=["0", "1", "2", "3"], initial_zombies=20, minimum_zombies=15,
+          agent_weapons=["shotgun", "rifle", "axe", "gun"]), [31, 32], 150, 1, 0, {"views": True}),
+    ("views_single_fort_safehouse", "single", "rich",
+     dict(rules_name="safehouse", player_names=["terminator", "sniper"], map_name="fort", agent_id=0,
+          initial_zombies=30, minimum_zombies=30, observation_scope="surroundings:11",
+          observation_position_encoding="channels", agent_weapon="shotgun"), [33], 150, 1, 60, {"views": True}),
 ]
 
 

@@ -55,6 +55,45 @@ def canonical_state(game, obstacles, K):
             "agents": agents, "players": players}
 
 
+class ViewTracker(object):
+    """extras["views"]: per call, World.decoration in its dict order ([x, y, class, name]), the zombies
+    of World.things in dict order with a stable identity ([ident, x, y, life]; the same object keeps
+    its ident, a respawned zombie is a new one), and after a step the zombies that left the world
+    since the previous call, read through the objects the driver still holds ([ident, x, y, life]:
+    the reference object keeps its values at removal, core.py:121-138)."""
+
+    def __init__(self, K):
+        self.K = K
+        self.held = {}  # ident -> object
+        self.ids = {}   # id(object) -> ident
+        self.next = 0
+
+    def new_world(self):
+        self.held, self.ids = {}, {}
+
+    def record(self, game, rec, step):
+        K = self.K
+        w = game.world
+        rec["deco"] = [[p[0], p[1], type(d).__name__, getattr(d, "name", "")] for p, d in w.decoration.items()]
+        zs, seen = [], set()
+        for t in w.things.values():
+            if isinstance(t, K.Zombie):
+                k = self.ids.get(id(t))
+                if k is None:
+                    k = self.ids[id(t)] = self.next
+                    self.held[k] = t
+                    self.next += 1
+                seen.add(k)
+                zs.append([k, t.position[0], t.position[1], t.life])
+        rec["zid"] = zs
+        if step:
+            rec["zgone"] = [[k, t.position[0], t.position[1], t.life] for k, t in sorted(self.held.items())
+                            if k not in seen]
+        for k in [k for k in self.held if k not in seen]:
+            del self.ids[id(self.held[k])]
+            del self.held[k]
+
+
 def obs_bytes_single(obs):
     return np.ascontiguousarray(obs, dtype="<i4").tobytes()
 
@@ -92,6 +131,7 @@ def run_config(cfg, K):
         for i, life in extras.get("poke_obstacles", []):
             obstacles[i].life = life
         recs = []
+        views = ViewTracker(K) if extras.get("views") else None
         random.seed(seed)
         obs, _ = env.reset()
         need_reset = False
@@ -101,6 +141,8 @@ def run_config(cfg, K):
             if call == 0 or need_reset:
                 if call > 0:
                     obs, _ = env.reset()
+                if views:
+                    views.new_world()
                 rec["kind"] = "reset"
                 need_reset = False
                 elapsed = 0
@@ -165,6 +207,8 @@ def run_config(cfg, K):
                     rec["obs"] = [np.asarray(obs[k], dtype=np.int64).ravel().tolist() for k in keys]
             rec["obs_sha"] = h256(ob)
             rec["state"] = canonical_state(game, obstacles, K)
+            if views:
+                views.record(game, rec, rec["kind"] == "step")
             recs.append(rec)
         out.append({"seed": seed, "calls": recs})
     res = {"name": name, "surface": surface, "stream": stream, "kwargs": dict(cfg[3]),

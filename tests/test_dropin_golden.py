@@ -31,7 +31,7 @@ def _cfg(fx):
 
 
 # the 32-agent fort fixture is covered through the batched ABI (test_engine_golden)
-NAMES = [n for n in G.fixture_names() if "fort" not in n]
+NAMES = [n for n in G.fixture_names() if n != "multi_fort_a32_z100"]
 
 
 @pytest.mark.parametrize("name", NAMES)

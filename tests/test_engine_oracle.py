@@ -133,8 +133,9 @@ PATHS = {
     "obs_in_step": {"fobs": 1},               # observations written by the step / reset launches
     "obs_in_step_unfused": {"fobs": 1, "fused": -1},
     "obs_k_obs": {"fobs": -1, "obs_pipe": -1, "obs_gather": -1},  # one-env-per-wave k_obs
-    "obs_gather": {"fobs": -1, "obs_pipe": -1},  # window-only fetches (k_obs_gather)
-    "obs_gather_scell": {"fobs": -1, "obs_pipe": -1, "obs_gather_stat": -1},  # ... global static words
+    "obs_gather": {"fobs": -1, "obs_pipe": -1, "obs_ring": -1},  # window-only fetches (k_obs_gather)
+    "obs_gather_scell": {"fobs": -1, "obs_pipe": -1, "obs_ring": -1, "obs_gather_stat": -1},  # ... global static words
+    "obs_bring": {"fobs": -1, "obs_pipe": -1},  # window-only encoders + writer waves (k_obs_bring)
     "obs_pipe_cells": {"obs_lds": -1},          # k_obs_pipe's per-cell stores instead of k_obs_lds
     "obs_lds": {"obs_lds": 1},                 # the LDS-staged store stream at any env count (k_obs_patch)
     "obs_lds_select": {"obs_lds": 1, "obs_patch": -1},  # ... k_obs_lds's per-cell select chain
@@ -220,13 +221,16 @@ def test_store_stream_every_phase(patch):
                64, 60, n_discrete=6, check_state_every=30, launch=lo)
 
 
-@pytest.mark.parametrize("stat", [-1, 1])
-def test_city128_gather_paths(stat):
-    """C4's observation kernel (k_obs_gather): static words from the LDS tables (default) or one
-    global load per window cell."""
+CITY128_OBS = {"bring": {}, "gather": {"obs_ring": -1}, "gather_scell": {"obs_ring": -1, "obs_gather_stat": -1}}
+
+
+@pytest.mark.parametrize("path", sorted(CITY128_OBS))
+def test_city128_obs_paths(path):
+    """C4's observation kernels: k_obs_bring (default: window-only encoders, writer waves), k_obs_gather
+    with static words from the LDS tables or one global load per window cell."""
     run_parity(lambda n: _abi.multi_env_config(n, "safehouse", [], "city128", ["0", "1", "2", "3"],
                                                initial_zombies=50, minimum_zombies=50),
-               24, 30, check_state_every=15, launch={"obs_gather_stat": stat})
+               24, 30, check_state_every=15, launch=CITY128_OBS[path])
 
 
 @pytest.mark.parametrize("lanes", [4, 8, 16, 32, 64])

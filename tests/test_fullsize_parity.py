@@ -179,14 +179,22 @@ def test_c5_65536_int16_truncation_waves():
 
 
 def test_c4_16384_graph():
-    """C4: city128 safehouse, 4 agents + 50 zombies (minimum 50): k_obs_gather, k_respawn after zombie deaths
-    and safehouse / all-dead autoresets, at full size."""
+    """C4: city128 safehouse, 4 agents + 50 zombies (minimum 50): k_obs_bring (window-only encoders and
+    writer waves), k_respawn after zombie deaths and safehouse / all-dead autoresets, at full size."""
     def respawned(eng):
+        assert eng.describe()["obs_kernel"] == "k_obs_bring"
         # every zombie death leaves a deficit under minimum 50 that the same step's respawn fills
         zd = sum(eng.get_state(e).zombie_deaths for e in range(0, 16384, 97))
         assert zd > 0, "no zombie died in the sampled envs: k_respawn untested"
         assert eng.describe()["respawn"] == "k_respawn"
     run_full(c4, 16384, 80, min_resets=1, after=respawned)
+
+
+def test_c4_4096_gather():
+    """C4's map through k_obs_gather (the big-map kernel without writer waves)."""
+    def gather(eng):
+        assert eng.describe()["obs_kernel"] == "k_obs_gather"
+    run_full(c4, 4096, 40, min_resets=0, launch={"obs_ring": -1}, after=gather)
 
 
 def test_c3_8192_shard_eager():
@@ -201,6 +209,21 @@ def test_c3_8192_shard_graph():
         desc = eng.describe()
         assert desc["step_kernel"] == "k_step" and desc["par_exec"] == 1, desc
     run_full(c3, 8192, 60, seed0=6 * 8192, after=fused)
+
+
+def test_c3_8192_shard_graph_obs_in_step():
+    """The 8 192-env shard with the observations written by the step launch (zs_launch.fobs: the ticks run
+    k_obs_pipe's walk over their own envs, zs_tick.hpp fobs_pipe; the reset work writes its envs')."""
+    def in_step(eng):
+        assert eng.describe()["obs_kernel"] == "step launch"
+    run_full(c3, 8192, 60, seed0=2 * 8192, launch={"fobs": 1}, after=in_step)
+
+
+def test_c5_8192_int16_obs_in_step():
+    """C5's shard (int16, 4 agents) with the observations written by the step launch; TimeLimit 16, so the
+    reset work (which then writes its envs' observations too) runs every 16 steps."""
+    r = run_full(lambda n: c5(n, max_steps=16), 8192, 40, seed0=5 * 8192, launch={"fobs": 1}, min_resets=2 * 8192)
+    assert r >= 2 * 8192
 
 
 def test_c3_8192_shard_serial_exec():

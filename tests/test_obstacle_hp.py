@@ -222,6 +222,66 @@ def test_raise_kind_only_in_debug_envs():
         eng.close()
 
 
+BIG_ENCODERS = {"k_obs_bring": {}, "k_obs_gather": {"obs_ring": -1}}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kernel", sorted(BIG_ENCODERS))
+@pytest.mark.parametrize("dtype", [_abi.DTYPE_I64, _abi.DTYPE_I16])
+def test_big_map_encoders_on_poked_states(dtype, kernel):
+    """The big-map observation kernels (C4's city128: 3689 obstacles, 512 dead-body words, past the register
+    prefetch of the store-stream kernels) against the oracle's encoder (gym/observation.py:57-173) on poked
+    states: dead bodies in every dead-body chunk (clean chunks read the shared zero row), damaged and
+    cleaned-up obstacles in several HP chunks (clean chunks read hp_init), lives below the int16 range.
+    1536 envs: k_obs_bring's 256 workgroups walk six envs each, so its four ring slots are reused."""
+    from libzombsole_amd.engine import Engine
+    from oracle.oracle import OracleEnv
+    n = 1536
+
+    def cfg(k):
+        return _abi.multi_env_config(k, "safehouse", [], "city128", ["0", "1", "2", "3"], initial_zombies=50,
+                                     minimum_zombies=50, obs_dtype=dtype)
+
+    eng = Engine(cfg(n).set_launch(BIG_ENCODERS[kernel]))
+    assert eng.describe()["obs_kernel"] == kernel
+    eng.seed([1300 + i for i in range(n)])
+    eng.reset()
+    rng = np.random.default_rng(12)
+    st0 = eng.get_state(0)
+    W, cells = st0.W, st0.W * st0.H
+    refs = {}
+    for e in range(n):
+        if e % 3 and e % 97:  # every third env and a scattered set poked; the others as reset
+            continue
+        o = OracleEnv(cfg(1))
+        o.seed(1300 + e)
+        o.reset()
+        st = eng.get_state(e)
+        dw = st.dead_words.view(np.uint32)
+        for c in rng.choice(cells, size=(0, 30, 400, 3000)[e % 4], replace=False):
+            dw[int(c) >> 5] |= np.uint32(1 << (int(c) & 31))
+            o.poke_dead(int(c) % W, int(c) // W)
+        for i in rng.choice(st.O, size=(0, 5, 40, 200)[(e // 3) % 4], replace=False):
+            st.obst_life[i] = int(rng.integers(-40000, 199))
+            o.poke_obstacle(int(i), int(st.obst_life[i]))
+            if st.obst_life[i] <= 0 and rng.integers(2):
+                st.obst_present[i] = 0
+                o.poke_obstacle_gone(int(i))
+        eng.set_state(e, st)
+        refs[e] = o
+    got = eng.observe().cpu().numpy()
+    for e, o in refs.items():
+        assert np.array_equal(got[e], o.obs()), ("obs", kernel, e)
+    # envs left as reset: the reset observation of the same seed
+    for e in (1, 2, 4, 1535):
+        if e in refs:
+            continue
+        o = OracleEnv(cfg(1))
+        o.seed(1300 + e)
+        assert np.array_equal(got[e], o.reset()), ("reset obs", kernel, e)
+    eng.close()
+
+
 ENCODERS = {"k_obs_patch": {"obs_lds": 1, "obs_ring": -1, "obs_patch": 1},
             "k_obs_lds": {"obs_lds": 1, "obs_ring": -1, "obs_patch": -1},
             "k_obs_ring": {"obs_lds": 1, "obs_ring": 1}}
