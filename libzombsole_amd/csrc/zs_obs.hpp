@@ -520,6 +520,9 @@ struct ObsPrefetch {
 
 // {hp_dirty, dead_dirty} of env e
 __device__ __forceinline__ zs_v2u obs_dirty(const Dev& d, int e) { return zs_v2u{d.hp_dirty[e], d.dead_dirty[e]}; }
+// dirty masks that read every chunk from the env's own rows: for a kernel's first env, whose masks
+// would otherwise be one more load round ahead of its first store (the rows hold the values either way)
+#define OBS_OWN_ROWS (zs_v2u{~0u, ~0u})
 
 // Every load is unconditional (addresses clamped into the row): a load under a lane predicate
 // becomes a branch whose join needs the loaded value, i.e. a wait right after the prefetch.
@@ -617,7 +620,7 @@ __global__ void __launch_bounds__(256, ZS_OBS_PIPE_WAVES) k_obs_pipe(Dev d, T* o
     const int code_s = lane < d.A ? (ch ? d.agent_codes[lane < d.A ? lane : 0] : ZS_THING_AGENT)
                                   : (lane < d.A + d.P ? ZS_THING_PLAYER : ZS_THING_ZOMBIE);
     ObsPrefetch f;
-    obs_prefetch(d, e, min(e + waves, env1 - 1), obs_dirty(d, e), f);
+    obs_prefetch(d, e, min(e + waves, env1 - 1), OBS_OWN_ROWS, f);
     for (; e < env1; e += waves) {
         obs_build_compact(d, L, img, f, code_s, lane);  // the image of env e from the registers
         // the next env (the last wave re-reads its own), with the dirty masks its prefetch loaded
@@ -908,7 +911,7 @@ __global__ void __launch_bounds__(256, ZS_OBS_PIPE_WAVES) k_obs_lds(Dev d, T* ou
     ObsPrefetch fa, fb;
     {
         const int e1 = min(e + waves, env1 - 1);
-        obs_prefetch(d, e, min(e + 2 * waves, env1 - 1), obs_dirty(d, e), fa);
+        obs_prefetch(d, e, min(e + 2 * waves, env1 - 1), OBS_OWN_ROWS, fa);
         obs_prefetch(d, e1, min(e1 + 2 * waves, env1 - 1), obs_dirty(d, e1), fb);
     }
     build(fa);
@@ -1215,7 +1218,7 @@ __global__ void __launch_bounds__(64 * PATCH_WPG, ZS_OBS_PIPE_WAVES) k_obs_patch
     ObsPrefetch fa, fb;
     {
         const int e1 = min(e + waves, env1 - 1);
-        obs_prefetch(d, e, min(e + 2 * waves, env1 - 1), obs_dirty(d, e), fa);
+        obs_prefetch(d, e, min(e + 2 * waves, env1 - 1), OBS_OWN_ROWS, fa);
         obs_prefetch(d, e1, min(e1 + 2 * waves, env1 - 1), obs_dirty(d, e1), fb);
     }
     pe.build(d, fa);
@@ -1401,7 +1404,7 @@ __global__ void __launch_bounds__(64 * (RING_ENC + RING_WRT), 1) k_obs_ring(Dev 
     // encoding of one env
     ObsPrefetch fa, fb;
     zs_v2u qa, qb;
-    obs_prefetch_env(d, envc(t), obs_dirty(d, envc(t)), fa);
+    obs_prefetch_env(d, envc(t), OBS_OWN_ROWS, fa);
     obs_prefetch_env(d, envc(t + RING_ENC), obs_dirty(d, envc(t + RING_ENC)), fb);
     qa = obs_dirty(d, envc(t + 2 * RING_ENC));
     qb = obs_dirty(d, envc(t + 3 * RING_ENC));

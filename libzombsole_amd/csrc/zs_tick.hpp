@@ -1402,6 +1402,28 @@ __device__ __forceinline__ void coop_refill(const Dev& d, int base, int count, c
 }
 
 
+// The HBM home of MISC row f of env e (MISC_NMOVED / MISC_NORD: none): an int32 word of the scalar rows
+// or of prev_life, or (listed, rows MISC_N + A ..) a byte, as one address select instead of a branch per
+// row (every row a separate masked load or store)
+static_assert(MISC_T == S_T && MISC_DEATHS == S_DEATHS && MISC_ZD == S_ZD && MISC_EPSTEPS == S_EPSTEPS &&
+                  MISC_PREVZD + 2 == S_PREVZD && MISC_SERIAL + 2 == S_SERIAL && MISC_ODIRTY + 2 == S_ODIRTY,
+              "MISC rows -> scalar rows");
+__device__ __forceinline__ int32_t* misc_word(const Dev& d, int f, int e) {
+    const size_t N = d.N;
+    return f < MISC_NMOVED ? d.scal + (size_t)(f < MISC_PREVZD ? f : f + 2) * N + e
+                           : d.prev_life + (size_t)(f - MISC_N) * N + e;  // f < MISC_N + A
+}
+__device__ __forceinline__ int misc_load(const Dev& d, int f, int e) {
+    if (f >= MISC_N + d.A) return d.listed[(size_t)(f - MISC_N - d.A) * d.N + e];
+    const int v = *misc_word(d, f < MISC_NMOVED || f >= MISC_N ? f : 0, e);
+    return f == MISC_NMOVED || f == MISC_NORD ? 0 : v;
+}
+__device__ __forceinline__ void misc_store(const Dev& d, int f, int e, int v) {
+    if (f == MISC_NMOVED || f == MISC_NORD) return;
+    if (f >= MISC_N + d.A) d.listed[(size_t)(f - MISC_N - d.A) * d.N + e] = (uint8_t)v;
+    else *misc_word(d, f, e) = v;
+}
+
 // ---------------------------------------------------------------------------
 // Observations written by the step launch itself (Dev::fobs_pipe, zs_launch.fobs), for the registered
 // shape k_obs_pipe serves (surroundings of width 21, static tables, staged HP, window map): the tick
@@ -1517,7 +1539,8 @@ __device__ __forceinline__ void fobs_pipe(const Dev& d, const Grp& c, uint8_t* r
 // ---------------------------------------------------------------------------
 // envs [env0, env1) of this launch; workgroup wg takes the NE envs from env0 + wg * NE.
 // EARLY (the one-round fused launch, whose register budget has room): the RNG window's first 4G words
-// are loaded as soon as the stream state is in, overlapped with the first load round, instead of after it
+// are loaded in registers right after the first load round and reach LDS only after the decisions, so
+// their round trip (it needs the stream state) overlaps the decisions instead of the stage-in
 template <int G, bool EARLY = false>
 __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* actions, double* rew, uint8_t* done_out,
                                         uint8_t* trunc_out, uint8_t* listed_out, uint8_t* reset_out, int* reset_list,
@@ -1571,7 +1594,6 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
     int mval = 0, av = 0;
     uint32_t bmv[8], opw = 0u;
     uint32_t wv[4];  // EARLY: the window's words j, j + G, j + 2G, j + 3G (raw)
-    uint32_t woff = 0, wslot = 0, wready = 0;
     uint64_t pseed = 0, pstep = 0;  // the fused policy's inputs (zs_step_graph)
     // the window of the stream state st: its first word (off, slot, ready) and length
     auto window = [&](uint32_t st_, uint32_t& off, uint32_t& slot, uint32_t& ready) {
@@ -1606,33 +1628,12 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
                 vo[u] = d.order[EIX(d, s, e)];
             }
         }
-        const int f = min(j, nmisc - 1);
-        if (f == MISC_T) mval = d.scal[S_T * N + e];
-        else if (f == MISC_DEATHS) mval = d.scal[S_DEATHS * N + e];
-        else if (f == MISC_ZD) mval = d.scal[S_ZD * N + e];
-        else if (f == MISC_EPSTEPS) mval = d.scal[S_EPSTEPS * N + e];
-        else if (f == MISC_PREVZD) mval = d.scal[S_PREVZD * N + e];
-        else if (f == MISC_SERIAL) mval = d.scal[S_SERIAL * N + e];
-        else if (f == MISC_ODIRTY) mval = d.scal[S_ODIRTY * N + e];
-        else if (f == MISC_NMOVED || f == MISC_NORD) mval = 0;
-        else if (f < MISC_N + A) mval = d.prev_life[(size_t)(f - MISC_N) * N + e];
-        else mval = d.listed[(size_t)(f - MISC_N - A) * N + e];
+        mval = misc_load(d, min(j, nmisc - 1), e);
         // occupancy is rebuilt here, not kept in HBM: the map's obstacle cells (static, shared by every
         // env, cache-resident), minus the obstacles this env has lost, plus its present things
 #pragma unroll
         for (int u = 0; u < 8; u++) bmv[u] = d.obstbits[min(j + u * G, d.DW - 1)];
         opw = d.obst_present[(size_t)e * d.OW + min(j, d.OW - 1)];
-        if constexpr (EARLY) {
-            if (needs_reset == 0) {  // waits for the first two loads of the round only
-                wlen = window(st, woff, wslot, wready);
-                const uint32_t* ring = d.ring + (size_t)e * ZS_RING_WORDS;
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const uint32_t q = woff + min(j + u * G, max(wlen - 1, 0));
-                    wv[u] = q < ZS_MT_N ? ring[wslot * ZS_MT_N + q] : ring[(wslot ^ 1u) * ZS_MT_N + q - ZS_MT_N];
-                }
-            }
-        }
     }
     stepping = active && needs_reset == 0;
     if (active && d.pol_n) {
@@ -1695,34 +1696,25 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
             }
         }
         // the rest of the per-env scalars and reward tracker / env.agents rows (more rows than lanes)
-        for (int f = j + G; f < nmisc; f += G) {
-            int v;
-            if (f == MISC_T) v = d.scal[S_T * N + e];
-            else if (f == MISC_DEATHS) v = d.scal[S_DEATHS * N + e];
-            else if (f == MISC_ZD) v = d.scal[S_ZD * N + e];
-            else if (f == MISC_EPSTEPS) v = d.scal[S_EPSTEPS * N + e];
-            else if (f == MISC_PREVZD) v = d.scal[S_PREVZD * N + e];
-            else if (f == MISC_SERIAL) v = d.scal[S_SERIAL * N + e];
-            else if (f == MISC_ODIRTY) v = d.scal[S_ODIRTY * N + e];
-            else if (f == MISC_NMOVED || f == MISC_NORD) v = 0;
-            else if (f < MISC_N + A) v = d.prev_life[(size_t)(f - MISC_N) * N + e];
-            else v = d.listed[(size_t)(f - MISC_N - A) * N + e];
-            MISC(c, f) = v;
-        }
+        for (int f = j + G; f < nmisc; f += G) MISC(c, f) = misc_load(d, f, e);
         // the rest of the static obstacle bitmap
         if (d.DW > 8 * G)
             stage_in(d.obstbits + 8 * G, d.DW - 8 * G, j, G, c.bm, [&](int w) { return IX(c, w + 8 * G); });
         // RNG window: the next words of this env's stream, tempered
         uint32_t off, slot, ready;
         int b0 = j;
+        wlen = window(st, off, slot, ready);
         if constexpr (EARLY) {
-            off = woff, slot = wslot, ready = wready;
+            // the window's first 4G words: issued now, into LDS only once the decisions are made (the first
+            // reader is the shuffle), so their round trip, which needs the stream state of round 1, runs
+            // under the decisions instead of lengthening the stage-in
+            const uint32_t* ringe = d.ring + (size_t)e * ZS_RING_WORDS;
 #pragma unroll
-            for (int u = 0; u < 4; u++)
-                if (j + u * G < wlen) c.rw[IX(c, j + u * G)] = mt_temper(wv[u]);
+            for (int u = 0; u < 4; u++) {
+                const uint32_t q = off + min(j + u * G, max(wlen - 1, 0));
+                wv[u] = q < ZS_MT_N ? ringe[slot * ZS_MT_N + q] : ringe[(slot ^ 1u) * ZS_MT_N + q - ZS_MT_N];
+            }
             b0 = j + 4 * G;
-        } else {
-            wlen = window(st, off, slot, ready);
         }
         const uint32_t* ring = d.ring + (size_t)e * ZS_RING_WORDS;
         for (int b = b0; b < wlen; b += 8 * G) {
@@ -1793,6 +1785,11 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
             nact += __popcll(gk);
         }
         if (j == 0) MISC(c, MISC_NMOVED) = special ? -1 : nact;
+        if constexpr (EARLY) {  // the window's first 4G words (issued at the stage-in)
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                if (j + u * G < wlen) c.rw[IX(c, j + u * G)] = mt_temper(wv[u]);
+        }
     }
     wave_sync();
     STAMP(2);
@@ -1888,19 +1885,7 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
             d.present[EIX(d, s, e)] = LPR(c, s);
             d.order[EIX(d, s, e)] = LO(c, s);
         }
-        for (int f = j; f < MISC_N + 2 * A; f += G) {
-            int v = MISC(c, f);
-            if (f == MISC_T) d.scal[S_T * N + e] = v;
-            else if (f == MISC_DEATHS) d.scal[S_DEATHS * N + e] = v;
-            else if (f == MISC_ZD) d.scal[S_ZD * N + e] = v;
-            else if (f == MISC_EPSTEPS) d.scal[S_EPSTEPS * N + e] = v;
-            else if (f == MISC_PREVZD) d.scal[S_PREVZD * N + e] = v;
-            else if (f == MISC_SERIAL) d.scal[S_SERIAL * N + e] = v;
-            else if (f == MISC_ODIRTY) d.scal[S_ODIRTY * N + e] = v;
-            else if (f == MISC_NMOVED || f == MISC_NORD) {
-            } else if (f < MISC_N + A) d.prev_life[(size_t)(f - MISC_N) * N + e] = v;
-            else d.listed[(size_t)(f - MISC_N - A) * N + e] = (uint8_t)v;
-        }
+        for (int f = j; f < MISC_N + 2 * A; f += G) misc_store(d, f, e, MISC(c, f));
     }
     wave_sync();
     STAMP(6);

@@ -8,7 +8,7 @@ cd "$(dirname "$0")/.." || exit 2
 TAG=${TAG:-r03}
 OUT=gpurun_out/round/$TAG
 mkdir -p "$OUT"
-args() { case $1 in n8) echo "--config c3 --envs 8192";; *) echo "--config $1";; esac; }
+args() { case $1 in n8) echo "--config c3 --envs 8192";; c5n8) echo "--config c5 --envs 8192";; *) echo "--config $1";; esac; }
 if [ -z "$NO_TESTS" ]; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1 \
       || { tail -30 "$OUT/pytest_gpu.log"; exit 1; }
