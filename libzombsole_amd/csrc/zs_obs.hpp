@@ -680,8 +680,14 @@ __host__ __device__ constexpr int obs_stage_slot_bytes(int tsize, int nblk = 1) 
 // of assuming the shortest path and draining most of the stores still in flight.
 #define ZS_OOB 0x80000000u
 
+// base is wave-uniform at every caller (one block per wave); read through readfirstlane so the descriptor
+// is built in SGPRs even where the compiler cannot prove that (k_obs_bring<int64, 4> wrapped each of its
+// writers' buffer stores in a readfirstlane waterfall loop without it)
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t zs_rsrc(void* base, uint32_t bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(base, (short)0, (int)bytes, 0x00020000);
+    const uint64_t b = (uint64_t)(uintptr_t)base;
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)b);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(b >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)(((uint64_t)hi << 32) | lo), (short)0, (int)bytes, 0x00020000);
 }
 template <typename T>
 __device__ __forceinline__ void zs_buf_store(__amdgpu_buffer_rsrc_t r, uint32_t off, T v) {
