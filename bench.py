@@ -67,6 +67,9 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-graph", action="store_true",
                    help="launch every step's kernels from the host instead of replaying the step as a hipGraph")
+    p.add_argument("--graph-steps", type=int, default=8,
+                   help="steps per graph launch at most (zs_step_graph_n; the largest count dividing --steps; "
+                        "--warmup rounded up to whole launches); 1 = one graph launch per step")
     p.add_argument("--cpu-steps", type=int, default=2000)
     p.add_argument("--launch", default="",
                    help="launch overrides for A/B runs, 'field=v,...' (zs_launch fields; 1 = on, -1 = off, n = size)")
@@ -270,11 +273,25 @@ def main():
 
     step = 0
     use_graph = not args.no_graph
+    # steps per graph launch: every step still runs its policy, tick and observation launches; only the
+    # graph launches are fewer (the outputs of a launch's earlier steps are overwritten, as they are by
+    # the next launch with one step per graph).  Not with the per-step exchange.
+    # the timed region covers exactly --steps steps: the largest count up to --graph-steps that divides it
+    # (warmup rounded up to whole launches, so the timed launches replay an already captured graph)
+    gsteps = 1
+    if use_graph and not gather:
+        gsteps = max(d for d in range(1, max(1, args.graph_steps) + 1) if args.steps % d == 0)
+    args.warmup = -(-args.warmup // gsteps) * gsteps
+    launch["graph_steps"] = gsteps
 
     def one_step():
         # the bench loop's step: the on-device policy's actions for step t, then zs_step; with graphs
         # both are one replayed hipGraph whose step counter advances on the device
         nonlocal step
+        if gsteps > 1:
+            eng.step_graph(step + 1, 7, steps=gsteps)
+            step += gsteps
+            return
         step += 1
         if gather:
             if use_graph:
@@ -288,7 +305,7 @@ def main():
             eng.gen_actions(step, 7)
             eng.step()
 
-    elapsed = timed_loop(one_step, args.steps, args.warmup, torch.cuda.synchronize, distributed,
+    elapsed = timed_loop(one_step, args.steps // gsteps, args.warmup // gsteps, torch.cuda.synchronize, distributed,
                          before_timing=None if use_graph else (lambda: eng.profile(True)))
     prof_steps = args.steps
     if use_graph:

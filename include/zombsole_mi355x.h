@@ -247,6 +247,12 @@ int zs_gen_actions(zs_handle* h, uint64_t step, int32_t n_discrete, int32_t* act
 int zs_step_graph(zs_handle* h, uint64_t step0, int32_t n_discrete, int32_t* actions_dev, void* obs_dev,
                   double* rewards_dev, uint8_t* done_dev, uint8_t* trunc_dev, uint8_t* listed_dev,
                   uint8_t* reset_dev, void* stream);
+/* n_steps consecutive steps of zs_step_graph in one graph launch (1 <= n_steps <= 64): each step is
+ * the same policy launch + zs_step on the same outputs, so the outputs hold the last step's results
+ * (a caller that reads every step's outputs takes n_steps = 1).  Saves the per-graph launch gap. */
+int zs_step_graph_n(zs_handle* h, uint64_t step0, int32_t n_discrete, int32_t n_steps, int32_t* actions_dev,
+                    void* obs_dev, double* rewards_dev, uint8_t* done_dev, uint8_t* trunc_dev,
+                    uint8_t* listed_dev, uint8_t* reset_dev, void* stream);
 
 /* Host view of one env's state as a flat int32 record (layout below). */
 int zs_state_size(const zs_handle* h, int32_t* n_words);

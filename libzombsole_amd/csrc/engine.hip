@@ -261,7 +261,7 @@ struct zs_handle {
     // a few buffer sets cached (a caller alternating double-buffered outputs, vector.StepGather)
     struct GraphSet {
         hipGraphExec_t g[2] = {nullptr, nullptr};  // per pending-list parity
-        const void* key[8] = {};
+        const void* key[9] = {};
         uint64_t used = 0;
     };
     static const int kGraphSets = 4;
@@ -1234,16 +1234,24 @@ extern "C" int zs_gen_actions(zs_handle* h, uint64_t step, int32_t n_discrete, i
 extern "C" int zs_step_graph(zs_handle* h, uint64_t step0, int32_t n_discrete, int32_t* actions_dev, void* obs_dev,
                              double* rewards_dev, uint8_t* done_dev, uint8_t* trunc_dev, uint8_t* listed_dev,
                              uint8_t* reset_dev, void* stream) {
+    return zs_step_graph_n(h, step0, n_discrete, 1, actions_dev, obs_dev, rewards_dev, done_dev, trunc_dev, listed_dev,
+                           reset_dev, stream);
+}
+
+extern "C" int zs_step_graph_n(zs_handle* h, uint64_t step0, int32_t n_discrete, int32_t n_steps, int32_t* actions_dev,
+                               void* obs_dev, double* rewards_dev, uint8_t* done_dev, uint8_t* trunc_dev,
+                               uint8_t* listed_dev, uint8_t* reset_dev, void* stream) {
     if (!h || !actions_dev || !rewards_dev || !done_dev || !trunc_dev) return fail(ZS_EINVAL, "null argument");
     if (n_discrete < 1 || n_discrete > 7) return fail(ZS_EINVAL, "n_discrete must be in 1..7");
+    if (n_steps < 1 || n_steps > 64) return fail(ZS_EINVAL, "n_steps must be in 1..64");
     hipStream_t s = (hipStream_t)stream;
     HIPCHK(hipSetDevice(h->device));
-    const void* key[8] = {actions_dev, obs_dev, rewards_dev, done_dev, trunc_dev, listed_dev, reset_dev,
-                          (const void*)(intptr_t)n_discrete};
+    const void* key[9] = {actions_dev, obs_dev, rewards_dev, done_dev, trunc_dev, listed_dev, reset_dev,
+                          (const void*)(intptr_t)n_discrete, (const void*)(intptr_t)n_steps};
     zs_handle::GraphSet* set = nullptr;
     for (auto& gs : h->gsets) {
         bool same = gs.g[0] && gs.g[1];
-        for (int k = 0; k < 8 && same; k++) same = key[k] == gs.key[k];
+        for (int k = 0; k < 9 && same; k++) same = key[k] == gs.key[k];
         if (same) set = &gs;
     }
     if (!set) {  // capture into the least recently used set
@@ -1268,16 +1276,18 @@ extern "C" int zs_step_graph(zs_handle* h, uint64_t step0, int32_t n_discrete, i
         h->prof = 0;  // no timing events inside a graph
         const int p0 = h->rpar;
         int rc = ZS_OK;
-        for (int g = 0; g < 2 && rc == ZS_OK; g++) {  // parity p0, then 1 - p0 (zs_step flips rpar)
+        for (int g = 0; g < 2 && rc == ZS_OK; g++) {  // starting parity p0, then 1 - p0 (zs_step flips rpar)
             hipGraph_t graph = nullptr;
+            h->rpar = (p0 + g) & 1;
             if (hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal) != hipSuccess) {
                 rc = fail(ZS_EHIP, "hipStreamBeginCapture failed");
                 break;
             }
-            // the step's policy reads the step number *d_gstep (zs_step: its own launch, or inside the
+            // each step's policy reads the step number *d_gstep (zs_step: its own launch, or inside the
             // step launch), the step's tail advances it
             h->graph_pol = n_discrete;
-            rc = zs_step(h, actions_dev, obs_dev, rewards_dev, done_dev, trunc_dev, listed_dev, reset_dev, cs);
+            for (int k = 0; k < n_steps && rc == ZS_OK; k++)
+                rc = zs_step(h, actions_dev, obs_dev, rewards_dev, done_dev, trunc_dev, listed_dev, reset_dev, cs);
             h->graph_pol = 0;
             hipError_t ce = hipStreamEndCapture(cs, &graph);
             if (rc == ZS_OK && ce != hipSuccess) rc = fail(ZS_EHIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(ce));
@@ -1298,12 +1308,12 @@ extern "C" int zs_step_graph(zs_handle* h, uint64_t step0, int32_t n_discrete, i
                 }
             return rc;
         }
-        for (int k = 0; k < 8; k++) set->key[k] = key[k];
+        for (int k = 0; k < 9; k++) set->key[k] = key[k];
     }
     set->used = ++h->gclock;
-    // g[p] drains list p (the parity of this step) and fills list 1 - p
+    // g[p] starts by draining list p (the parity of its first step); each step flips the parity
     HIPCHK(hipGraphLaunch(set->g[h->rpar], s));
-    h->rpar = 1 - h->rpar;
+    h->rpar ^= n_steps & 1;
     return ZS_OK;
 }
 

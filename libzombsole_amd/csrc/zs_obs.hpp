@@ -1438,11 +1438,13 @@ __global__ void __launch_bounds__(64 * (RING_ENC + RING_WRT), 1) k_obs_ring(Dev 
 // Unit slots: as many as fit beside the tables and the encoder images (us, at most 8 / PAIR; 4 for
 // city128's 42-KB int64 envs).
 // ---------------------------------------------------------------------------
+// measured at C4 on one MI355X (2 runs each, profiles/r04_ab_c4_*.log): 9 / 3 159.5-159.9 us, 8 / 4 164.5,
+// 8 / 3 170, 5 / 3 184-202, 12 / 3 (4 slots) 201
 #ifndef BRING_ENC
-#define BRING_ENC 8
+#define BRING_ENC 9
 #endif
 #ifndef BRING_WRT
-#define BRING_WRT 4
+#define BRING_WRT 3
 #endif
 #ifndef BRING_THR
 #define BRING_THR RING_THR
@@ -1605,9 +1607,10 @@ __global__ void __launch_bounds__(64 * (BRING_ENC + BRING_WRT), 1) k_obs_bring(D
                 const int sb = wm[cc];
                 const int v = icw[sb ? sb - 1 : 0], elife = ilife[sb ? sb - 1 : 0];
                 const zs_v4u sw = st4[c >> 5];
-                const bool isob = sw.x & bit;
+                const uint32_t isob = (sw.x & bit) ? 1u : 0u;
                 const int oi = isob ? (int)(sw.w + __popc(sw.x & (bit - 1u))) : 0;
-                const bool obp = isob && ((iopres[oi >> 5] >> (oi & 31)) & 1u);
+                // unconditional read (oi 0 off an obstacle): a read under the test became a branch per cell
+                const bool obp = (isob & (iopres[oi >> 5] >> (oi & 31))) & 1u;
                 int code = (idead[c >> 5] & bit) ? ZS_THING_DEADBODY : (sw.z & bit) ? ZS_THING_OBJECTIVE : ZS_THING_NONE;
                 code = obp ? ((sw.y & bit) ? ZS_THING_BOX : ZS_THING_WALL) : code;
                 code = sb ? (v & 255) : code;

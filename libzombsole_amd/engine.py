@@ -13,7 +13,7 @@ from . import _abi
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_build", "libzombsole_mi355x.so")
 SYMBOLS = ["zs_last_error", "zs_create", "zs_destroy", "zs_obs_shape", "zs_seed", "zs_reset", "zs_step", "zs_observe",
-           "zs_gen_actions", "zs_step_graph", "zs_state_size", "zs_get_state", "zs_set_state", "zs_get_rng", "zs_set_rng", "zs_overflow", "zs_profile", "zs_profile_read", "zs_describe",
+           "zs_gen_actions", "zs_step_graph", "zs_step_graph_n", "zs_state_size", "zs_get_state", "zs_set_state", "zs_get_rng", "zs_set_rng", "zs_overflow", "zs_profile", "zs_profile_read", "zs_describe",
            "zs_debug_stamps", "zs_debug_stamps_wg", "zs_debug_timeline", "zs_debug_lists", "zs_death_log"]
 
 _lib = None
@@ -49,6 +49,7 @@ def load_library(path=None):
     L.zs_observe.argtypes = [vp, vp, vp, vp]
     L.zs_gen_actions.argtypes = [vp, u64, i32, vp, vp]
     L.zs_step_graph.argtypes = [vp, u64, i32, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.zs_step_graph_n.argtypes = [vp, u64, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp]
     L.zs_state_size.argtypes = [vp, C.POINTER(i32)]
     L.zs_get_state.argtypes = [vp, i32, vp, vp]
     L.zs_set_state.argtypes = [vp, i32, vp, vp]
@@ -178,13 +179,19 @@ class Engine(object):
             _raise(self.L, rc, "zs_step")
         return o.obs[:self.N], o.rewards[:self.N], o.done[:self.N], o.trunc[:self.N]
 
-    def step_graph(self, step0, n_discrete, out=None):
+    def step_graph(self, step0, n_discrete, out=None, steps=1):
         """gen_actions(t, n_discrete) + step() as one replayed hipGraph (t = step0 on the first call,
-        then advancing by one per call on the device)."""
+        then advancing by one per step on the device).  steps > 1: that many steps per graph launch
+        (zs_step_graph_n), the outputs holding the last one's."""
         o = self.out if out is None else out
-        rc = self.L.zs_step_graph(self.h, int(step0), int(n_discrete), _ptr(self.actions), _ptr(o.obs),
-                                  _ptr(o.rewards), _ptr(o.done), _ptr(o.trunc), _ptr(o.listed),
-                                  _ptr(o.was_reset), self._stream())
+        if steps == 1:
+            rc = self.L.zs_step_graph(self.h, int(step0), int(n_discrete), _ptr(self.actions), _ptr(o.obs),
+                                      _ptr(o.rewards), _ptr(o.done), _ptr(o.trunc), _ptr(o.listed),
+                                      _ptr(o.was_reset), self._stream())
+        else:
+            rc = self.L.zs_step_graph_n(self.h, int(step0), int(n_discrete), int(steps), _ptr(self.actions),
+                                        _ptr(o.obs), _ptr(o.rewards), _ptr(o.done), _ptr(o.trunc), _ptr(o.listed),
+                                        _ptr(o.was_reset), self._stream())
         if rc:
             _raise(self.L, rc, "zs_step_graph")
         return o.obs[:self.N], o.rewards[:self.N], o.done[:self.N], o.trunc[:self.N]

@@ -67,7 +67,8 @@ def oracle_state(make_builder, seed, steps, nd, twice):
     return o.state()
 
 
-def run_full(make_builder, n, steps, nd=7, seed0=0, graph=True, twice=0, min_resets=1, launch=None, after=None):
+def run_full(make_builder, n, steps, nd=7, seed0=0, graph=True, twice=0, min_resets=1, launch=None, after=None,
+             graph_steps=1):
     import torch
 
     from libzombsole_amd.engine import Engine
@@ -85,7 +86,11 @@ def run_full(make_builder, n, steps, nd=7, seed0=0, graph=True, twice=0, min_res
     got[:, 0] = hs.obs_hash().cpu().numpy().view(np.uint64)
     resets = 0
     for t in range(1, steps + 1):
-        if graph:
+        if graph_steps > 1:  # zs_step_graph_n: the outputs of every graph_steps-th step are seen
+            if t % graph_steps:
+                continue
+            eng.step_graph(t - graph_steps + 1, nd, steps=graph_steps)
+        elif graph:
             eng.step_graph(t, nd)
         else:
             eng.gen_actions(t, nd)
@@ -93,6 +98,9 @@ def run_full(make_builder, n, steps, nd=7, seed0=0, graph=True, twice=0, min_res
         got[:, t] = hs.step_hash().cpu().numpy().view(np.uint64)
         resets += int(eng.was_reset.sum().item())
     exp = run_hashes(make_builder(1), seed0, n, steps, nd, threads=0, reset_twice_mod=twice)
+    if graph_steps > 1:
+        seen = [0] + list(range(graph_steps, steps + 1, graph_steps))
+        got, exp = got[:, seen], exp[:, seen]
     bad = np.argwhere(got != exp)
     assert bad.size == 0, "%d of %d env-steps differ; first (env, step): %s" % (
         len(bad), got.size, bad[:12].tolist())
@@ -209,6 +217,19 @@ def test_c3_8192_shard_graph():
         desc = eng.describe()
         assert desc["step_kernel"] == "k_step" and desc["par_exec"] == 1, desc
     run_full(c3, 8192, 60, seed0=6 * 8192, after=fused)
+
+
+def test_c3_8192_shard_multistep_graph():
+    """Eight steps per graph launch (zs_step_graph_n) at the shard size, TimeLimit 15 so that autoresets
+    fall inside a launch: the outputs of every eighth step and the final states against the oracle."""
+    r = run_full(lambda n: c3(n, max_steps=15), 8192, 48, seed0=4 * 8192, graph_steps=8, min_resets=1)
+    assert r >= 1
+
+
+def test_c2_4096_multistep_graph_odd():
+    """Three steps per graph launch: an odd count, so consecutive launches start on alternate pending-list
+    parities (two graphs per buffer set)."""
+    run_full(lambda n: c3(n, max_steps=10), 4096, 45, seed0=7 * 4096, graph_steps=3, min_resets=1)
 
 
 def test_c3_8192_shard_graph_obs_in_step():
