@@ -5,7 +5,7 @@
 # exchange's cost on the step at world size 1.
 cd "$(dirname "$0")/.." || exit 2
 mkdir -p gpurun_out
-timeout -k 10 180 python bench.py --config c5 --envs 8192 --steps ${STEPS:-200} --warmup 20 --no-cpu-baseline \
+timeout -k 10 180 python bench.py --config c5 --envs 8192 --steps ${STEPS:-200} --warmup 20 --no-cpu-baseline --graph-steps 1 \
     > gpurun_out/bench_c5n8.json 2> gpurun_out/bench_c5n8.err || { tail -5 gpurun_out/bench_c5n8.err; exit 1; }
 timeout -k 10 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
     --master-port ${PORT:-29533} bench.py --config c5 --envs 8192 --gather --steps ${STEPS:-200} --warmup 20 \
