@@ -547,7 +547,7 @@ __device__ __forceinline__ void obs_prefetch_env(const Dev& d, int e, zs_v2u dir
         f.dead[i] = (((dirty.y >> ((w * d.dead_chunk_m) >> 20)) & 1u) ? dr : d.dead_zero)[w];
     }
     // an obstacle is cleaned up only at life <= 0, so an env with no HP chunk dirty has every one
-    f.opres = (dirty.x ? d.obst_present + (size_t)ed * d.OW : d.opres_full)[min(lane, d.OW - 1)];
+    f.opres = (dirty.x ? d.obst_present + (size_t)ed * d.OW : d.opres_full)[min(lane, max(d.OW - 1, 0))];
     const int32_t* hr = d.obst_hp + (size_t)eh * d.O;
 #pragma unroll
     for (int i = 0; i < OBS_PF_H; i++) {
@@ -1082,7 +1082,7 @@ struct PatchEnc {
         }
         // obstacles away from the table's value: life off MAX_LIFE, or cleaned up.  The Box bits are read
         // back per env rather than held (a loop-invariant register set the compiler would spill).
-        const int ow = min(lane, d.OW - 1), nb = min(32, d.O - 32 * ow);
+        const int ow = min(lane, max(d.OW - 1, 0)), nb = min(32, d.O - 32 * ow);
         const uint32_t full = nb == 32 ? 0xffffffffu : ((1u << nb) - 1u);
         bool odd = lane < d.OW && f.opres != full;
         const uint32_t boxm = boxl[lane];
@@ -1439,12 +1439,13 @@ __global__ void __launch_bounds__(64 * (RING_ENC + RING_WRT), 1) k_obs_ring(Dev 
 // city128's 42-KB int64 envs).
 // ---------------------------------------------------------------------------
 // measured at C4 on one MI355X (2 runs each, profiles/r04_ab_c4_*.log): 9 / 3 159.5-159.9 us, 8 / 4 164.5,
-// 8 / 3 170, 5 / 3 184-202, 12 / 3 (4 slots) 201
+// 8 / 3 170, 5 / 3 184-202, 12 / 3 (4 slots) 201; with the 63-lane cell walk 9 / 3 158.3-159.7, 10 / 2
+// 153.6-155.0 (profiles/r04_ab_c4_enc.log)
 #ifndef BRING_ENC
-#define BRING_ENC 9
+#define BRING_ENC 10
 #endif
 #ifndef BRING_WRT
-#define BRING_WRT 3
+#define BRING_WRT 2
 #endif
 #ifndef BRING_THR
 #define BRING_THR RING_THR
@@ -1469,7 +1470,8 @@ __global__ void __launch_bounds__(64 * (BRING_ENC + BRING_WRT), 1) k_obs_bring(D
     if (blockIdx.x == 0 && threadIdx.x == 0) step_tail(d);  // a zs_step's tail (Dev::tail_*)
     extern __shared__ __align__(16) uint8_t smem[];
     typedef typename obs_stage<T>::type S;
-    constexpr int WW = 21, PLANE = WW * WW, PER = (PLANE + 63) / 64, TS = (int)sizeof(T);
+    constexpr int WW = 21, PLANE = WW * WW, PER = PLANE / 63, TS = (int)sizeof(T);
+    static_assert(PLANE % 63 == 0, "63 lanes x PER rows of three");
     constexpr int PAIR = ring_pair(TS, NOBS), SLOT = obs_stage_slot_bytes(TS, NOBS * PAIR), BLK = NOBS * 3 * PLANE;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     lv4u* st4 = (lv4u*)smem;
@@ -1504,6 +1506,8 @@ __global__ void __launch_bounds__(64 * (BRING_ENC + BRING_WRT), 1) k_obs_bring(D
     lu32* iopres = (lu32*)(img + L.off_opres);
     const int code_s = lane < d.A ? d.agent_codes[lane < d.A ? lane : 0] : (lane < d.A + d.P ? ZS_THING_PLAYER : ZS_THING_ZOMBIE);
     const int W = d.W, H = d.H, sl = lane < d.E ? lane : d.E - 1;
+    // a lane's window cells: lane + 63 i, row lr + 3 i, column lq (lane 63 repeats lane 0's next cell)
+    const int lr = lane / WW, lq = lane - lr * WW;
     auto item_env = [&](int t) { return unit_env(t / PAIR) + t % PAIR; };
     if (wave >= count) return;
     // Three load rounds per item, software-pipelined over two register sets: while item t is encoded,
@@ -1539,18 +1543,19 @@ __global__ void __launch_bounds__(64 * (BRING_ENC + BRING_WRT), 1) k_obs_bring(D
         }
         const uint32_t* orow = r.hd ? d.obst_present + (size_t)e * d.OW : d.opres_full;
 #pragma unroll
-        for (int i = 0; i < BRING_O; i++) q.ov[i] = orow[min(lane + 64 * i, d.OW - 1)];
+        for (int i = 0; i < BRING_O; i++) q.ov[i] = orow[min(lane + 64 * i, max(d.OW - 1, 0))];
         const int32_t* hrow = d.obst_hp + (size_t)e * d.O;
 #pragma unroll
         for (int a = 0; a < NOBS; a++) {
             const int32_t ap = __builtin_amdgcn_readlane(r.p, a);
             const int ox = unpack_x(ap) - WW / 2, oy = unpack_y(ap) - WW / 2;
+            const bool xin = (unsigned)(ox + lq) < (unsigned)W;
+            const int c0 = (oy + lr) * W + ox + lq;
 #pragma unroll
             for (int i = 0; i < PER; i++) {
-                const int cc = min(lane + 64 * i, PLANE - 1), rr = cc / WW, qq = cc - rr * WW;
-                const int x = ox + qq, y = oy + rr;
-                const bool inb = (unsigned)x < (unsigned)W && (unsigned)y < (unsigned)H;
-                const int c = inb ? y * W + x : 0;
+                const int y = oy + lr + 3 * i;
+                const bool inb = xin && (unsigned)y < (unsigned)H;
+                const int c = inb ? c0 + 3 * i * W : 0;
                 const uint32_t bit = 1u << (c & 31);
                 const zs_v4u sw = st4[c >> 5];
                 const int o = (sw.x & bit) ? (int)(sw.w + __popc(sw.x & (bit - 1u))) : 0;
@@ -1596,13 +1601,14 @@ __global__ void __launch_bounds__(64 * (BRING_ENC + BRING_WRT), 1) k_obs_bring(D
             const int ox = unpack_x(ap) - WW / 2, oy = unpack_y(ap) - WW / 2;
             const lu8* wm = img + a * PLANE;
             ZS_LDS S* ot = ot0 + a * 3 * PLANE;
+            const bool xin = (unsigned)(ox + lq) < (unsigned)W;
+            const int c0 = (oy + lr) * W + ox + lq;
 #pragma unroll
             for (int i = 0; i < PER; i++) {
-                const int cell = lane + 64 * i;
-                const int cc = cell < PLANE ? cell : PLANE - 1, rr = cc / WW, qq = cc - rr * WW;
-                const int x = ox + qq, y = oy + rr;
-                const bool inb = (unsigned)x < (unsigned)W && (unsigned)y < (unsigned)H;
-                const int c = inb ? y * W + x : 0;
+                const int cell = lane + 63 * i, cc = i < PER - 1 ? cell : min(cell, PLANE - 1);
+                const int y = oy + lr + 3 * i;
+                const bool inb = xin && (unsigned)y < (unsigned)H;
+                const int c = inb ? c0 + 3 * i * W : 0;
                 const uint32_t bit = 1u << (c & 31);
                 const int sb = wm[cc];
                 const int v = icw[sb ? sb - 1 : 0], elife = ilife[sb ? sb - 1 : 0];

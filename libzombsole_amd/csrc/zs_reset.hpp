@@ -263,7 +263,7 @@ __device__ __forceinline__ void reset_env_wave(const Dev& d, const ResetLds& L, 
 }
 
 // the reset work's LDS image (reset_lds_bytes), the static spawn lists staged when they fit
-__device__ __forceinline__ ResetLds reset_lds_carve(const Dev& d, uint8_t* smem) {
+__device__ __forceinline__ ResetLds reset_lds_carve(const Dev& d, uint8_t* smem, bool stage_lists = true) {
     ResetLds L;
     int o = 0;
     L.bm = (lu32*)(smem + o);
@@ -288,7 +288,7 @@ __device__ __forceinline__ ResetLds reset_lds_carve(const Dev& d, uint8_t* smem)
     o += (d.E + 8) * 4;
     o = ((o + 15) / 16) * 16;
     L.tw = (lu32*)(smem + o);
-    if (d.rlists_cap)
+    if (d.rlists_cap && stage_lists)
         for (int i = threadIdx.x; i < d.nps + d.nzs; i += 64) L.lists[i] = i < d.nps ? d.pspawn[i] : d.zspawn[i - d.nps];
     wave_sync();
     return L;
@@ -341,8 +341,43 @@ __global__ void __launch_bounds__(64, ZS_RESET_WAVES) k_reset(Dev d, int list_mo
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void respawn_env_wave(const Dev& d, const ResetLds& L, int e) {
     const int lane = threadIdx.x, N = d.N, E = d.E, Z0 = d.A + d.P;
-    for (int w = lane; w < d.DW; w += 64) L.bm[w] = d.obstbits[w];
-    for (int s = lane; s < E; s += 64) {
+    WaveRng r;
+    r.ring = d.ring + (size_t)e * ZS_RING_WORDS;
+    r.lr = L.tw;
+    // one round of loads for all the respawn reads: the env's ring (both slots) and stream state, its
+    // counters, entity rows and obstacle-present words, the zombie spawn list, the static bitmap
+    uint32_t rv[WR_STAGE_K];
+    wave_rng_fetch(r, rv);
+    const uint32_t st_in = d.rngst[e];
+    const int n0 = d.scal[S_NORDER * N + e], serial0 = d.scal[S_SERIAL * N + e];
+    const int sl = min(lane, E - 1);
+    const int32_t vp = d.pos[EIX(d, sl, e)], vl = d.life[EIX(d, sl, e)];
+    const uint8_t vw = d.weapon[EIX(d, sl, e)], vr = d.present[EIX(d, sl, e)], vo = d.order[EIX(d, sl, e)];
+    uint32_t opv[2];
+#pragma unroll
+    for (int u = 0; u < 2; u++)
+        if (64 * u < d.OW) opv[u] = d.obst_present[(size_t)e * d.OW + min(lane + 64 * u, d.OW - 1)];
+    int32_t zl[8];  // k_respawn stages only the zombie spawn list (reset_lds_carve's stage_lists false)
+    if (d.rlists_cap) {
+#pragma unroll
+        for (int u = 0; u < 8; u++)
+            if (64 * u < d.nzs) zl[u] = d.zspawn[min(lane + 64 * u, d.nzs - 1)];
+    }
+    stage_in(d.obstbits, d.DW, lane, 64, L.bm, [](int w) { return w; });
+    if (d.rlists_cap) {
+#pragma unroll
+        for (int u = 0; u < 8; u++)
+            if (64 * u < d.nzs && lane + 64 * u < d.nzs) L.lists[d.nps + lane + 64 * u] = zl[u];
+        for (int i = 512 + lane; i < d.nzs; i += 64) L.lists[d.nps + i] = d.zspawn[i];
+    }
+    if (lane < E) {
+        L.lpos[lane] = vp;
+        L.llife[lane] = vl;
+        L.lweap[lane] = vw;
+        L.lpres[lane] = vr;
+        L.lorder[lane] = vo;
+    }
+    for (int s = 64 + lane; s < E; s += 64) {
         L.lpos[s] = d.pos[EIX(d, s, e)];
         L.llife[s] = d.life[EIX(d, s, e)];
         L.lweap[s] = d.weapon[EIX(d, s, e)];
@@ -352,27 +387,27 @@ __device__ __forceinline__ void respawn_env_wave(const Dev& d, const ResetLds& L
     // occupancy (as k_tick rebuilds it): the map's obstacle cells minus the lost obstacles, then the
     // present things
     wave_sync();
-    for (int w = lane; w < d.OW; w += 64) {
+    auto lost = [&](int w, uint32_t pw) {
         const int nb = min(32, d.O - 32 * w);
-        uint32_t gone = ~d.obst_present[(size_t)e * d.OW + w] & (nb == 32 ? 0xffffffffu : ((1u << nb) - 1u));
+        uint32_t gone = ~pw & (nb == 32 ? 0xffffffffu : ((1u << nb) - 1u));
         while (gone) {
             const int32_t op = d.obst_xy[32 * w + __ffs(gone) - 1];
             gone &= gone - 1;
             const int cell = unpack_y(op) * d.W + unpack_x(op);
             __hip_atomic_fetch_and(&L.bm[cell >> 5], ~(1u << (cell & 31)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
-    }
+    };
+#pragma unroll
+    for (int u = 0; u < 2; u++)
+        if (lane + 64 * u < d.OW) lost(lane + 64 * u, opv[u]);
+    for (int w = 128 + lane; w < d.OW; w += 64) lost(w, d.obst_present[(size_t)e * d.OW + w]);
     wave_sync();
     for (int s = lane; s < E; s += 64)
         if (L.lpres[s]) {
             const int cell = unpack_y(L.lpos[s]) * d.W + unpack_x(L.lpos[s]);
             __hip_atomic_fetch_or(&L.bm[cell >> 5], 1u << (cell & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
-    WaveRng r;
-    r.ring = d.ring + (size_t)e * ZS_RING_WORDS;
-    r.lr = L.tw;
-    const uint32_t st_in = d.rngst[e];
-    wave_rng_stage(r);
+    wave_rng_put(r, rv);
     rng_block_load(r, st_in);
     // Game.spawn_zombies(count): the deficit's Zombie()s go into the free zombie slots, lowest first
     int nz = 0;
@@ -393,8 +428,7 @@ __device__ __forceinline__ void respawn_env_wave(const Dev& d, const ResetLds& L
         L.llife[s] = 50 + (int)v;
         L.lweap[s] = ZS_WEAPON_CLAWS;
     });
-    const int n0 = d.scal[S_NORDER * N + e];
-    int n_order = n0, serial = d.scal[S_SERIAL * N + e];
+    int n_order = n0, serial = serial0;
     const int placed = wave_spawn(d, L, r, e, k, 1, d.nzs, n_order, serial);
     const uint32_t stf = wave_rng_finish(r);
     for (int m = lane; m < k; m += 64) {  // the new zombies (dropped ones keep their drawn life)
@@ -414,12 +448,18 @@ __device__ __forceinline__ void respawn_env_wave(const Dev& d, const ResetLds& L
 }
 
 #ifdef ZS_DEFINE_RESET_KERNELS
-__global__ void __launch_bounds__(64, ZS_STEP_WAVES) k_respawn(Dev d) {
+// the merged load round needs the registers: at 6 waves per SIMD 244 B of spills, at 4 60 B; at 3 none
+// (C4, one box: respawn + gaps 31 us before the merge, 35 at 4 waves, 30 at 3; profiles/r04_ab_respawn.log)
+#ifndef ZS_RESPAWN_WAVES
+#define ZS_RESPAWN_WAVES 3
+#endif
+__global__ void __launch_bounds__(64, ZS_RESPAWN_WAVES) k_respawn(Dev d) {
     extern __shared__ __align__(16) uint8_t smem[];
-    const int n = min(*d.resp_count, d.N);
+    const int cnt = *d.resp_count, e0 = d.resp_list[blockIdx.x];  // one round trip (grid <= N)
+    const int n = min(cnt, d.N);
     if ((int)blockIdx.x >= n) return;
-    const ResetLds L = reset_lds_carve(d, smem);
-    for (int idx = blockIdx.x; idx < n; idx += gridDim.x) respawn_env_wave(d, L, d.resp_list[idx]);
+    const ResetLds L = reset_lds_carve(d, smem, false);  // the zombie list: with the env's loads
+    for (int idx = blockIdx.x; idx < n; idx += gridDim.x) respawn_env_wave(d, L, idx == (int)blockIdx.x ? e0 : d.resp_list[idx]);
 }
 
 // Drop the envs a mask-mode reset just rebuilt from the pending list (src -> dst, dst count

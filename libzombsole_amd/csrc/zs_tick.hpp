@@ -1487,7 +1487,7 @@ __device__ __forceinline__ void fobs_pipe(const Dev& d, const Grp& c, uint8_t* r
             const int w = min(lane + 64 * i, d.DW - 1);
             f.dead[i] = ld((((dd >> ((w * d.dead_chunk_m) >> 20)) & 1u) ? dr : d.dead_zero) + w);
         }
-        f.opres = ld((hd ? d.obst_present + (size_t)e * d.OW : d.opres_full) + min(lane, d.OW - 1));
+        f.opres = ld((hd ? d.obst_present + (size_t)e * d.OW : d.opres_full) + min(lane, max(d.OW - 1, 0)));
         const int32_t* hr = d.obst_hp + (size_t)e * d.O;
 #pragma unroll
         for (int i = 0; i < OBS_PF_H; i++) {
@@ -1531,6 +1531,19 @@ __device__ __forceinline__ void fobs_pipe(const Dev& d, const Grp& c, uint8_t* r
         else fobs_pipe_env(d, L, st4, img, (int16_t*)obs_out, e, nobs, lane);
         wave_sync();
         g2 = gn;
+    }
+}
+
+// word v into every env's copy of LDS row w (IX layout: row w of env g at w * NE + g), one store
+template <int NE>
+__device__ __forceinline__ void bcast_row(lu32* base, int w, uint32_t v) {
+    if constexpr (NE == 1) {
+        base[w] = v;
+    } else if constexpr (NE == 2) {
+        *(ZS_LDS zs_v2u*)(base + 2 * w) = zs_v2u{v, v};
+    } else {
+#pragma unroll
+        for (int k = 0; k < NE / 4; k++) *(lv4u*)(base + w * NE + 4 * k) = zs_v4u{v, v, v, v};
     }
 }
 
@@ -1629,12 +1642,14 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
             }
         }
         mval = misc_load(d, min(j, nmisc - 1), e);
-        // occupancy is rebuilt here, not kept in HBM: the map's obstacle cells (static, shared by every
-        // env, cache-resident), minus the obstacles this env has lost, plus its present things
-#pragma unroll
-        for (int u = 0; u < 8; u++) bmv[u] = d.obstbits[min(j + u * G, d.DW - 1)];
-        opw = d.obst_present[(size_t)e * d.OW + min(j, d.OW - 1)];
+        opw = d.obst_present[(size_t)e * d.OW + min(j, max(d.OW - 1, 0))];
     }
+    // occupancy is rebuilt here, not kept in HBM: the map's obstacle cells (static, shared by every env,
+    // cache-resident; loaded once per wave, each word stored to all NE envs' rows), minus the obstacles
+    // an env has lost, plus its present things
+#pragma unroll
+    for (int u = 0; u < 8; u++)
+        if (64 * u < d.DW) bmv[u] = d.obstbits[min(lane + 64 * u, d.DW - 1)];
     stepping = active && needs_reset == 0;
     if (active && d.pol_n) {
         // zs_step_graph: the policy's actions for this step (zs_gen_actions' stream), written out to the
@@ -1645,6 +1660,10 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
             if (stepping) LACT(c, k) = v;
         }
     }
+#pragma unroll
+    for (int u = 0; u < 8; u++)
+        if (64 * u < d.DW && lane + 64 * u < d.DW) bcast_row<NE>(c.bm, lane + 64 * u, bmv[u]);
+    for (int w = 512 + lane; w < d.DW; w += 64) bcast_row<NE>(c.bm, w, d.obstbits[w]);  // maps past 128 x 128
     if (stepping) {
 #pragma unroll
         for (int u = 0; u < 4; u++) {
@@ -1662,9 +1681,6 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
             if (j < 3 * A) LACT(c, j) = av;
             for (int k = j + G; k < 3 * A; k += G) LACT(c, k) = actions[(size_t)e * A * 3 + k];
         }
-#pragma unroll
-        for (int u = 0; u < 8; u++)
-            if (j + u * G < d.DW) c.bm[IX(c, j + u * G)] = bmv[u];
         SX(1);
         // the rest of the entity table (E > 4G) (SoA [slot][N]: this env's column)
         {
@@ -1697,9 +1713,6 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
         }
         // the rest of the per-env scalars and reward tracker / env.agents rows (more rows than lanes)
         for (int f = j + G; f < nmisc; f += G) MISC(c, f) = misc_load(d, f, e);
-        // the rest of the static obstacle bitmap
-        if (d.DW > 8 * G)
-            stage_in(d.obstbits + 8 * G, d.DW - 8 * G, j, G, c.bm, [&](int w) { return IX(c, w + 8 * G); });
         // RNG window: the next words of this env's stream, tempered
         uint32_t off, slot, ready;
         int b0 = j;
@@ -1736,8 +1749,7 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
         // dict-order ranks for closest() tie-breaks
         for (int k = j; k < n_order; k += G) LR(c, LO(c, k)) = (uint8_t)k;
         // the cells of obstacles this env has lost (cleaned up, core.py:121-138) are free
-        for (int w = j; w < d.OW; w += G) {
-            const uint32_t pw = w == j ? opw : d.obst_present[(size_t)e * d.OW + w];
+        auto lost = [&](int w, uint32_t pw) {
             const int nb = min(32, d.O - 32 * w);
             uint32_t gone = ~pw & (nb == 32 ? 0xffffffffu : ((1u << nb) - 1u));
             while (gone) {
@@ -1747,7 +1759,9 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
                 __hip_atomic_fetch_and(&c.bm[IX(c, cell >> 5)], ~(1u << (cell & 31)), __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_WORKGROUP);
             }
-        }
+        };
+        if (j < d.OW) lost(j, opw);
+        for (int w = j + G; w < d.OW; w += G) lost(w, d.obst_present[(size_t)e * d.OW + w]);
     }
     wave_sync();
     if (stepping) {  // the present things' cells (one may stand where a lost obstacle was)
