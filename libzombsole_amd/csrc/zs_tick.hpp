@@ -907,6 +907,16 @@ __device__ __forceinline__ void grp_execute(const Dev& d, Grp& c, int n, int& po
     for (int c0 = 0; c0 < n; c0 += G) {
         const int m = min(G, n - c0);
         const bool act = j < m;
+        // the scans below stop at the wave's longest chunk (entries past an env's m hold no move / no hit),
+        // rounded up to the 4-entry reads
+        int mw;
+        {
+            const unsigned long long am = __ballot(act);
+            unsigned long long comb = 0ull;
+#pragma unroll
+            for (int g = 0; g < 64 / G; g++) comb |= (am >> (g * G)) & gfull;
+            mw = min(G, (64 - __clzll((long long)comb) + 3) & ~3);
+        }
         int s = 0, kind = K_NONE, tgt = 0, p = 0, w = 0;
         if (act) {
             s = LPE(c, c0 + j);
@@ -945,7 +955,7 @@ __device__ __forceinline__ void grp_execute(const Dev& d, Grp& c, int n, int& po
         unsigned long long dep = 0ull, vac = 0ull;
         constexpr int UNR = G <= 16 ? G / 4 : 2;  // whole scans up to 16 lanes; wider groups by halves of 8
 #pragma unroll UNR
-        for (int k0 = 0; k0 < G; k0 += 4) {
+        for (int k0 = 0; k0 < mw; k0 += 4) {
             const zs_v4i dv = t0v[k0 >> 2], sv = t1v[k0 >> 2];
 #pragma unroll
             for (int u = 0; u < 4; u++) {
@@ -1012,7 +1022,7 @@ __device__ __forceinline__ void grp_execute(const Dev& d, Grp& c, int n, int& po
         bool last = inr;
         uint32_t ovf = 0u;  // an obstacle's life after one of the hits left the int16 / int32 range
 #pragma unroll UNR
-        for (int k0 = 0; k0 < G; k0 += 4) {
+        for (int k0 = 0; k0 < mw; k0 += 4) {
             const zs_v4i tv = t0v[k0 >> 2], hvv = t1v[k0 >> 2];
 #pragma unroll
             for (int u = 0; u < 4; u++) {
