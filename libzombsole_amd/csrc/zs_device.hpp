@@ -333,6 +333,49 @@ typedef ZS_LDS int32_t li32;
 typedef ZS_LDS uint16_t lu16;
 typedef ZS_LDS uint8_t lu8;
 
+// One wave twists the 624-word block src into nw (both LDS; _randommodule.c genrand_uint32), in the
+// three dependency phases of the in-place update (words [0, 227) from src alone, [227, 454) reading
+// phase 1's new words, [454, 624) phase 2's and nw[0]).  Each phase's reads are issued before its
+// stores (no read of a phase touches a word it writes): one LDS round trip per phase, not one per word
+// group.  The caller syncs the wave before (src complete) and after (nw complete).
+__device__ __forceinline__ void lds_twist(const ZS_LDS uint32_t* src, ZS_LDS uint32_t* nw, int lane) {
+    constexpr int N = ZS_MT_N, M = ZS_MT_M, P1 = N - M, P3 = N - 2 * P1, K1 = (P1 + 63) / 64, K3 = (P3 + 63) / 64;
+    static_assert(P3 > 0 && P3 <= P1, "MT19937 phase split");
+    uint32_t a[K1], b[K1], c[K1];
+#pragma unroll
+    for (int u = 0; u < K1; u++) {
+        const int k = min(lane + 64 * u, P1 - 1);
+        a[u] = src[k];
+        b[u] = src[k + 1];
+        c[u] = src[k + M];
+    }
+#pragma unroll
+    for (int u = 0; u < K1; u++)
+        if (lane + 64 * u < P1) nw[lane + 64 * u] = mt_f(a[u], b[u], c[u]);
+    wave_sync();
+#pragma unroll
+    for (int u = 0; u < K1; u++) {
+        const int k = P1 + min(lane + 64 * u, P1 - 1);
+        a[u] = src[k];
+        b[u] = src[k + 1];
+        c[u] = nw[k + M - N];
+    }
+#pragma unroll
+    for (int u = 0; u < K1; u++)
+        if (lane + 64 * u < P1) nw[P1 + lane + 64 * u] = mt_f(a[u], b[u], c[u]);
+    wave_sync();
+#pragma unroll
+    for (int u = 0; u < K3; u++) {
+        const int k = 2 * P1 + min(lane + 64 * u, P3 - 1);
+        a[u] = src[k];
+        b[u] = k + 1 < N ? src[k + 1] : nw[0];
+        c[u] = nw[k + M - N];
+    }
+#pragma unroll
+    for (int u = 0; u < K3; u++)
+        if (lane + 64 * u < P3) nw[2 * P1 + lane + 64 * u] = mt_f(a[u], b[u], c[u]);
+}
+
 // Stage n global words into LDS: lane `lane0` of a team of `step` lanes copies elements
 // lane0, lane0 + step, ...  All loads of a chunk of 8 are issued before any LDS store, so one
 // memory latency is paid per chunk instead of one per element.

@@ -46,21 +46,32 @@ __device__ __forceinline__ int wave_spawn(const Dev& d, const ResetLds& L, WaveR
     const int lane = threadIdx.x;
     const int total = nlist ? nlist : d.W * d.H;
     int n = 0;
-    for (int b = 0; b < total; b += 64) {
-        int i = b + lane;
-        int cell = -1;
-        if (i < total) {
-            if (nlist) {
-                int32_t p = d.rlists_cap ? L.lists[(which ? d.nps : 0) + i] : (which ? d.zspawn[i] : d.pspawn[i]);
-                cell = unpack_y(p) * d.W + unpack_x(p);
-            } else {
-                cell = (i % d.H) * d.W + i / d.H;  // x-major (core.py:45-47)
+    // 512 candidates per pass: every list and bitmap read of the pass before its compaction stores
+    for (int b0 = 0; b0 < total; b0 += 512) {
+        int cell[8];
+        bool fr[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int i = b0 + 64 * u + lane;
+            cell[u] = -1;
+            if (b0 + 64 * u < total && i < total) {  // the first test uniform: short lists skip whole rows
+                if (nlist) {
+                    int32_t p = d.rlists_cap ? L.lists[(which ? d.nps : 0) + i] : (which ? d.zspawn[i] : d.pspawn[i]);
+                    cell[u] = unpack_y(p) * d.W + unpack_x(p);
+                } else {
+                    cell[u] = (i % d.H) * d.W + i / d.H;  // x-major (core.py:45-47)
+                }
             }
         }
-        bool fr = cell >= 0 && !rbm_test(L, cell);
-        unsigned long long m = __ballot(fr);
-        if (fr) L.cand[n + __popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)cell;
-        n += __popcll(m);
+#pragma unroll
+        for (int u = 0; u < 8; u++) fr[u] = b0 + 64 * u < total && cell[u] >= 0 && !rbm_test(L, max(cell[u], 0));
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            if (b0 + 64 * u >= total) break;
+            const unsigned long long m = __ballot(fr[u]);
+            if (fr[u]) L.cand[n + __popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)cell[u];
+            n += __popcll(m);
+        }
     }
     wave_sync();
     // random.shuffle: for i = n-1 .. 1, j = _randbelow(i+1), swap.  Iterations i >= n-k decide the
@@ -341,6 +352,11 @@ __global__ void __launch_bounds__(64, ZS_RESET_WAVES) k_reset(Dev d, int list_mo
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void respawn_env_wave(const Dev& d, const ResetLds& L, int e) {
     const int lane = threadIdx.x, N = d.N, E = d.E, Z0 = d.A + d.P;
+    RST_DECL
+    RST(0);
+#ifdef ZS_STAMPS
+    if (lane == 0 && blockIdx.x < ZS_STAMP_WGS) g_stamp_wg[blockIdx.x * ZS_NPHASE + 19] += 1;  // respawns (slot 19)
+#endif
     WaveRng r;
     r.ring = d.ring + (size_t)e * ZS_RING_WORDS;
     r.lr = L.tw;
@@ -384,6 +400,7 @@ __device__ __forceinline__ void respawn_env_wave(const Dev& d, const ResetLds& L
         L.lpres[s] = d.present[EIX(d, s, e)];
         L.lorder[s] = d.order[EIX(d, s, e)];
     }
+    RST(1);
     // occupancy (as k_tick rebuilds it): the map's obstacle cells minus the lost obstacles, then the
     // present things
     wave_sync();
@@ -409,6 +426,7 @@ __device__ __forceinline__ void respawn_env_wave(const Dev& d, const ResetLds& L
         }
     wave_rng_put(r, rv);
     rng_block_load(r, st_in);
+    RST(2);
     // Game.spawn_zombies(count): the deficit's Zombie()s go into the free zombie slots, lowest first
     int nz = 0;
     for (int b = Z0; b < E; b += 64) nz += __popcll(__ballot(b + lane < E && L.lpres[b + lane]));
@@ -429,7 +447,9 @@ __device__ __forceinline__ void respawn_env_wave(const Dev& d, const ResetLds& L
         L.lweap[s] = ZS_WEAPON_CLAWS;
     });
     int n_order = n0, serial = serial0;
+    RST(3);
     const int placed = wave_spawn(d, L, r, e, k, 1, d.nzs, n_order, serial);
+    RST(4);
     const uint32_t stf = wave_rng_finish(r);
     for (int m = lane; m < k; m += 64) {  // the new zombies (dropped ones keep their drawn life)
         const int s = L.lslots[m];
@@ -445,6 +465,7 @@ __device__ __forceinline__ void respawn_env_wave(const Dev& d, const ResetLds& L
         d.rngst[e] = stf;
     }
     wave_sync();
+    RST(5);
 }
 
 #ifdef ZS_DEFINE_RESET_KERNELS

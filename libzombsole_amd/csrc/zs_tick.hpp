@@ -1391,13 +1391,7 @@ __device__ __forceinline__ void wave_refill(const Dev& d, int e, uint32_t st, lu
         if (lane + 64 * u < ZS_MT_N) tw[lane + 64 * u] = v[u];
     wave_sync();
     lu32* nw = tw + ZS_MT_N;
-    for (int k = lane; k < ZS_MT_N - ZS_MT_M; k += 64) nw[k] = mt_f(tw[k], tw[k + 1], tw[k + ZS_MT_M]);
-    wave_sync();
-    for (int k = (ZS_MT_N - ZS_MT_M) + lane; k < 2 * (ZS_MT_N - ZS_MT_M); k += 64)
-        nw[k] = mt_f(tw[k], tw[k + 1], nw[k + ZS_MT_M - ZS_MT_N]);
-    wave_sync();
-    for (int k = 2 * (ZS_MT_N - ZS_MT_M) + lane; k < ZS_MT_N; k += 64)
-        nw[k] = mt_f(tw[k], k + 1 < ZS_MT_N ? tw[k + 1] : nw[0], nw[k + ZS_MT_M - ZS_MT_N]);
+    lds_twist(tw, nw, lane);
     wave_sync();
     for (int k = lane; k < ZS_MT_N; k += 64) dst[k] = nw[k];
     if (lane == 0) d.rngst[e] = st | (1u << 11);

@@ -67,6 +67,11 @@ def main():
                 print("   %-10s per-reset %9.0f cyc" % (name, ssum[k] / max(1, nres)))
             else:
                 print("   %-10s mean %9.0f cyc   max %9d cyc" % (name, ssum[k] / (wgs * steps), smax[k]))
+        if ssum[19]:  # k_respawn (its phases share the R: slots; resets are few where respawns are many)
+            nr = float(ssum[19])
+            print("respawns per step: %.1f" % (nr / steps))
+            for i, name in enumerate(["loads+rows", "occupancy+rng", "lives draws", "spawn", "finish+out"]):
+                print("   P:%-14s per-respawn %9.0f cyc" % (name, ssum[13 + i] / nr))
         desc = eng.describe()
         if desc.get("step_kernel") == "k_step":
             # workgroup timeline of one more fused step launch (s_memrealtime, 10 ns)
