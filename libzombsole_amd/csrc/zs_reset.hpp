@@ -46,32 +46,21 @@ __device__ __forceinline__ int wave_spawn(const Dev& d, const ResetLds& L, WaveR
     const int lane = threadIdx.x;
     const int total = nlist ? nlist : d.W * d.H;
     int n = 0;
-    // 512 candidates per pass: every list and bitmap read of the pass before its compaction stores
-    for (int b0 = 0; b0 < total; b0 += 512) {
-        int cell[8];
-        bool fr[8];
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-            const int i = b0 + 64 * u + lane;
-            cell[u] = -1;
-            if (b0 + 64 * u < total && i < total) {  // the first test uniform: short lists skip whole rows
-                if (nlist) {
-                    int32_t p = d.rlists_cap ? L.lists[(which ? d.nps : 0) + i] : (which ? d.zspawn[i] : d.pspawn[i]);
-                    cell[u] = unpack_y(p) * d.W + unpack_x(p);
-                } else {
-                    cell[u] = (i % d.H) * d.W + i / d.H;  // x-major (core.py:45-47)
-                }
+    for (int b = 0; b < total; b += 64) {
+        int i = b + lane;
+        int cell = -1;
+        if (i < total) {
+            if (nlist) {
+                int32_t p = d.rlists_cap ? L.lists[(which ? d.nps : 0) + i] : (which ? d.zspawn[i] : d.pspawn[i]);
+                cell = unpack_y(p) * d.W + unpack_x(p);
+            } else {
+                cell = (i % d.H) * d.W + i / d.H;  // x-major (core.py:45-47)
             }
         }
-#pragma unroll
-        for (int u = 0; u < 8; u++) fr[u] = b0 + 64 * u < total && cell[u] >= 0 && !rbm_test(L, max(cell[u], 0));
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-            if (b0 + 64 * u >= total) break;
-            const unsigned long long m = __ballot(fr[u]);
-            if (fr[u]) L.cand[n + __popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)cell[u];
-            n += __popcll(m);
-        }
+        bool fr = cell >= 0 && !rbm_test(L, cell);
+        unsigned long long m = __ballot(fr);
+        if (fr) L.cand[n + __popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)cell;
+        n += __popcll(m);
     }
     wave_sync();
     // random.shuffle: for i = n-1 .. 1, j = _randbelow(i+1), swap.  Iterations i >= n-k decide the

@@ -50,7 +50,15 @@ __device__ __forceinline__ void wave_rng_stage(WaveRng& r) {
 // twist), cooperatively in three dependency phases
 __device__ __forceinline__ void wave_twist(WaveRng& r, uint32_t slot) {
     const int lane = threadIdx.x;
-    lds_twist(r.lr + slot * ZS_MT_N, r.lr + (slot ^ 1u) * ZS_MT_N, lane);
+    const lu32* src = r.lr + slot * ZS_MT_N;
+    lu32* nw = r.lr + (slot ^ 1u) * ZS_MT_N;
+    for (int k = lane; k < ZS_MT_N - ZS_MT_M; k += 64) nw[k] = mt_f(src[k], src[k + 1], src[k + ZS_MT_M]);
+    wave_sync();
+    for (int k = (ZS_MT_N - ZS_MT_M) + lane; k < 2 * (ZS_MT_N - ZS_MT_M); k += 64)
+        nw[k] = mt_f(src[k], src[k + 1], nw[k + ZS_MT_M - ZS_MT_N]);
+    wave_sync();
+    for (int k = 2 * (ZS_MT_N - ZS_MT_M) + lane; k < ZS_MT_N; k += 64)
+        nw[k] = mt_f(src[k], k + 1 < ZS_MT_N ? src[k + 1] : nw[0], nw[k + ZS_MT_M - ZS_MT_N]);
     wave_sync();
     r.dirty |= 1 << (slot ^ 1u);
 }
