@@ -163,7 +163,7 @@ def test_kernel_paths(path):
 # Zombie respawn in the tick's leader or deferred to k_respawn (wave per env): both bit-exact, on a
 # long candidate list (city128, 439 spawns), on every-cell candidates (city_for_safehouse) and on a
 # short list under Extermination, where a respawn decides whether the game ends (boxed: 1 zombie,
-# minimum 1).
+# minimum 1), and on a map without obstacles.
 RESPAWN = {
     "leader": {"defer_respawn": -1},
     "deferred": {"defer_respawn": 1},
@@ -186,6 +186,10 @@ def test_respawn_paths(path):
                24, 40, check_state_every=20, launch=lo)
     run_parity(lambda n: _abi.multi_env_config(n, "extermination", [], "city_for_safehouse", ["0", "1"],
                                                initial_zombies=3, minimum_zombies=2, max_episode_steps=40),
+               32, 60, stream="rich", check_state_every=20, launch=lo)
+    # a map without obstacles (easy_exit: no obstacle-present words to stage)
+    run_parity(lambda n: _abi.single_env_config(n, "evacuation", ["terminator"], "easy_exit", "0",
+                                                initial_zombies=8, minimum_zombies=6, max_episode_steps=60),
                32, 60, stream="rich", check_state_every=20, launch=lo)
 
 
