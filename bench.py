@@ -61,15 +61,28 @@ def parse():
     p.add_argument("--rules", default=None)
     p.add_argument("--gather", action="store_true", default=None,
                    help="all-gather the observation shards every step (C5's RCCL exchange)")
+    p.add_argument("--gather-self", action="store_true",
+                   help="(diagnostics) issue the exchange's collectives at world size 1 too (StepGather "
+                        "self_exchange; by default they are skipped there: the output sets are the whole buffers)")
     p.add_argument("--max-episode-steps", type=int, default=1000)
     p.add_argument("--obs-dtype", default=None, choices=["int64", "int32", "int16"])
     p.add_argument("--lanes-per-env", type=int, default=0, help="k_tick lanes per env (0 = engine default)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-graph", action="store_true",
                    help="launch every step's kernels from the host instead of replaying the step as a hipGraph")
-    p.add_argument("--graph-steps", type=int, default=8,
+    p.add_argument("--graph-steps", type=int, default=1,
                    help="steps per graph launch at most (zs_step_graph_n; the largest count dividing --steps; "
-                        "--warmup rounded up to whole launches); 1 = one graph launch per step")
+                        "--warmup rounded up to whole launches); 1 (default) = one graph launch per step, every "
+                        "step's outputs visible to the caller")
+    p.add_argument("--multi-steps", type=int, default=8,
+                   help="after the timed loop, time the same steps again with up to this many steps per graph "
+                        "launch and report them in the separate 'multi_step_graph' field (0 = skip); the "
+                        "intermediate steps' outputs are overwritten there, so it is not the headline value")
+    p.add_argument("--policy", default="device", choices=["device", "external"],
+                   help="device: the uniform Discrete(7) policy generated on device inside the step graph "
+                        "(SURVEY.md §8(d)); external: a caller-side policy, torch ops on the engine's stream "
+                        "that derive every step's actions from the previous step's observations, then the "
+                        "graphed step on those actions (zs_step_graph with n_discrete = 0; a learner's loop)")
     p.add_argument("--cpu-steps", type=int, default=2000)
     p.add_argument("--launch", default="",
                    help="launch overrides for A/B runs, 'field=v,...' (zs_launch fields; 1 = on, -1 = off, n = size)")
@@ -175,6 +188,27 @@ def cpu_baseline(args, builder_fn):
                           n_envs, steps, dt, rate1, steps1)}
 
 
+def external_policy(eng, n_discrete=7):
+    """A learner-side policy with a true per-step dependency: every agent's Discrete(n) id is taken from
+    its own window-centre cell of the previous step's observations (code + life + weapon channels) plus
+    the step number, by torch ops on the engine's stream, and written as triples into the engine's
+    action buffer, which the graphed step then reads (Engine.step_graphed).  Four small kernels."""
+    import torch
+    from libzombsole_amd.actions import DISCRETE_TRIPLES
+    assert eng.multi, "the external policy reads the multi-agent [N, A, 3, w, w] observations"
+    triples = torch.from_numpy(DISCRETE_TRIPLES[:n_discrete].copy()).to(eng.device)
+    N, (nobs, C, H, W) = eng.N, eng.obs_shape
+    centre = (H // 2) * W + W // 2
+    cells = eng.obs.view(N, nobs, C, H * W)[:, :, :, centre]  # [N, A, 3] strided view
+    dst = eng.actions.view(-1, 3)
+
+    def policy(t):
+        ids = cells.sum(-1, dtype=torch.int64)
+        ids.add_(t).remainder_(n_discrete)
+        torch.index_select(triples, 0, ids.view(-1), out=dst)
+    return policy
+
+
 def env_range(rank, world, total_envs, envs_per_gpu=0):
     """(envs on this rank, first global env, scaling, node-wide envs): a fixed count per rank (weak
     scaling) or the node's total split into contiguous ranges by vector.shard_range, the partition
@@ -269,7 +303,8 @@ def main():
         # C5: every step's observation shards + rewards / done / truncated, all-gathered over RCCL into
         # node-wide tensors (a centralised learner's input) on a second stream while the next step runs
         from libzombsole_amd.vector import StepGather
-        gather = StepGather(eng)
+        gather = StepGather(eng, self_exchange=args.gather_self)
+        launch["exchange"] = "skipped (world size 1)" if gather.skip else "RCCL all-gathers (in place)"
 
     step = 0
     use_graph = not args.no_graph
@@ -278,22 +313,35 @@ def main():
     # the next launch with one step per graph).  Not with the per-step exchange.
     # the timed region covers exactly --steps steps: the largest count up to --graph-steps that divides it
     # (warmup rounded up to whole launches, so the timed launches replay an already captured graph)
+    external = args.policy == "external"
+    policy = external_policy(eng) if external else None
     gsteps = 1
-    if use_graph and not gather:
+    if use_graph and not gather and not external:
         gsteps = max(d for d in range(1, max(1, args.graph_steps) + 1) if args.steps % d == 0)
     args.warmup = -(-args.warmup // gsteps) * gsteps
     launch["graph_steps"] = gsteps
+    launch["policy"] = "external: torch ops on the previous step's observations" if external else "on device"
 
-    def one_step():
+    def one_step(gs=None):
         # the bench loop's step: the on-device policy's actions for step t, then zs_step; with graphs
-        # both are one replayed hipGraph whose step counter advances on the device
+        # both are one replayed hipGraph whose step counter advances on the device.  external: the
+        # caller's policy writes the engine's action buffer from the last observations, then the step
         nonlocal step
-        if gsteps > 1:
-            eng.step_graph(step + 1, 7, steps=gsteps)
-            step += gsteps
+        gs = gsteps if gs is None else gs
+        if gs > 1:
+            eng.step_graph(step + 1, 7, steps=gs)
+            step += gs
             return
         step += 1
-        if gather:
+        if external:
+            policy(step)
+            if gather:
+                gather.step(lambda out: eng.step_graphed(out=out) if use_graph else eng.step(out=out))
+            elif use_graph:
+                eng.step_graphed()
+            else:
+                eng.step()
+        elif gather:
             if use_graph:
                 gather.step(lambda out: eng.step_graph(step, 7, out=out))
             else:
@@ -307,6 +355,19 @@ def main():
 
     elapsed = timed_loop(one_step, args.steps // gsteps, args.warmup // gsteps, torch.cuda.synchronize, distributed,
                          before_timing=None if use_graph else (lambda: eng.profile(True)))
+    # the same workload with several steps per graph launch (the launch gap paid once per launch; the
+    # outputs of a launch's earlier steps are overwritten): reported beside the headline, never as it
+    multi = None
+    if use_graph and not gather and not external and gsteps == 1 and args.multi_steps > 1:
+        ms = max(d for d in range(1, args.multi_steps + 1) if args.steps % d == 0)
+        if ms > 1:
+            el = timed_loop(lambda: one_step(ms), args.steps // ms, max(1, -(-args.warmup // ms)),
+                            torch.cuda.synchronize, distributed)
+            if distributed:
+                el = max_over_ranks(el, torch.device("cuda", local))
+            multi = {"graph_steps": ms, "value": total_envs * args.steps / el, "ms_per_step": el * 1e3 / args.steps,
+                     "note": "%d steps per graph launch: only every %d-th step's outputs are visible to the caller; "
+                             "not the headline" % (ms, ms)}
     prof_steps = args.steps
     if use_graph:
         # per-kernel HIP-event durations: the same steps launched one kernel at a time right after
@@ -391,13 +452,17 @@ def main():
         "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True,
         "scaling": scaling, "vs_baseline": None, "dtype": "int32", "data": "synthetic",
         "config": {"workload": "%s: %d parallel %dx%d '%s' envs over %d GPU(s) (%d per GPU), %s, %d agents + "
-                               "%d zombies (minimum %d), MultiagentZombsoleEnv rewards, uniform Discrete(7) policy "
-                               "on device, 21x21x3 %s obs per agent written to HBM every step%s, TimeLimit %d, "
-                               "next-step autoreset" % (
+                               "%d zombies (minimum %d), MultiagentZombsoleEnv rewards, %s, 21x21x3 %s obs per "
+                               "agent written to HBM every step%s, TimeLimit %d, next-step autoreset, one step per "
+                               "graph launch%s" % (
                                    args.config.upper(), total_envs, m.size[0], m.size[1], args.map, world, n_local,
-                                   args.rules, args.agents, args.zombies, args.min_zombies, args.obs_dtype,
+                                   args.rules, args.agents, args.zombies, args.min_zombies,
+                                   "a caller-side torch policy on the previous step's observations" if external
+                                   else "uniform Discrete(7) policy on device", args.obs_dtype,
                                    " and all-gathered over RCCL with rewards/done/truncated" if gather else "",
-                                   args.max_episode_steps),
+                                   args.max_episode_steps,
+                                   "" if gsteps == 1 else " (here %d: only every %d-th step's outputs visible)" % (
+                                       gsteps, gsteps)),
                    "preset": args.config, "envs_per_gpu": n_local, "total_envs": total_envs, "map": args.map,
                    "rules": args.rules, "agents": args.agents, "zombies": args.zombies,
                    "minimum_zombies": args.min_zombies, "obs_dtype": args.obs_dtype,
@@ -421,6 +486,8 @@ def main():
                      "issue": issue},
         "cpu_baseline": None,
     }
+    if multi:
+        out["multi_step_graph"] = multi
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args, builder)
     if rank == 0:

@@ -243,13 +243,19 @@ int zs_gen_actions(zs_handle* h, uint64_t step, int32_t n_discrete, int32_t* act
  * zs_step (same outputs), where t = step0 on the first call after a (re)capture and advances by
  * one per call on the device.  The launches are captured once per pending-reset-list parity for
  * each set of buffer arguments (the last 4 sets are kept, so double-buffered outputs replay
- * without recapture); results equal zs_gen_actions + zs_step. */
+ * without recapture); results equal zs_gen_actions + zs_step.
+ * n_discrete = 0: no policy.  The graph replays zs_step on the caller's actions_dev, which the
+ * caller fills on `stream` before each call (a learner's actions, derived from the previous step's
+ * observations); results equal zs_step.  This is the graphed form of the reference's per-tick
+ * MultiagentZombsoleEnv.step(actions) / ZombsoleGymEnv.step(action) (zombsole/gym/multiagent_env.py:111-171,
+ * zombsole/gym_env.py:99-145), one graph launch per step. */
 int zs_step_graph(zs_handle* h, uint64_t step0, int32_t n_discrete, int32_t* actions_dev, void* obs_dev,
                   double* rewards_dev, uint8_t* done_dev, uint8_t* trunc_dev, uint8_t* listed_dev,
                   uint8_t* reset_dev, void* stream);
 /* n_steps consecutive steps of zs_step_graph in one graph launch (1 <= n_steps <= 64): each step is
  * the same policy launch + zs_step on the same outputs, so the outputs hold the last step's results
- * (a caller that reads every step's outputs takes n_steps = 1).  Saves the per-graph launch gap. */
+ * (a caller that reads every step's outputs takes n_steps = 1).  Saves the per-graph launch gap.
+ * With n_discrete = 0 every step of the launch reads the same actions_dev. */
 int zs_step_graph_n(zs_handle* h, uint64_t step0, int32_t n_discrete, int32_t n_steps, int32_t* actions_dev,
                     void* obs_dev, double* rewards_dev, uint8_t* done_dev, uint8_t* trunc_dev,
                     uint8_t* listed_dev, uint8_t* reset_dev, void* stream);

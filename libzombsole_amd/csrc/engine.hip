@@ -1242,7 +1242,8 @@ extern "C" int zs_step_graph_n(zs_handle* h, uint64_t step0, int32_t n_discrete,
                                void* obs_dev, double* rewards_dev, uint8_t* done_dev, uint8_t* trunc_dev,
                                uint8_t* listed_dev, uint8_t* reset_dev, void* stream) {
     if (!h || !actions_dev || !rewards_dev || !done_dev || !trunc_dev) return fail(ZS_EINVAL, "null argument");
-    if (n_discrete < 1 || n_discrete > 7) return fail(ZS_EINVAL, "n_discrete must be in 1..7");
+    // n_discrete = 0: the caller's actions (no policy launch; the graph replays zs_step on actions_dev)
+    if (n_discrete < 0 || n_discrete > 7) return fail(ZS_EINVAL, "n_discrete must be in 0..7");
     if (n_steps < 1 || n_steps > 64) return fail(ZS_EINVAL, "n_steps must be in 1..64");
     hipStream_t s = (hipStream_t)stream;
     HIPCHK(hipSetDevice(h->device));

@@ -179,22 +179,32 @@ class Engine(object):
             _raise(self.L, rc, "zs_step")
         return o.obs[:self.N], o.rewards[:self.N], o.done[:self.N], o.trunc[:self.N]
 
-    def step_graph(self, step0, n_discrete, out=None, steps=1):
+    def step_graph(self, step0, n_discrete, out=None, steps=1, actions=None):
         """gen_actions(t, n_discrete) + step() as one replayed hipGraph (t = step0 on the first call,
         then advancing by one per step on the device).  steps > 1: that many steps per graph launch
-        (zs_step_graph_n), the outputs holding the last one's."""
+        (zs_step_graph_n), the outputs holding the last one's.  n_discrete = 0: no policy, the graph
+        replays step(actions) on the caller's action tensor (default self.actions), which the caller
+        fills on the current stream before each call (see step_graphed)."""
         o = self.out if out is None else out
+        a = self.actions if actions is None else actions
         if steps == 1:
-            rc = self.L.zs_step_graph(self.h, int(step0), int(n_discrete), _ptr(self.actions), _ptr(o.obs),
+            rc = self.L.zs_step_graph(self.h, int(step0), int(n_discrete), _ptr(a), _ptr(o.obs),
                                       _ptr(o.rewards), _ptr(o.done), _ptr(o.trunc), _ptr(o.listed),
                                       _ptr(o.was_reset), self._stream())
         else:
-            rc = self.L.zs_step_graph_n(self.h, int(step0), int(n_discrete), int(steps), _ptr(self.actions),
+            rc = self.L.zs_step_graph_n(self.h, int(step0), int(n_discrete), int(steps), _ptr(a),
                                         _ptr(o.obs), _ptr(o.rewards), _ptr(o.done), _ptr(o.trunc), _ptr(o.listed),
                                         _ptr(o.was_reset), self._stream())
         if rc:
             _raise(self.L, rc, "zs_step_graph")
         return o.obs[:self.N], o.rewards[:self.N], o.done[:self.N], o.trunc[:self.N]
+
+    def step_graphed(self, actions=None, out=None):
+        """step(actions) as one replayed hipGraph launch (zs_step_graph with n_discrete = 0): the
+        learner's per-step call (gym/multiagent_env.py:111-171) without the 3-5 host dispatches of an
+        eager zs_step.  The graph is keyed on the action and output buffers, so a caller keeps them
+        fixed (self.actions, an output set) and rewrites their contents each step."""
+        return self.step_graph(0, 0, out=out, actions=actions)
 
     def observe(self, mask=None):
         """Re-encode observations from the current state (after pokes)."""

@@ -134,8 +134,9 @@ class _EntityView(object):
     def __init__(self, game, slot):
         self._game = game
         self._slot = slot
-        self._serial = int(game._state().ent[slot][7])
-        self._last = None
+        r = game._state().ent[slot]
+        self._serial = int(r[7])
+        self._last = [int(v) for v in r]  # always holds a row of this thing (see _finalize)
         self._gone = False
 
     def _row(self):
@@ -147,7 +148,9 @@ class _EntityView(object):
         return self._last
 
     def _finalize(self, x, y, life):
-        """Removed from the world with these values (core.py:121-138)."""
+        """Removed from the world with these values (core.py:121-138).  The slot may already hold the
+        same step's respawned zombie (a new serial): the row kept from this thing's last read (every
+        poke refreshes it) supplies the fields the death log does not carry (kind, weapon)."""
         r = list(self._row())
         r[1], r[2], r[3], r[4] = 0, int(x), int(y), int(life)
         self._last = r
@@ -175,6 +178,7 @@ class _EntityView(object):
             return
         self._game._poke_entity(self._slot, int(value))
         self._last = None
+        self._row()  # re-read now, while the slot still holds this thing
 
     @property
     def weapon(self):

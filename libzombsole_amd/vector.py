@@ -76,13 +76,29 @@ class BatchedZombsole(object):
         """Discrete(6)/(7) ids [N, A] (gym_env.py:328-351, gym/multiagent_env.py:259-285) -> [N, A, 3]."""
         return self._triples[ids.long()]
 
-    def step(self, actions):
+    @property
+    def actions(self):
+        """The engine's action buffer, int32 [N, A, 3]: a caller that writes its actions here (e.g.
+        `torch.index_select(..., out=venv.actions.view(-1, 3))`) saves step()'s copy."""
+        return self.engine.actions
+
+    def step(self, actions, graph=True):
+        """One tick of every env on the caller's actions (int32 [N, A, 3] triples, or Discrete ids
+        [N, A]), as MultiagentZombsoleEnv.step / ZombsoleGymEnv.step do per env
+        (gym/multiagent_env.py:111-171, gym_env.py:99-145).  graph=True replays the step as one hipGraph
+        launch reading the engine's action buffer (Engine.step_graphed); graph=False dispatches its
+        kernels one by one (zs_step)."""
         t = self.torch
         if actions.dim() == 2:
             actions = self.discrete_to_triples(actions)
-        if actions.dtype != t.int32 or not actions.is_contiguous():
-            actions = actions.to(t.int32).contiguous()
-        return self.engine.step(actions)
+        if not graph:
+            if actions.dtype != t.int32 or not actions.is_contiguous():
+                actions = actions.to(t.int32).contiguous()
+            return self.engine.step(actions)
+        buf = self.engine.actions
+        if actions.data_ptr() != buf.data_ptr():
+            buf.copy_(actions)
+        return self.engine.step_graphed(buf)
 
     def sample_actions(self, step):
         """The bench/parity uniform policy, generated on device (zs_gen_actions)."""
@@ -168,7 +184,7 @@ class StepGather(object):
     passes after=fn to step(): fn(k) runs there right after the collectives that fill set k.
     """
 
-    def __init__(self, engine, group=None, depth=2):
+    def __init__(self, engine, group=None, depth=2, self_exchange=False):
         import torch
         import torch.distributed as dist
         self.torch = torch
@@ -193,6 +209,10 @@ class StepGather(object):
         cuda = dev.type == "cuda"
         self.comm = torch.cuda.Stream(device=dev) if cuda else None
         self.pending = [None] * self.depth  # per set: event after the collectives that read it
+        # world size 1: the output sets are the whole gather buffers, so the gathered tensors are already
+        # complete and the collectives are skipped (self_exchange=True issues them anyway: diagnostics of
+        # the exchange's fixed cost)
+        self.skip = self.world == 1 and not self_exchange
         self.t = 0
         self.last = None
 
@@ -206,7 +226,10 @@ class StepGather(object):
         if self.pending[k] is not None:
             torch.cuda.current_stream(self.eng.device).wait_event(self.pending[k])
         run(out)
-        if self.comm is not None:
+        if self.skip:
+            if after is not None:
+                after(k)
+        elif self.comm is not None:
             done = torch.cuda.Event()
             done.record(torch.cuda.current_stream(self.eng.device))
             self.comm.wait_event(done)

@@ -250,3 +250,29 @@ def test_c5_8192_int16_obs_in_step():
 def test_c3_8192_shard_serial_exec():
     """The same shard with the leader's serial execution (zs_launch.par_exec = -1)."""
     run_full(c3, 8192, 40, seed0=2 * 8192, launch={"par_exec": -1})
+
+
+def _side_reset(eng):
+    desc = eng.describe()
+    assert desc["step_kernel"] == "k_tick" and desc["reset_side_stream"] == 1, desc
+
+
+def test_c3_65536_multistep_graph_side_reset():
+    """Five steps per graph launch at the headline size (zs_step_graph_n), the reset work on the side
+    stream forked and joined inside every captured step; TimeLimit 16, so 65 536-env autoreset waves fall
+    inside launches.  Every fifth step's outputs and the final states against the oracle."""
+    r = run_full(lambda n: c3(n, max_steps=16), 65536, 40, graph_steps=5, min_resets=1, after=_side_reset)
+    assert r >= 1
+
+
+def test_c5_65536_multistep_graph_side_reset():
+    """Eight steps per graph launch at C5's size (int16, side-stream reset), TimeLimit 12."""
+    run_full(lambda n: c5(n, max_steps=12), 65536, 32, graph_steps=8, min_resets=1, after=_side_reset)
+
+
+def test_c4_16384_multistep_graph_respawn():
+    """Eight steps per graph launch at C4 (side-stream reset, k_respawn after every tick)."""
+    def check(eng):
+        _side_reset(eng)
+        assert eng.describe()["respawn"] == "k_respawn"
+    run_full(c4, 16384, 48, graph_steps=8, min_resets=1, after=check)

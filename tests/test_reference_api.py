@@ -229,3 +229,24 @@ def test_two_envs_share_the_global_stream():
     r1, s1 = run()
     r2, s2 = run()
     assert r1 == r2 and s1 == s2
+
+
+# ---- drop-in views ---------------------------------------------------------------------
+def test_zombie_view_after_life_poke_and_slot_reuse():
+    """A zombie whose life is poked to 0 (the view's cached row is refreshed by the poke) is removed by
+    the next step's cleanup while the same step's respawn (minimum_zombies) refills its slot with a new
+    zombie: the view keeps the removed zombie's final values (core.py:121-138, game.py:196-201)."""
+    random.seed(77)
+    env = MultiagentZombsoleEnv("extermination", [], "bridge", ["0"], initial_zombies=10, minimum_zombies=10)
+    env.reset()
+    zs = sorted((t for t in env.game.world.things.values() if isinstance(t, Zombie)), key=lambda z: z._slot)
+    z = zs[0]
+    serial = z._serial
+    z.life = 0
+    assert z.life == 0
+    env.step({"0": {"action_type": "heal", "parameter": [0, 0]}})
+    st = env.game._state()
+    assert int(st.ent[z._slot][7]) != serial, "the slot was not reused by the respawn"
+    assert z.life <= 0 and not z.alive_in_world
+    assert all(t is not z for t in env.game.world.things.values())
+    assert isinstance(z.position, tuple) and z.weapon is not None

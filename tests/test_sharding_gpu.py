@@ -63,7 +63,11 @@ def _free_port():
     return p
 
 
-def test_rccl_world1_gather():
+@pytest.mark.parametrize("self_exchange", [True, False])
+def test_rccl_world1_gather(self_exchange):
+    """World size 1: with self_exchange the in-place RCCL all-gathers run (the exchange's code path at one
+    rank); without, StepGather skips them (its output sets are the whole buffers) and the results are
+    the same."""
     import torch
     import torch.distributed as dist
 
@@ -78,7 +82,8 @@ def test_rccl_world1_gather():
         eng = Engine(_c5(2048))
         eng.seed(list(range(2048)))
         eng.reset()
-        g = StepGather(eng)
+        g = StepGather(eng, self_exchange=self_exchange)
+        assert g.skip == (not self_exchange)
         ref = Engine(_c5(2048))  # the same envs stepped without the exchange, default outputs
         ref.seed(list(range(2048)))
         ref.reset()
@@ -100,7 +105,8 @@ def test_rccl_world1_gather():
         dist.destroy_process_group()
 
 
-def test_rccl_world1_gather_in_flight():
+@pytest.mark.parametrize("self_exchange", [True, False])
+def test_rccl_world1_gather_in_flight(self_exchange):
     """C5's exchange with steps in flight: 8 gathered steps issued back to back with no host sync and no
     wait on the caller's stream, so step t + 1 computes while step t's collectives run, and a set is
     written again only after the collectives of two steps earlier.  A consumer on the communication stream
@@ -121,7 +127,7 @@ def test_rccl_world1_gather_in_flight():
         eng = Engine(_c5(n))
         eng.seed(list(range(n)))
         eng.reset()
-        g = StepGather(eng)
+        g = StepGather(eng, self_exchange=self_exchange)
         hashes = torch.zeros((steps, 2), dtype=torch.int64, device=dev)
         wts = torch.arange(1, g.g_obs[0].numel() + 1, dtype=torch.int64, device=dev) % 1000003
 
