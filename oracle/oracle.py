@@ -55,6 +55,11 @@ def load(path):
     L.zo_run_hashes.restype = C.c_int64
     L.zo_run_hashes.argtypes = [C.c_void_p, C.c_uint64, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                                 C.c_void_p]
+    L.zo_run_hashes_census.restype = C.c_int64
+    L.zo_run_hashes_census.argtypes = [C.c_void_p, C.c_uint64, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+                                       C.c_void_p, C.c_int32, C.c_void_p]
+    L.zo_set_census.argtypes = [C.c_void_p, C.c_int]
+    L.zo_census.argtypes = [C.c_void_p, C.c_void_p]
     return L
 
 
@@ -151,6 +156,15 @@ class OracleEnv(object):
     def poke_dead(self, x, y):
         return self.L.zo_poke_dead(self.h, x, y)
 
+    def set_census(self, chunk_g):
+        """Count the conflict cases of the engine's chunked execution with G = chunk_g (0 = off)."""
+        self.L.zo_set_census(self.h, int(chunk_g))
+
+    def census(self):
+        out = np.zeros(len(CENSUS), dtype=np.int64)
+        self.L.zo_census(self.h, out.ctypes.data)
+        return dict(zip(CENSUS, (int(v) for v in out)))
+
     def poke_obstacle_gone(self, i):
         return self.L.zo_poke_obstacle_gone(self.h, i)
 
@@ -171,10 +185,22 @@ def hash_weights(idx):
 HASH_R, HASH_D = 1 << 20, 1 << 21  # weight offsets of rewards / done, truncated, autoreset (zs_oracle.c)
 
 
-def run_hashes(builder, seed0, n_envs, steps, n_discrete, threads=0, reset_twice_mod=0):
+# conflict census of the engine's chunked execution (zs_oracle.h ZO_CF_*), in index order
+CENSUS = ("enter_vacated", "same_dest", "target_moved", "target_later", "multi_hit", "hit_dead", "heal_clamp",
+          "obst_int16", "lists", "lists_serial", "chunks", "max_in_chunk", "chunks_all6")
+CENSUS_CASES = CENSUS[:8]
+
+
+def run_hashes(builder, seed0, n_envs, steps, n_discrete, threads=0, reset_twice_mod=0, chunk_g=0):
     """Per env and step output hashes of the bench workload: uint64 [n_envs, steps + 1]
-    (column 0 = the reset observation), see zo_run_hashes."""
+    (column 0 = the reset observation), see zo_run_hashes.  chunk_g > 0: also the conflict census of
+    every env summed (a dict, CENSUS), returned as (hashes, census)."""
     out = np.zeros((n_envs, steps + 1), dtype=np.uint64)
-    lib().zo_run_hashes(C.cast(builder.ptr(), C.c_void_p), seed0, n_envs, steps, n_discrete, threads,
-                        reset_twice_mod, out.ctypes.data)
-    return out
+    if chunk_g <= 0:
+        lib().zo_run_hashes(C.cast(builder.ptr(), C.c_void_p), seed0, n_envs, steps, n_discrete, threads,
+                            reset_twice_mod, out.ctypes.data)
+        return out
+    cen = np.zeros(len(CENSUS), dtype=np.int64)
+    lib().zo_run_hashes_census(C.cast(builder.ptr(), C.c_void_p), seed0, n_envs, steps, n_discrete, threads,
+                               reset_twice_mod, out.ctypes.data, int(chunk_g), cen.ctypes.data)
+    return out, dict(zip(CENSUS, (int(v) for v in cen)))
