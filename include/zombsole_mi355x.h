@@ -167,7 +167,9 @@ typedef struct zs_launch {
     int32_t obs_wgs;         /* observation workgroups per CU (store-stream kernels)                   */
     int32_t par_exec;        /* -1: the leader lane executes the shuffled actions serially instead of
                               * the env's lanes in parallel (core.py:103-119)                          */
-    int32_t reserved[10];
+    int32_t fstep;           /* the step as one launch (k_fstep): tick, observation encoder and writer
+                              * waves in every workgroup, the tick overlapping the observation stream  */
+    int32_t reserved[9];
 } zs_launch;
 
 typedef struct zs_config {

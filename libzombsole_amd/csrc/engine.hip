@@ -286,6 +286,10 @@ struct zs_handle {
     int rpar = 0;
     size_t reset_lds = 0;
     int fused = 0;  // zs_step runs reset work and the tick in one launch (k_step)
+    int fstep = 0;  // zs_step is one k_fstep launch (tick, encoder and writer waves per workgroup, zs_fstep.hpp)
+    FsLayout fs_l;
+    int fs_grid = 0;
+    int* d_fsctr = nullptr;  // k_fstep's finished-workgroup counter (zero between launches)
     int resident = 0;  // step-launch workgroups resident per CU (layout choice)
     int want = 0;      // workgroups per CU the launch has (capped at 32)
     // diagnostics: HIP events bracketing every k_tick / k_obs launch on its stream
@@ -878,6 +882,36 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
         delete h;
         return fail(ZS_EHIP, "cannot raise k_reset's dynamic LDS limit");
     }
+    // k_fstep (zs_fstep.hpp): the multi-round step (reset work on the side stream, k_tick, the padded-table
+    // k_obs_ring) as one launch, one workgroup per CU, its tick waves overlapping its observation stream.
+    // It needs the ring's shape (channels, padded-table encoders), respawns in the tick (no k_respawn),
+    // an instance for (G, dtype, observations per env), and its tables, encoder regions, >= 2 ring slots
+    // and FS_TICK tick / reset images in 160 KB.  zs_launch.fstep forces either.
+    if (h->ov.fstep > 0 && !h->fused && !d.defer_respawn && !d.fobs && h->obs_ring == 2 &&
+        d.obs_enc == ZS_ENC_CHANNELS) {
+        const int nobs = obs_count(d.obs_scope, d.reward_mode, d.A);
+        const int ts = d.obs_dtype == ZS_DTYPE_I64 ? 8 : d.obs_dtype == ZS_DTYPE_I32 ? 4 : 2;
+        const int pair = ring_pair(ts, nobs);
+        int cus = 256;
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+        const int nunits = (d.N + 64 / h->G - 1) / (64 / h->G);
+        const int grid = std::max(1, std::min(cus, nunits));
+        const int upw = (nunits + grid - 1) / grid;
+        const int tick_b = (int)std::max(h->lds, h->reset_lds);
+        FsLayout L;
+        int us = 8 / pair;
+        for (; us >= 2; us--) {
+            L = fs_layout(patch_static_bytes(d.opad_n, d.O), patch_enc_bytes(d.DW, d.O),
+                          obs_stage_slot_bytes(ts, nobs * pair), us, tick_b);
+            if (L.bytes <= 160 * 1024) break;
+        }
+        if (us >= 2 && upw <= FS_MAX_UNITS && fstep_attr(h->G, d.obs_dtype, nobs, L.bytes) == hipSuccess) {
+            TRY(dalloc(h, &h->d_fsctr, 1));
+            h->fstep = 1;
+            h->fs_l = L;
+            h->fs_grid = grid;
+        }
+    }
     if (getenv("ZS_VERBOSE"))
         fprintf(stderr, "zs_create: N=%d E=%d G=%d step_lds=%zu resident=%d reset_lds=%zu rw_cap=%d cand_cap=%d "
                         "lists_cap=%d fused=%d fobs=%d obs_img=%d k_obs_img=%d x%d pipe=%d gather=%d pipe_wgs=%d reset_side=%d defer_respawn=%d\n",
@@ -1126,11 +1160,54 @@ extern "C" int zs_observe(zs_handle* h, const uint8_t* env_mask_dev, void* obs_d
     return launch_obs(h, obs_dev, env_mask_dev, s);
 }
 
+// zs_step as one k_fstep launch (zs_fstep.hpp): the envs pending a reset (S_NEEDRESET, i.e. list[p]) are
+// rebuilt by the tick waves that find them, the ticks append this step's ended envs to list[q], and the
+// launch's last workgroup empties list[p] and advances the policy's step counter (the step's tail).  The
+// policy of zs_step_graph runs inside the tick, as in the fused step launch.
+static int step_fstep(zs_handle* h, const int32_t* actions_dev, void* obs_dev, double* rewards_dev, uint8_t* done_dev,
+                      uint8_t* trunc_dev, uint8_t* listed_dev, uint8_t* reset_dev, hipStream_t s) {
+    Dev& d = h->d;
+    const int p = h->rpar, q = 1 - p;
+    d.pol_n = h->graph_pol;
+    d.pol_step = h->graph_pol ? h->d_gstep : nullptr;
+    d.tail_cnt0 = h->d_rcount + p;
+    d.tail_cnt1 = nullptr;
+    d.tail_step = h->graph_pol ? h->d_gstep : nullptr;
+    FsArgs a;
+    a.actions = actions_dev;
+    a.rew = rewards_dev;
+    a.done = done_dev;
+    a.trunc = trunc_dev;
+    a.listed = listed_dev;
+    a.reset_out = reset_dev;
+    a.rlist = h->d_rlist[q];
+    a.rcount = h->d_rcount + q;
+    a.err = h->d_err;
+    a.obs = obs_dev;
+    a.done_ctr = h->d_fsctr;
+    a.L = h->fs_l;
+    int i0 = -1, i1 = -1;
+    if (h->prof) HIPCHK(hipEventRecord(prof_event(h, &i0), s));
+    const hipError_t le = launch_fstep(h->G, d.obs_dtype, obs_count(d.obs_scope, d.reward_mode, d.A),
+                                       (unsigned)h->fs_grid, s, d, a);
+    d.pol_n = 0, d.pol_step = nullptr;
+    d.tail_cnt0 = d.tail_cnt1 = nullptr, d.tail_step = nullptr;
+    if (le != hipSuccess) return fail(ZS_EHIP, std::string("k_fstep: ") + hipGetErrorString(le));
+    if (h->prof) {
+        HIPCHK(hipEventRecord(prof_event(h, &i1), s));
+        h->ev_tick.push_back({i0, i1});
+    }
+    h->rpar = q;
+    return ZS_OK;
+}
+
 extern "C" int zs_step(zs_handle* h, const int32_t* actions_dev, void* obs_dev, double* rewards_dev, uint8_t* done_dev,
                        uint8_t* trunc_dev, uint8_t* listed_dev, uint8_t* reset_dev, void* stream) {
     if (!h || !actions_dev || !rewards_dev || !done_dev || !trunc_dev) return fail(ZS_EINVAL, "null argument");
     hipStream_t s = (hipStream_t)stream;
     HIPCHK(hipSetDevice(h->device));
+    if (h->fstep && obs_dev) return step_fstep(h, actions_dev, obs_dev, rewards_dev, done_dev, trunc_dev, listed_dev,
+                                               reset_dev, s);
     // 1) rebuild the envs that ended at the previous call (list[p]); fused into the tick launch
     //    when the LDS images allow, else a k_reset launch first
     int q = 1 - h->rpar, rc = ZS_OK;
@@ -1466,14 +1543,15 @@ extern "C" int zs_profile_read(zs_handle* h, double* out) {
 extern "C" int zs_describe(zs_handle* h, char* buf, int32_t len) {
     if (!h || !buf || len <= 0) return fail(ZS_EINVAL, "null argument");
     const Dev& d = h->d;
-    const char* obs_kernel = d.fobs ? "step launch"
+    const char* obs_kernel = h->fstep ? "k_fstep" : d.fobs ? "step launch"
                              : h->obs_pipe ? (h->obs_ring ? "k_obs_ring" : h->obs_patch ? "k_obs_patch" : h->obs_lds ? "k_obs_lds" : "k_obs_pipe")
                              : h->obs_bring ? "k_obs_bring" : h->obs_gather ? "k_obs_gather" : "k_obs";
     snprintf(buf, (size_t)len,
              "{\"envs\": %d, \"entities\": %d, \"lanes_per_env\": %d, \"step_kernel\": \"%s\", \"step_lds\": %zu, "
              "\"step_wgs_per_cu\": %d, \"rng_window\": %d, \"obs_kernel\": \"%s\", \"reset_side_stream\": %d, "
              "\"reset_lds\": %zu, \"respawn\": \"%s\", \"tick_waves\": %d, \"rng_step\": %d, \"par_exec\": %d}",
-             d.N, d.E, h->G, h->fused ? "k_step" : "k_tick", h->lds, h->resident, d.rw_cap, obs_kernel, h->reset_side,
+             d.N, d.E, h->G, h->fstep ? "k_fstep" : h->fused ? "k_step" : "k_tick", h->lds, h->resident, d.rw_cap, obs_kernel,
+             h->fstep ? 0 : h->reset_side,
              h->reset_lds, d.defer_respawn ? "k_respawn" : "tick", h->fused ? ZS_FUSED_WAVES : h->tick_waves, d.rw_step,
              d.par_exec);
     return ZS_OK;

@@ -18,12 +18,13 @@ __global__ void __launch_bounds__(64, ZS_FUSED_WAVES) k_step(Dev d, int n_reset,
                                              uint8_t* done_out, uint8_t* trunc_out, uint8_t* listed_out,
                                              uint8_t* reset_out, int* reset_list, int* reset_count,
                                              const int* cur_list, const int* cur_count, int* err_out, void* obs_out) {
+    extern __shared__ __align__(16) uint8_t smem[];
     TL(0);
     if ((int)blockIdx.x < n_reset)
         reset_role(d, 1, cur_list, cur_count, nullptr, err_out, blockIdx.x, n_reset, d.fobs ? obs_out : nullptr);
     else
         tick_wg<G, true>(d, xcd_remap(blockIdx.x - n_reset, gridDim.x - n_reset), actions, rew, done_out, trunc_out,
-                   listed_out, reset_out, reset_list, reset_count, obs_out, 0, d.N);
+                   listed_out, reset_out, reset_list, reset_count, obs_out, 0, d.N, (lu8*)smem);
     TL(1);
 }
 

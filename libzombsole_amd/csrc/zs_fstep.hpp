@@ -1,0 +1,152 @@
+// zs_fstep.hpp — k_fstep: one step (reset work, tick and observations) as one persistent launch whose
+// workgroups overlap the tick with the observation stream inside the step.
+//
+// The unfused step runs k_tick (issue / latency bound: C3 86 us), then k_obs_ring (HBM-write bound:
+// C3 266 us) back to back, so the step costs their sum.  Envs are independent, so the observations of
+// env block b can stream while block b + 1 ticks.  One workgroup per CU owns a contiguous range of the
+// step's tick units (64 / G envs each) and splits its waves into three roles:
+//   * FS_TICK tick waves take the range's units from an LDS counter and run the tick on each
+//     (tick_wg, zs_tick.hpp: decisions, shuffle, execution, cleanup, rewards, rules for the stepping
+//     envs; gym/multiagent_env.py:111-171 with core.py:72-78), then rebuild the unit's envs that ended
+//     at the previous step (reset_env_wave, zs_reset.hpp; game.py:151-169: the next-step autoreset the
+//     unfused step leaves to k_reset on its side stream), and publish the unit as ready in LDS;
+//   * FS_ENC encoder waves walk the range's envs in order, wait for each env's unit, load the env's new
+//     state from L2 (device-scope loads, which bypass the CU's L1: lines loaded before the tick wrote
+//     them may be there) and encode its agents' 21 x 21 x 3 windows into a ring slot with the
+//     padded-table encoder (PatchEnc, zs_obs.hpp; gym/observation.py:57-173);
+//   * FS_WRT writer waves stream the ring's slots out as 16-B stores (obs_stage_flush), as k_obs_ring's do.
+// No wave waits on a wave of another workgroup, and inside the workgroup the waits only point from
+// encoders to tick waves (a unit is published once ticked) and to writers (a slot is free once written
+// out), writers to encoders (a slot is written out once filled), all in rising order: every wave reaches
+// its end.  The last workgroup to finish does the step's tail (Dev::tail_*): the pending list this step
+// drained by flag (S_NEEDRESET) is emptied and the policy's step counter advanced.
+#pragma once
+#include "zs_obs.hpp"
+#include "zs_reset.hpp"
+#include "zs_tick.hpp"
+#include "zs_launch.hpp"
+
+// device-scope (L2) loads of words this launch's tick waves wrote
+template <typename V>
+__device__ __forceinline__ V ld_l2(const V* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// obs_prefetch_env's loads (zs_obs.hpp) from L2: the env's dirty masks first (they select its own rows
+// or the shared clean rows), then the entity slots, dead-body words, present words and obstacle HP
+__device__ __forceinline__ void fs_prefetch_env(const Dev& d, int e, ObsPrefetch& f) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t hd = ld_l2(d.hp_dirty + e), dd = ld_l2(d.dead_dirty + e);
+    const int s = lane < d.E ? lane : d.E - 1;
+    f.pos = ld_l2(d.pos + EIX(d, s, e));
+    f.life = ld_l2(d.life + EIX(d, s, e));
+    f.wp = ld_l2(d.weapon + EIX(d, s, e));
+    f.pr = ld_l2(d.present + EIX(d, s, e));
+    const uint32_t* dr = d.dead + (size_t)e * d.DW;
+#pragma unroll
+    for (int i = 0; i < OBS_PF_D; i++) {
+        const int w = min(lane + 64 * i, d.DW - 1);
+        f.dead[i] = ld_l2((((dd >> ((w * d.dead_chunk_m) >> 20)) & 1u) ? dr : d.dead_zero) + w);
+    }
+    f.opres = ld_l2((hd ? d.obst_present + (size_t)e * d.OW : d.opres_full) + min(lane, max(d.OW - 1, 0)));
+    const int32_t* hr = d.obst_hp + (size_t)e * d.O;
+#pragma unroll
+    for (int i = 0; i < OBS_PF_H; i++) {
+        const int o = min(lane + 64 * i, d.O - 1);
+        f.hp[i] = ld_l2((((hd >> ((o * d.hp_chunk_m) >> 20)) & 1u) ? hr : d.hp_init) + o);
+    }
+}
+
+template <int G, typename T, int NOBS>
+__global__ void __launch_bounds__(64 * FS_WAVES, 1) k_fstep(Dev d, FsArgs a) {
+    extern __shared__ __align__(16) uint8_t smem[];
+    typedef typename obs_stage<T>::type S;
+    constexpr int NE = 64 / G, WW = 21, PLANE = WW * WW, TS = (int)sizeof(T);
+    constexpr int PAIR = ring_pair(TS, NOBS), BLK = NOBS * 3 * PLANE;
+    const FsLayout& FL = a.L;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    // this workgroup's tick units [u0, u1) and envs [e_lo, e_hi)
+    const int nunits = (d.N + NE - 1) / NE;
+    const int upw = (nunits + (int)gridDim.x - 1) / (int)gridDim.x;
+    const int u0 = min((int)blockIdx.x * upw, nunits), u1 = min(u0 + upw, nunits), nu = u1 - u0;
+    const int e_lo = u0 * NE, n_env = max(0, min(u1 * NE, d.N) - e_lo);
+    ZS_LDS int* state = (ZS_LDS int*)(smem + FL.off_state);  // ring protocol word per slot and env of a unit
+    ZS_LDS int* ready = (ZS_LDS int*)(smem + FL.off_ready);  // 1 once tick unit u0 + k is ticked and reset
+    ZS_LDS int* ctr = (ZS_LDS int*)(smem + FL.off_ctr);      // next tick unit to take
+    for (int i = threadIdx.x; i < 16 + FS_MAX_UNITS + 4; i += blockDim.x) state[i] = 0;  // the three arrays are adjacent
+    patch_stage_static(d, smem);  // barriers: the zeroed words and the tables before any role starts
+    const int US = FL.us;
+    lu8* slots = (lu8*)(smem + FL.off_slots);
+    if (wave < FS_TICK) {
+        // ---- tick role ----
+        lu8* reg = (lu8*)(smem + FL.off_tick + wave * FL.tick_bytes);
+        for (;;) {
+            int k = 0;
+            if (lane == 0) k = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            k = __builtin_amdgcn_readfirstlane(__shfl(k, 0));
+            if (k >= nu) break;
+            unsigned long long pend = 0ull;
+            tick_wg<G>(d, u0 + k, a.actions, a.rew, a.done, a.trunc, a.listed, a.reset_out, a.rlist, a.rcount, nullptr,
+                       0, d.N, reg, &pend);
+            wave_sync();
+            if (pend) {  // the unit's envs that ended at the previous step: World rebuilt (game.py:151-169)
+                const ResetLds Lr = reset_lds_carve(d, (uint8_t*)reg);
+                while (pend) {
+                    const int g = (__ffsll((long long)pend) - 1) / G;
+                    pend &= ~(1ull << (g * G));
+                    reset_env_wave(d, Lr, (u0 + k) * NE + g, 1, a.err);
+                }
+            }
+            // the unit's stores completed (in L2) before its flag: a workgroup release waits for them
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (lane == 0) ring_state_store(&ready[k], 1);
+            wave_sync();
+        }
+    } else if (wave < FS_TICK + FS_ENC) {
+        // ---- encoder role: envs e_lo + w, + FS_ENC, ... ----
+        const int w = wave - FS_TICK;
+        lu8* wb = (lu8*)(smem + FL.off_enc + w * FL.enc_bytes);
+        PatchEnc<S> pe(d, smem, wb, lane);
+        T* out = (T*)a.obs;
+        for (int t = w; t < n_env; t += FS_ENC) {
+            const int e = e_lo + t;
+            ring_wait(&ready[t / NE], 1);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            ObsPrefetch f;
+            fs_prefetch_env(d, e, f);
+            pe.build(d, f);
+            const int u = t / PAIR, h = t % PAIR, q = u % US;
+            if (u >= US) ring_wait(&state[PAIR * q + h], 2 * (u - US) + 2);
+            wave_sync();
+            ZS_LDS S* ot0 = (ZS_LDS S*)(slots + q * FL.slot_bytes) + (int)((uintptr_t)(out + (size_t)(e - h) * BLK) & 15) / TS +
+                            h * BLK;
+#pragma unroll
+            for (int ag = 0; ag < NOBS; ag++) pe.block(d, ot0 + ag * 3 * PLANE, ag);
+            ring_state_store(&state[PAIR * q + h], 2 * u + 1);
+        }
+    } else {
+        // ---- writer role: ring units w, w + FS_WRT, ... (PAIR envs each) ----
+        T* out = (T*)a.obs;
+        const int nru = (n_env + PAIR - 1) / PAIR;
+        for (int u = wave - FS_TICK - FS_ENC; u < nru; u += FS_WRT) {
+            const int q = u % US, e = e_lo + PAIR * u;
+            const bool whole = PAIR * u + PAIR <= n_env;
+            for (int h = 0; h < PAIR; h++)
+                if (PAIR * u + h < n_env) ring_wait(&state[PAIR * q + h], 2 * u + 1);
+            if (whole) obs_stage_flush<T, NOBS * PAIR, RING_THR>(slots + q * FL.slot_bytes, out + (size_t)e * BLK, lane);
+            else obs_stage_flush<T, NOBS, RING_THR>(slots + q * FL.slot_bytes, out + (size_t)e * BLK, lane);
+            for (int h = 0; h < PAIR; h++) ring_state_store(&state[PAIR * q + h], 2 * u + 2);
+        }
+    }
+    // the step's tail, by the last workgroup to get here (every tick of the launch has read the policy's
+    // step counter by then)
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        const int k = atomicAdd(a.done_ctr, 1);
+        if (k == (int)gridDim.x - 1) {
+            step_tail(d);
+            *a.done_ctr = 0;
+        }
+    }
+}

@@ -41,6 +41,71 @@ ZS_TICK_DECL(32)
 ZS_TICK_DECL(64)
 #undef ZS_TICK_DECL
 
+// k_fstep (zs_fstep.hpp): the step as one launch with tick, encoder and writer waves per workgroup
+#ifndef FS_TICK
+#define FS_TICK 4
+#endif
+#ifndef FS_ENC
+#define FS_ENC 8
+#endif
+#ifndef FS_WRT
+#define FS_WRT 3
+#endif
+#define FS_WAVES (FS_TICK + FS_ENC + FS_WRT)
+#define FS_MAX_UNITS 512  // tick units per workgroup (ready flags in LDS)
+
+// LDS of a k_fstep workgroup: the padded-table encoder's static tables, FS_ENC encoder regions, `us` ring
+// slots, FS_TICK tick regions (each the tick's image of one unit, or the reset image of one env), then the
+// ring protocol words, the units' ready flags and the unit counter.
+struct FsLayout {
+    int off_enc, enc_bytes;
+    int off_slots, slot_bytes, us;
+    int off_tick, tick_bytes;
+    int off_state, off_ready, off_ctr;
+    int bytes;
+};
+
+__host__ __device__ inline FsLayout fs_layout(int stat_bytes, int enc_bytes, int slot_bytes, int us, int tick_bytes) {
+    FsLayout L;
+    int o = ((stat_bytes + 15) / 16) * 16;
+    L.off_enc = o;
+    L.enc_bytes = ((enc_bytes + 15) / 16) * 16;
+    o += FS_ENC * L.enc_bytes;
+    L.off_slots = o;
+    L.slot_bytes = ((slot_bytes + 15) / 16) * 16;
+    L.us = us;
+    o += us * L.slot_bytes;
+    L.off_tick = o;
+    L.tick_bytes = ((tick_bytes + 15) / 16) * 16;
+    o += FS_TICK * L.tick_bytes;
+    L.off_state = o;
+    o += 16 * 4;
+    L.off_ready = o;
+    o += FS_MAX_UNITS * 4;
+    L.off_ctr = o;
+    o += 16;
+    L.bytes = o;
+    return L;
+}
+
+struct FsArgs {
+    const int32_t* actions;
+    double* rew;
+    uint8_t* done;
+    uint8_t* trunc;
+    uint8_t* listed;
+    uint8_t* reset_out;
+    int* rlist;        // the pending-reset list this step appends to (the next step's resets)
+    int* rcount;
+    int* err;
+    void* obs;
+    int* done_ctr;     // workgroups finished (the last one does the step's tail, then zeroes it)
+    FsLayout L;
+};
+
+hipError_t launch_fstep(int G, int dtype, int nobs, unsigned grid, hipStream_t s, const Dev& d, const FsArgs& a);
+hipError_t fstep_attr(int G, int dtype, int nobs, int bytes);  // hipErrorNotSupported: no such instance
+
 // observation kernels
 enum { OBSK_OBS = 0, OBSK_GATHER, OBSK_PIPE, OBSK_LDS, OBSK_PATCH, OBSK_RING, OBSK_BRING };
 struct ObsLaunch {

@@ -43,7 +43,7 @@ __device__ __forceinline__ bool rbm_test(const ResetLds& L, int cell) { return (
 // remaining iterations only consume their draws.  Returns the number of things placed.
 __device__ __forceinline__ int wave_spawn(const Dev& d, const ResetLds& L, WaveRng& r, int e, int k, int which,
                                           int nlist, int& n_order, int& serial) {
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & 63;
     const int total = nlist ? nlist : d.W * d.H;
     int n = 0;
     for (int b = 0; b < total; b += 64) {
@@ -102,7 +102,7 @@ __device__ __forceinline__ uint32_t wave_rng_finish(WaveRng& r) {
 }
 
 __device__ __forceinline__ void reset_env_wave(const Dev& d, const ResetLds& L, int e, int list_mode, int* err_out) {
-    const int lane = threadIdx.x, N = d.N, E = d.E, A = d.A, P = d.P;
+    const int lane = threadIdx.x & 63, N = d.N, E = d.E, A = d.A, P = d.P;
     RST_DECL
     RST(0);
     const uint32_t st_in = d.rngst[e];
@@ -289,7 +289,7 @@ __device__ __forceinline__ ResetLds reset_lds_carve(const Dev& d, uint8_t* smem,
     o = ((o + 15) / 16) * 16;
     L.tw = (lu32*)(smem + o);
     if (d.rlists_cap && stage_lists)
-        for (int i = threadIdx.x; i < d.nps + d.nzs; i += 64) L.lists[i] = i < d.nps ? d.pspawn[i] : d.zspawn[i - d.nps];
+        for (int i = threadIdx.x & 63; i < d.nps + d.nzs; i += 64) L.lists[i] = i < d.nps ? d.pspawn[i] : d.zspawn[i - d.nps];
     wave_sync();
     return L;
 }
@@ -311,7 +311,7 @@ __device__ __forceinline__ void reset_role(const Dev& d, int list_mode, const in
             wave_sync();
             lu8* img = (lu8*)L.tw;
             lu32* st = d.obs_stat ? (lu32*)((lu8*)L.tw + d.obsl.bytes) : nullptr;
-            if (st) obs_stage_static(d, st, threadIdx.x, 64);
+            if (st) obs_stage_static(d, st, threadIdx.x & 63, 64);
             obs_build(d, d.obsl, img, e, [&](int s, int& p, int& lf, int& wp, int& pr) {
                 p = L.lpos[s];
                 lf = L.llife[s];
@@ -340,7 +340,7 @@ __global__ void __launch_bounds__(64, ZS_RESET_WAVES) k_reset(Dev d, int list_mo
 // (core.py:40-66) as wave work (wave_spawn), new zombies appended to the dict order.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void respawn_env_wave(const Dev& d, const ResetLds& L, int e) {
-    const int lane = threadIdx.x, N = d.N, E = d.E, Z0 = d.A + d.P;
+    const int lane = threadIdx.x & 63, N = d.N, E = d.E, Z0 = d.A + d.P;
     RST_DECL
     RST(0);
 #ifdef ZS_STAMPS

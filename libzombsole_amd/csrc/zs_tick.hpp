@@ -1401,7 +1401,7 @@ __device__ __forceinline__ void wave_refill(const Dev& d, int e, uint32_t st, lu
 __device__ __forceinline__ void coop_refill(const Dev& d, int base, int count, const lu32* lst, lu32* tw) {
     for (int i = 0; i < count; i++) {
         const uint32_t st = lst[i];
-        if (!((st >> 11) & 1u)) wave_refill(d, base + i, st, tw, threadIdx.x);
+        if (!((st >> 11) & 1u)) wave_refill(d, base + i, st, tw, threadIdx.x & 63);
     }
 }
 
@@ -1467,7 +1467,7 @@ template <int NE>
 __device__ __forceinline__ void fobs_pipe(const Dev& d, const Grp& c, uint8_t* region, unsigned long long stepmask,
                                           int G, int base, void* obs_out) {
     constexpr int WW = 21, PLANE = WW * WW;
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & 63;
     const ObsLayout& L = d.obsl;
     lv4u* st4 = (lv4u*)region;
     lu8* img = (lu8*)(region + 16 * d.DW);
@@ -1558,13 +1558,15 @@ __device__ __forceinline__ void bcast_row(lu32* base, int w, uint32_t v) {
 // EARLY (the one-round fused launch, whose register budget has room): the RNG window's first 4G words
 // are loaded in registers right after the first load round and reach LDS only after the decisions, so
 // their round trip (it needs the stream state) overlaps the decisions instead of the stage-in
+// smem: this wave's LDS image (tick_layout); pend (optional): the ballot of the envs this call found
+// pending a reset (bit g * G for env base + g), which the caller's reset work rebuilds (k_fstep)
 template <int G, bool EARLY = false>
 __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* actions, double* rew, uint8_t* done_out,
                                         uint8_t* trunc_out, uint8_t* listed_out, uint8_t* reset_out, int* reset_list,
-                                        int* reset_count, void* obs_out, int env0, int env1) {
-    extern __shared__ __align__(16) uint8_t smem[];
+                                        int* reset_count, void* obs_out, int env0, int env1, lu8* smem,
+                                        unsigned long long* pend = nullptr) {
     constexpr int NE = 64 / G;
-    const int lane = threadIdx.x, g = lane / G, j = lane - g * G;
+    const int lane = threadIdx.x & 63, g = lane / G, j = lane - g * G;
     const int base = env0 + wg * NE, e = base + g, N = d.N, E = d.E, A = d.A;
     const bool active = e < env1;
     const bool leader = j == 0;
@@ -1811,6 +1813,7 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
     }
     wave_sync();
     STAMP(2);
+    if (pend) *pend = __ballot(active && leader && !stepping);
     if (active && leader && !stepping) {  // this call is the env's reset; outputs as after env.reset()
         int nr = d.reward_mode == ZS_REWARD_SINGLE ? 1 : A;
         for (int a = 0; a < nr; a++) rew[(size_t)e * nr + a] = 0.0;
@@ -1910,7 +1913,7 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
     // observations of the envs ticked here (envs reset by this call get theirs from the reset work):
     // the whole wave encodes one env at a time, its image aliasing the dead tick region
     if (d.fobs && obs_out && d.fobs_pipe) {
-        fobs_pipe<NE>(d, c, smem + L.off_region, __ballot(stepping && leader), G, base, obs_out);
+        fobs_pipe<NE>(d, c, (uint8_t*)(smem + L.off_region), __ballot(stepping && leader), G, base, obs_out);
     } else if (d.fobs && obs_out) {
         const unsigned long long stepmask = __ballot(stepping && leader);  // bit g * G per stepping env
         lu8* img = (lu8*)(smem + L.off_region);
@@ -1935,6 +1938,7 @@ template <int G, int W = ZS_STEP_WAVES>
 __global__ void __launch_bounds__(64, W) k_tick(Dev d, const int32_t* actions, double* rew, uint8_t* done_out,
                                              uint8_t* trunc_out, uint8_t* listed_out, uint8_t* reset_out,
                                              int* reset_list, int* reset_count, void* obs_out, int env0, int env1) {
+    extern __shared__ __align__(16) uint8_t smem[];
     tick_wg<G>(d, xcd_remap(blockIdx.x, gridDim.x), actions, rew, done_out, trunc_out, listed_out, reset_out, reset_list,
-               reset_count, obs_out, env0, env1);
+               reset_count, obs_out, env0, env1, (lu8*)smem);
 }

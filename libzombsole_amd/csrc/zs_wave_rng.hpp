@@ -28,12 +28,12 @@ struct WaveRng {
 // its other loads in between, and the round trips overlap.
 #define WR_STAGE_K ((2 * ZS_MT_N + 63) / 64)
 __device__ __forceinline__ void wave_rng_fetch(const WaveRng& r, uint32_t (&v)[WR_STAGE_K]) {
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & 63;
 #pragma unroll
     for (int u = 0; u < WR_STAGE_K; u++) v[u] = r.ring[min(lane + 64 * u, 2 * ZS_MT_N - 1)];
 }
 __device__ __forceinline__ void wave_rng_put(WaveRng& r, const uint32_t (&v)[WR_STAGE_K]) {
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & 63;
 #pragma unroll
     for (int u = 0; u < WR_STAGE_K; u++)
         if (lane + 64 * u < 2 * ZS_MT_N) r.lr[lane + 64 * u] = v[u];
@@ -49,7 +49,7 @@ __device__ __forceinline__ void wave_rng_stage(WaveRng& r) {
 // next block of the stream (LDS slot ^ 1) from the current one (_randommodule.c genrand_uint32's
 // twist), cooperatively in three dependency phases
 __device__ __forceinline__ void wave_twist(WaveRng& r, uint32_t slot) {
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & 63;
     const lu32* src = r.lr + slot * ZS_MT_N;
     lu32* nw = r.lr + (slot ^ 1u) * ZS_MT_N;
     for (int k = lane; k < ZS_MT_N - ZS_MT_M; k += 64) nw[k] = mt_f(src[k], src[k + 1], src[k + ZS_MT_M]);
@@ -65,7 +65,7 @@ __device__ __forceinline__ void wave_twist(WaveRng& r, uint32_t slot) {
 
 // write the twisted slots back to the env's ring in HBM (no wait: the next reader is a later launch)
 __device__ __forceinline__ void wave_rng_flush(const WaveRng& r) {
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & 63;
     for (int sl = 0; sl < 2; sl++)
         if ((r.dirty >> sl) & 1)
             for (int k = lane; k < ZS_MT_N; k += 64) r.ring[sl * ZS_MT_N + k] = r.lr[sl * ZS_MT_N + k];
@@ -86,7 +86,7 @@ __device__ __forceinline__ void rng_block_load(WaveRng& r, uint32_t st) {
     }
 #pragma unroll
     for (int q = 0; q < WR_Q; q++) {
-        uint32_t p = off + q * 64 + threadIdx.x;
+        uint32_t p = off + q * 64 + (threadIdx.x & 63);
         r.word[q] = mt_temper(p < ZS_MT_N ? r.lr[slot * ZS_MT_N + p] : r.lr[(slot ^ 1u) * ZS_MT_N + p - ZS_MT_N]);
     }
     r.st = st_pack(off, slot, ready);
@@ -113,7 +113,7 @@ __device__ __forceinline__ uint32_t wr_sub(const R& r, int q) {
 // the consumed words.
 template <class R, class Put>
 __device__ __forceinline__ void wave_draws(R& r, int n, int dstep, int count, int krec, Put put) {
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & 63;
     const unsigned long long below = (1ull << lane) - 1ull;
     int done = 0;
     while (done < count) {

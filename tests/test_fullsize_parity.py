@@ -259,15 +259,17 @@ def _side_reset(eng):
 
 def test_c3_65536_multistep_graph_side_reset():
     """Five steps per graph launch at the headline size (zs_step_graph_n), the reset work on the side
-    stream forked and joined inside every captured step; TimeLimit 16, so 65 536-env autoreset waves fall
-    inside launches.  Every fifth step's outputs and the final states against the oracle."""
-    r = run_full(lambda n: c3(n, max_steps=16), 65536, 40, graph_steps=5, min_resets=1, after=_side_reset)
-    assert r >= 1
+    stream forked and joined inside every captured step; TimeLimit 14, so 65 536-env autoreset waves fall
+    inside launches (their reset work at steps 15 and 30, the last steps of launches, whose outputs are
+    seen).  Every fifth step's outputs and the final states against the oracle."""
+    r = run_full(lambda n: c3(n, max_steps=14), 65536, 40, graph_steps=5, min_resets=2 * 65536, after=_side_reset)
+    assert r >= 2 * 65536
 
 
 def test_c5_65536_multistep_graph_side_reset():
-    """Eight steps per graph launch at C5's size (int16, side-stream reset), TimeLimit 12."""
-    run_full(lambda n: c5(n, max_steps=12), 65536, 32, graph_steps=8, min_resets=1, after=_side_reset)
+    """Eight steps per graph launch at C5's size (int16, side-stream reset), TimeLimit 15 (autoresets at
+    steps 16 and 32, the last steps of launches; the episodes' ends inside them)."""
+    run_full(lambda n: c5(n, max_steps=15), 65536, 32, graph_steps=8, min_resets=2 * 65536, after=_side_reset)
 
 
 def test_c4_16384_multistep_graph_respawn():
@@ -276,3 +278,31 @@ def test_c4_16384_multistep_graph_respawn():
         _side_reset(eng)
         assert eng.describe()["respawn"] == "k_respawn"
     run_full(c4, 16384, 48, graph_steps=8, min_resets=1, after=check)
+
+
+def _fstep(eng):
+    desc = eng.describe()
+    assert desc["step_kernel"] == "k_fstep" and desc["obs_kernel"] == "k_fstep", desc
+
+
+def test_c3_65536_fstep_graph():
+    """The headline size through the one-launch step (k_fstep: tick, encoder and writer waves in every
+    workgroup), TimeLimit 16: the tick waves rebuild the pending envs of 65 536-env autoreset waves."""
+    r = run_full(lambda n: c3(n, max_steps=16), 65536, 40, launch={"fstep": 1}, min_resets=2 * 65536, after=_fstep)
+    assert r >= 2 * 65536
+
+
+def test_c3_65536_fstep_eager_masked():
+    """k_fstep through eager launches after a masked reset of every third env."""
+    run_full(c3, 65536, 24, graph=False, twice=3, launch={"fstep": 1}, min_resets=0, after=_fstep)
+
+
+def test_c5_65536_fstep_graph():
+    """C5 (int16, 4 agents, env pairs per ring unit) through k_fstep, TimeLimit 12."""
+    run_full(lambda n: c5(n, max_steps=12), 65536, 30, launch={"fstep": 1}, min_resets=2 * 65536, after=_fstep)
+
+
+def test_c3_4097_fstep_odd():
+    """k_fstep over an env count that leaves the last unit and the last workgroup short."""
+    run_full(lambda n: c3(n, max_steps=10), 4097, 25, seed0=31, launch={"fstep": 1, "fused": -1}, min_resets=1,
+             after=_fstep)

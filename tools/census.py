@@ -38,12 +38,12 @@ def c5(n=1, max_steps=1000):
 RUNS = [
     ("test_c3_65536_graph", c3, 65536, 40, 0, 0, 8),
     ("test_c3_65536_truncation_waves", lambda: c3(max_steps=16), 65536, 40, 0, 3, 8),
-    ("test_c3_65536_multistep_graph_side_reset", lambda: c3(max_steps=16), 65536, 40, 0, 0, 8),
+    ("test_c3_65536_multistep_graph_side_reset", lambda: c3(max_steps=14), 65536, 40, 0, 0, 8),
     ("test_c2_4096_graph", c3, 4096, 60, 4242, 0, 16),
     ("test_c3_8192_shard_graph", c3, 8192, 60, 6 * 8192, 0, 16),
     ("test_c3_8192_shard_multistep_graph", lambda: c3(max_steps=15), 8192, 48, 4 * 8192, 0, 16),
     ("test_c5_65536_int16_graph", c5, 65536, 40, 0, 0, 16),
-    ("test_c5_65536_multistep_graph_side_reset", lambda: c5(max_steps=12), 65536, 32, 0, 0, 16),
+    ("test_c5_65536_multistep_graph_side_reset", lambda: c5(max_steps=15), 65536, 32, 0, 0, 16),
     ("test_c5_8192_int16_shard_graph", c5, 8192, 48, 5 * 8192, 0, 16),
     ("test_c4_16384_graph", c4, 16384, 80, 0, 0, 32),
     ("test_c4_16384_multistep_graph_respawn", c4, 16384, 48, 0, 0, 32),
