@@ -86,15 +86,22 @@ __global__ void __launch_bounds__(64 * FS_WAVES, 1) k_fstep(Dev d, FsArgs a) {
             k = __builtin_amdgcn_readfirstlane(__shfl(k, 0));
             if (k >= nu) break;
             unsigned long long pend = 0ull;
-            tick_wg<G>(d, u0 + k, a.actions, a.rew, a.done, a.trunc, a.listed, a.reset_out, a.rlist, a.rcount, nullptr,
+            // the tick reads the Dev fields through a kernarg pointer the loop cannot see through, so they are
+            // loaded where each unit uses them instead of being hoisted out of the loop and kept live across
+            // every unit (SGPR pressure: 668 B of spills per lane)
+            typedef const __attribute__((address_space(4))) Dev CDev;
+            CDev* dp = (CDev*)__builtin_amdgcn_kernarg_segment_ptr();
+            asm volatile("" : "+s"(dp));
+            const Dev& dd = *(const Dev*)dp;
+            tick_wg<G>(dd, u0 + k, a.actions, a.rew, a.done, a.trunc, a.listed, a.reset_out, a.rlist, a.rcount, nullptr,
                        0, d.N, reg, &pend);
             wave_sync();
             if (pend) {  // the unit's envs that ended at the previous step: World rebuilt (game.py:151-169)
-                const ResetLds Lr = reset_lds_carve(d, (uint8_t*)reg);
+                const ResetLds Lr = reset_lds_carve(dd, (uint8_t*)reg);
                 while (pend) {
                     const int g = (__ffsll((long long)pend) - 1) / G;
                     pend &= ~(1ull << (g * G));
-                    reset_env_wave(d, Lr, (u0 + k) * NE + g, 1, a.err);
+                    reset_env_wave(dd, Lr, (u0 + k) * NE + g, 1, a.err);
                 }
             }
             // the unit's stores completed (in L2) before its flag: a workgroup release waits for them

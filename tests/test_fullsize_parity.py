@@ -25,9 +25,9 @@ def c3(n, max_steps=1000):
                                  minimum_zombies=0, max_episode_steps=max_steps)
 
 
-def c4(n):
+def c4(n, max_steps=1000):
     return _abi.multi_env_config(n, "safehouse", [], "city128", ["0", "1", "2", "3"], initial_zombies=50,
-                                 minimum_zombies=50, max_episode_steps=1000)
+                                 minimum_zombies=50, max_episode_steps=max_steps)
 
 
 def c5(n, max_steps=1000):
@@ -273,11 +273,12 @@ def test_c5_65536_multistep_graph_side_reset():
 
 
 def test_c4_16384_multistep_graph_respawn():
-    """Eight steps per graph launch at C4 (side-stream reset, k_respawn after every tick)."""
+    """Eight steps per graph launch at C4 (side-stream reset, k_respawn after every tick), TimeLimit 15: the
+    16 384-env autoreset waves at steps 16 and 32 are the last steps of launches."""
     def check(eng):
         _side_reset(eng)
         assert eng.describe()["respawn"] == "k_respawn"
-    run_full(c4, 16384, 48, graph_steps=8, min_resets=1, after=check)
+    run_full(lambda n: c4(n, max_steps=15), 16384, 48, graph_steps=8, min_resets=2 * 16384, after=check)
 
 
 def _fstep(eng):
@@ -304,5 +305,5 @@ def test_c5_65536_fstep_graph():
 
 def test_c3_4097_fstep_odd():
     """k_fstep over an env count that leaves the last unit and the last workgroup short."""
-    run_full(lambda n: c3(n, max_steps=10), 4097, 25, seed0=31, launch={"fstep": 1, "fused": -1}, min_resets=1,
-             after=_fstep)
+    run_full(lambda n: c3(n, max_steps=10), 4097, 25, seed0=31,
+             launch={"fstep": 1, "fused": -1, "obs_lds": 1, "obs_ring": 1}, min_resets=1, after=_fstep)

@@ -28,9 +28,9 @@ def c5(n, max_steps=1000):
                                  minimum_zombies=0, max_episode_steps=max_steps, obs_dtype=_abi.DTYPE_I16)
 
 
-def c4(n):
+def c4(n, max_steps=1000):
     return _abi.multi_env_config(n, "safehouse", [], "city128", ["0", "1", "2", "3"], initial_zombies=50,
-                                 minimum_zombies=50, max_episode_steps=1000)
+                                 minimum_zombies=50, max_episode_steps=max_steps)
 
 
 def run_external_hashes(make_builder, n, steps, seed0=0, nd=7, min_resets=1):
@@ -77,7 +77,8 @@ def test_external_graph_c5_65536_int16():
 
 
 def test_external_graph_c4_16384():
-    run_external_hashes(c4, 16384, 40)
+    """C4 (k_respawn after every tick), TimeLimit 15: autoreset waves at steps 16 and 32."""
+    run_external_hashes(lambda n: c4(n, max_steps=15), 16384, 34, min_resets=2 * 16384)
 
 
 @pytest.mark.parametrize("maker,n", [(c3, 48), (c5, 40)])

@@ -24,9 +24,9 @@ def c3(n=1, max_steps=1000):
                                  minimum_zombies=0, max_episode_steps=max_steps)
 
 
-def c4(n=1):
+def c4(n=1, max_steps=1000):
     return _abi.multi_env_config(n, "safehouse", [], "city128", ["0", "1", "2", "3"], initial_zombies=50,
-                                 minimum_zombies=50, max_episode_steps=1000)
+                                 minimum_zombies=50, max_episode_steps=max_steps)
 
 
 def c5(n=1, max_steps=1000):
@@ -46,7 +46,7 @@ RUNS = [
     ("test_c5_65536_multistep_graph_side_reset", lambda: c5(max_steps=15), 65536, 32, 0, 0, 16),
     ("test_c5_8192_int16_shard_graph", c5, 8192, 48, 5 * 8192, 0, 16),
     ("test_c4_16384_graph", c4, 16384, 80, 0, 0, 32),
-    ("test_c4_16384_multistep_graph_respawn", c4, 16384, 48, 0, 0, 32),
+    ("test_c4_16384_multistep_graph_respawn", lambda: c4(max_steps=15), 16384, 48, 0, 0, 32),
     ("test_external_graph_c3_65536", lambda: c3(max_steps=16), 65536, 36, 0, 0, 8),
 ]
 
