@@ -169,7 +169,10 @@ typedef struct zs_launch {
                               * the env's lanes in parallel (core.py:103-119)                          */
     int32_t fstep;           /* the step as one launch (k_fstep): tick, observation encoder and writer
                               * waves in every workgroup, the tick overlapping the observation stream  */
-    int32_t reserved[9];
+    int32_t fs_tick;         /* k_fstep's tick waves per workgroup (4 or 6)                            */
+    int32_t tick_early;      /* k_tick (5 waves per SIMD) loads the RNG window's first words with its
+                              * first load round, overlapping their round trip with the decisions      */
+    int32_t reserved[7];
 } zs_launch;
 
 typedef struct zs_config {

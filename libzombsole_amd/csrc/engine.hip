@@ -288,6 +288,7 @@ struct zs_handle {
     int fused = 0;  // zs_step runs reset work and the tick in one launch (k_step)
     int fstep = 0;  // zs_step is one k_fstep launch (tick, encoder and writer waves per workgroup, zs_fstep.hpp)
     FsLayout fs_l;
+    FsShape fs_sh;
     int fs_grid = 0;
     int* d_fsctr = nullptr;  // k_fstep's finished-workgroup counter (zero between launches)
     int resident = 0;  // step-launch workgroups resident per CU (layout choice)
@@ -898,20 +899,26 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
         const int grid = std::max(1, std::min(cus, nunits));
         const int upw = (nunits + grid - 1) / grid;
         const int tick_b = (int)std::max(h->lds, h->reset_lds);
+        // role shape (tick / encoder / writer waves); zs_launch.fs_tick = 6 takes six tick waves
+        const FsShape sh = h->ov.fs_tick == 6 ? FsShape{6, 7, 3} : FsShape{4, 9, 3};
         FsLayout L;
         int us = 8 / pair;
         for (; us >= 2; us--) {
-            L = fs_layout(patch_static_bytes(d.opad_n, d.O), patch_enc_bytes(d.DW, d.O),
-                          obs_stage_slot_bytes(ts, nobs * pair), us, tick_b);
+            L = fs_layout(sh, patch_static_bytes(d.opad_n, d.O), patch_enc_bytes(d.DW, d.O),
+                          obs_stage_slot_bytes(ts, nobs * pair), us, tick_b, upw * (64 / h->G));
             if (L.bytes <= 160 * 1024) break;
         }
-        if (us >= 2 && upw <= FS_MAX_UNITS && fstep_attr(h->G, d.obs_dtype, nobs, L.bytes) == hipSuccess) {
+        if (us >= 2 && upw <= FS_MAX_UNITS && fstep_attr(h->G, d.obs_dtype, nobs, sh, L.bytes) == hipSuccess) {
             TRY(dalloc(h, &h->d_fsctr, 1));
             h->fstep = 1;
             h->fs_l = L;
+            h->fs_sh = sh;
             h->fs_grid = grid;
         }
     }
+    if (getenv("ZS_VERBOSE") && h->fstep)
+        fprintf(stderr, "zs_create: k_fstep shape %d/%d/%d, %d ring slots, %d B of LDS, grid %d\n", h->fs_sh.nt,
+                h->fs_sh.nen, h->fs_sh.nw, h->fs_l.us, h->fs_l.bytes, h->fs_grid);
     if (getenv("ZS_VERBOSE"))
         fprintf(stderr, "zs_create: N=%d E=%d G=%d step_lds=%zu resident=%d reset_lds=%zu rw_cap=%d cand_cap=%d "
                         "lists_cap=%d fused=%d fobs=%d obs_img=%d k_obs_img=%d x%d pipe=%d gather=%d pipe_wgs=%d reset_side=%d defer_respawn=%d\n",
@@ -1069,6 +1076,7 @@ static int launch_tick(zs_handle* h, const int32_t* actions, double* rew, uint8_
     a.cur_list = (const int*)h->d_rlist[p];
     a.cur_count = (const int*)(h->d_rcount + p);
     a.err = h->d_err;
+    a.early = h->ov.tick_early > 0;
     hipError_t le;
     switch (h->G) {
     case 1: le = launch_tick_g1(h->fused, h->tick_waves, grid, h->lds, s, d, a); break;
@@ -1188,7 +1196,7 @@ static int step_fstep(zs_handle* h, const int32_t* actions_dev, void* obs_dev, d
     a.L = h->fs_l;
     int i0 = -1, i1 = -1;
     if (h->prof) HIPCHK(hipEventRecord(prof_event(h, &i0), s));
-    const hipError_t le = launch_fstep(h->G, d.obs_dtype, obs_count(d.obs_scope, d.reward_mode, d.A),
+    const hipError_t le = launch_fstep(h->G, d.obs_dtype, obs_count(d.obs_scope, d.reward_mode, d.A), h->fs_sh,
                                        (unsigned)h->fs_grid, s, d, a);
     d.pol_n = 0, d.pol_step = nullptr;
     d.tail_cnt0 = d.tail_cnt1 = nullptr, d.tail_step = nullptr;

@@ -1,34 +1,42 @@
-// k_fstep.hip — the one-launch step (zs_fstep.hpp) for the shapes it is instantiated for:
-// lanes per env G, observation dtype and observations per env (C3: 8 / int64 / 2, C5: 16 / int16 / 4).
+// k_fstep.hip — the one-launch step (zs_fstep.hpp) for the shapes it is instantiated for: lanes per env G,
+// observation dtype, observations per env, and the role shape (tick, encoder, writer waves per workgroup).
 #include "zs_fstep.hpp"
 
-template <int G, typename T, int NOBS>
+template <int G, typename T, int NOBS, int NT, int NEN, int NW>
 static hipError_t fs_go(unsigned grid, hipStream_t s, const Dev& d, const FsArgs& a) {
-    hipLaunchKernelGGL((k_fstep<G, T, NOBS>), dim3(grid), dim3(64 * FS_WAVES), a.L.bytes, s, d, a);
+    hipLaunchKernelGGL((k_fstep<G, T, NOBS, NT, NEN, NW>), dim3(grid), dim3(64 * (NT + NEN + NW)), a.L.bytes, s, d, a);
     return hipGetLastError();
 }
 
-template <int G, typename T, int NOBS>
+template <int G, typename T, int NOBS, int NT, int NEN, int NW>
 static hipError_t fs_attr(int bytes) {
-    return hipFuncSetAttribute((const void*)k_fstep<G, T, NOBS>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    return hipFuncSetAttribute((const void*)k_fstep<G, T, NOBS, NT, NEN, NW>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               bytes);
 }
 
-#define FS_SHAPES(X)              \
-    X(8, ZS_DTYPE_I64, int64_t, 2) \
-    X(16, ZS_DTYPE_I64, int64_t, 2) \
-    X(16, ZS_DTYPE_I16, int16_t, 4)
+// (G, dtype, T, observations per env, tick / encoder / writer waves)
+#ifndef FS_SHAPES
+#define FS_SHAPES(X)                         \
+    X(8, ZS_DTYPE_I64, int64_t, 2, 4, 9, 3)  \
+    X(8, ZS_DTYPE_I64, int64_t, 2, 6, 7, 3)  \
+    X(16, ZS_DTYPE_I16, int16_t, 4, 4, 9, 3) \
+    X(16, ZS_DTYPE_I16, int16_t, 4, 6, 7, 3)
+#endif
 
-hipError_t launch_fstep(int G, int dtype, int nobs, unsigned grid, hipStream_t s, const Dev& d, const FsArgs& a) {
-#define FS_LAUNCH(g, dt, t, n) \
-    if (G == g && dtype == dt && nobs == n) return fs_go<g, t, n>(grid, s, d, a);
+hipError_t launch_fstep(int G, int dtype, int nobs, FsShape sh, unsigned grid, hipStream_t s, const Dev& d,
+                        const FsArgs& a) {
+#define FS_LAUNCH(g, dt, t, n, vt, ve, vw)                                                 \
+    if (G == g && dtype == dt && nobs == n && sh.nt == vt && sh.nen == ve && sh.nw == vw) \
+        return fs_go<g, t, n, vt, ve, vw>(grid, s, d, a);
     FS_SHAPES(FS_LAUNCH)
 #undef FS_LAUNCH
     return hipErrorNotSupported;
 }
 
-hipError_t fstep_attr(int G, int dtype, int nobs, int bytes) {
-#define FS_ATTR(g, dt, t, n) \
-    if (G == g && dtype == dt && nobs == n) return fs_attr<g, t, n>(bytes);
+hipError_t fstep_attr(int G, int dtype, int nobs, FsShape sh, int bytes) {
+#define FS_ATTR(g, dt, t, n, vt, ve, vw)                                                   \
+    if (G == g && dtype == dt && nobs == n && sh.nt == vt && sh.nen == ve && sh.nw == vw) \
+        return fs_attr<g, t, n, vt, ve, vw>(bytes);
     FS_SHAPES(FS_ATTR)
 #undef FS_ATTR
     return hipErrorNotSupported;

@@ -5,16 +5,17 @@
 // C3 266 us) back to back, so the step costs their sum.  Envs are independent, so the observations of
 // env block b can stream while block b + 1 ticks.  One workgroup per CU owns a contiguous range of the
 // step's tick units (64 / G envs each) and splits its waves into three roles:
-//   * FS_TICK tick waves take the range's units from an LDS counter and run the tick on each
+//   * NT tick waves take the range's units from an LDS counter and run the tick on each
 //     (tick_wg, zs_tick.hpp: decisions, shuffle, execution, cleanup, rewards, rules for the stepping
 //     envs; gym/multiagent_env.py:111-171 with core.py:72-78), then rebuild the unit's envs that ended
 //     at the previous step (reset_env_wave, zs_reset.hpp; game.py:151-169: the next-step autoreset the
 //     unfused step leaves to k_reset on its side stream), and publish the unit as ready in LDS;
-//   * FS_ENC encoder waves walk the range's envs in order, wait for each env's unit, load the env's new
-//     state from L2 (device-scope loads, which bypass the CU's L1: lines loaded before the tick wrote
-//     them may be there) and encode its agents' 21 x 21 x 3 windows into a ring slot with the
-//     padded-table encoder (PatchEnc, zs_obs.hpp; gym/observation.py:57-173);
-//   * FS_WRT writer waves stream the ring's slots out as 16-B stores (obs_stage_flush), as k_obs_ring's do.
+//   * NEN encoder waves walk the range's envs in order, wait for each env's unit, load the env's new
+//     state (its dirty masks from LDS, where the tick wave published them) and encode its agents'
+//     21 x 21 x 3 windows into a ring slot with the
+//     padded-table encoder (PatchEnc, zs_obs.hpp; gym/observation.py:57-173), the next env's loads in
+//     flight while one env encodes;
+//   * NW writer waves stream the ring's slots out as 16-B stores (obs_stage_flush), as k_obs_ring's do.
 // No wave waits on a wave of another workgroup, and inside the workgroup the waits only point from
 // encoders to tick waves (a unit is published once ticked) and to writers (a slot is free once written
 // out), writers to encoders (a slot is written out once filled), all in rising order: every wave reaches
@@ -26,46 +27,49 @@
 #include "zs_tick.hpp"
 #include "zs_launch.hpp"
 
-// device-scope (L2) loads of words this launch's tick waves wrote
+// device-scope loads: the dirty masks, which the tick updates with device-scope atomics and 16 envs share
+// a cache line of (a line another wave of this CU loaded earlier may be in its L1)
 template <typename V>
-__device__ __forceinline__ V ld_l2(const V* p) {
+__device__ __forceinline__ V ld_dev(const V* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// obs_prefetch_env's loads (zs_obs.hpp) from L2: the env's dirty masks first (they select its own rows
-// or the shared clean rows), then the entity slots, dead-body words, present words and obstacle HP
-__device__ __forceinline__ void fs_prefetch_env(const Dev& d, int e, ObsPrefetch& f) {
+// obs_prefetch_env's loads (zs_obs.hpp) for env e with its dirty masks dq (published in LDS by the tick
+// wave): the entity slots, dead-body words, present words and obstacle HP.  Plain loads: the tick wave that
+// wrote them is in this workgroup and released them before publishing the env (a workgroup-scope release /
+// acquire pair needs no cache maintenance on gfx950: the CU's waves share its L1).
+__device__ __forceinline__ void fs_prefetch_env(const Dev& d, int e, zs_v2u dq, ObsPrefetch& f) {
     const int lane = threadIdx.x & 63;
-    const uint32_t hd = ld_l2(d.hp_dirty + e), dd = ld_l2(d.dead_dirty + e);
+    const uint32_t hd = dq.x, dd = dq.y;
     const int s = lane < d.E ? lane : d.E - 1;
-    f.pos = ld_l2(d.pos + EIX(d, s, e));
-    f.life = ld_l2(d.life + EIX(d, s, e));
-    f.wp = ld_l2(d.weapon + EIX(d, s, e));
-    f.pr = ld_l2(d.present + EIX(d, s, e));
+    f.pos = d.pos[EIX(d, s, e)];
+    f.life = d.life[EIX(d, s, e)];
+    f.wp = d.weapon[EIX(d, s, e)];
+    f.pr = d.present[EIX(d, s, e)];
     const uint32_t* dr = d.dead + (size_t)e * d.DW;
 #pragma unroll
     for (int i = 0; i < OBS_PF_D; i++) {
         const int w = min(lane + 64 * i, d.DW - 1);
-        f.dead[i] = ld_l2((((dd >> ((w * d.dead_chunk_m) >> 20)) & 1u) ? dr : d.dead_zero) + w);
+        f.dead[i] = (((dd >> ((w * d.dead_chunk_m) >> 20)) & 1u) ? dr : d.dead_zero)[w];
     }
-    f.opres = ld_l2((hd ? d.obst_present + (size_t)e * d.OW : d.opres_full) + min(lane, max(d.OW - 1, 0)));
+    f.opres = (hd ? d.obst_present + (size_t)e * d.OW : d.opres_full)[min(lane, max(d.OW - 1, 0))];
     const int32_t* hr = d.obst_hp + (size_t)e * d.O;
 #pragma unroll
     for (int i = 0; i < OBS_PF_H; i++) {
         const int o = min(lane + 64 * i, d.O - 1);
-        f.hp[i] = ld_l2((((hd >> ((o * d.hp_chunk_m) >> 20)) & 1u) ? hr : d.hp_init) + o);
+        f.hp[i] = (((hd >> ((o * d.hp_chunk_m) >> 20)) & 1u) ? hr : d.hp_init)[o];
     }
 }
 
-template <int G, typename T, int NOBS>
-__global__ void __launch_bounds__(64 * FS_WAVES, 1) k_fstep(Dev d, FsArgs a) {
+template <int G, typename T, int NOBS, int NT, int NEN, int NW>
+__global__ void __launch_bounds__(64 * (NT + NEN + NW), 1) k_fstep(Dev d, FsArgs a) {
     extern __shared__ __align__(16) uint8_t smem[];
     typedef typename obs_stage<T>::type S;
     constexpr int NE = 64 / G, WW = 21, PLANE = WW * WW, TS = (int)sizeof(T);
     constexpr int PAIR = ring_pair(TS, NOBS), BLK = NOBS * 3 * PLANE;
     const FsLayout& FL = a.L;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    // this workgroup's tick units [u0, u1) and envs [e_lo, e_hi)
+    // this workgroup's tick units [u0, u1) and envs [e_lo, e_lo + n_env)
     const int nunits = (d.N + NE - 1) / NE;
     const int upw = (nunits + (int)gridDim.x - 1) / (int)gridDim.x;
     const int u0 = min((int)blockIdx.x * upw, nunits), u1 = min(u0 + upw, nunits), nu = u1 - u0;
@@ -73,11 +77,12 @@ __global__ void __launch_bounds__(64 * FS_WAVES, 1) k_fstep(Dev d, FsArgs a) {
     ZS_LDS int* state = (ZS_LDS int*)(smem + FL.off_state);  // ring protocol word per slot and env of a unit
     ZS_LDS int* ready = (ZS_LDS int*)(smem + FL.off_ready);  // 1 once tick unit u0 + k is ticked and reset
     ZS_LDS int* ctr = (ZS_LDS int*)(smem + FL.off_ctr);      // next tick unit to take
+    ZS_LDS zs_v2u* dqs = (ZS_LDS zs_v2u*)(smem + FL.off_dq); // {hp_dirty, dead_dirty} of env e_lo + t
     for (int i = threadIdx.x; i < 16 + FS_MAX_UNITS + 4; i += blockDim.x) state[i] = 0;  // the three arrays are adjacent
     patch_stage_static(d, smem);  // barriers: the zeroed words and the tables before any role starts
     const int US = FL.us;
     lu8* slots = (lu8*)(smem + FL.off_slots);
-    if (wave < FS_TICK) {
+    if (wave < NT) {
         // ---- tick role ----
         lu8* reg = (lu8*)(smem + FL.off_tick + wave * FL.tick_bytes);
         for (;;) {
@@ -104,24 +109,34 @@ __global__ void __launch_bounds__(64 * FS_WAVES, 1) k_fstep(Dev d, FsArgs a) {
                     reset_env_wave(dd, Lr, (u0 + k) * NE + g, 1, a.err);
                 }
             }
-            // the unit's stores completed (in L2) before its flag: a workgroup release waits for them
+            // the unit's dirty masks for its encoders (after every atomic of the unit: the loads wait for them)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (lane < NE && (u0 + k) * NE + lane < d.N) {
+                const int e = (u0 + k) * NE + lane;
+                dqs[e - e_lo] = zs_v2u{ld_dev(d.hp_dirty + e), ld_dev(d.dead_dirty + e)};
+            }
+            // the unit's stores completed before its flag: a workgroup release waits for them
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             if (lane == 0) ring_state_store(&ready[k], 1);
             wave_sync();
         }
-    } else if (wave < FS_TICK + FS_ENC) {
-        // ---- encoder role: envs e_lo + w, + FS_ENC, ... ----
-        const int w = wave - FS_TICK;
+    } else if (wave < NT + NEN) {
+        // ---- encoder role: envs e_lo + w, + NEN, ...; the next env's loads in flight while this one encodes ----
+        const int w = wave - NT;
         lu8* wb = (lu8*)(smem + FL.off_enc + w * FL.enc_bytes);
         PatchEnc<S> pe(d, smem, wb, lane);
         T* out = (T*)a.obs;
-        for (int t = w; t < n_env; t += FS_ENC) {
-            const int e = e_lo + t;
+        ObsPrefetch f;
+        auto fetch = [&](int t) {  // wait for env e_lo + t's unit, then issue its loads into f
             ring_wait(&ready[t / NE], 1);
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            ObsPrefetch f;
-            fs_prefetch_env(d, e, f);
+            fs_prefetch_env(d, e_lo + t, dqs[t], f);
+        };
+        if (w < n_env) fetch(w);
+        for (int t = w; t < n_env; t += NEN) {
+            const int e = e_lo + t;
             pe.build(d, f);
+            if (t + NEN < n_env) fetch(t + NEN);
             const int u = t / PAIR, h = t % PAIR, q = u % US;
             if (u >= US) ring_wait(&state[PAIR * q + h], 2 * (u - US) + 2);
             wave_sync();
@@ -132,10 +147,10 @@ __global__ void __launch_bounds__(64 * FS_WAVES, 1) k_fstep(Dev d, FsArgs a) {
             ring_state_store(&state[PAIR * q + h], 2 * u + 1);
         }
     } else {
-        // ---- writer role: ring units w, w + FS_WRT, ... (PAIR envs each) ----
+        // ---- writer role: ring units w, w + NW, ... (PAIR envs each) ----
         T* out = (T*)a.obs;
         const int nru = (n_env + PAIR - 1) / PAIR;
-        for (int u = wave - FS_TICK - FS_ENC; u < nru; u += FS_WRT) {
+        for (int u = wave - NT - NEN; u < nru; u += NW) {
             const int q = u % US, e = e_lo + PAIR * u;
             const bool whole = PAIR * u + PAIR <= n_env;
             for (int h = 0; h < PAIR; h++)

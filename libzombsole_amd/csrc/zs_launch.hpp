@@ -26,6 +26,7 @@ struct TickArgs {
     const int* cur_list;  // k_step: the pending list this step drains
     const int* cur_count;
     int* err;
+    int early;           // k_tick: the RNG window's first 4G words loaded with the first load round (EARLY)
 };
 
 #define ZS_TICK_DECL(G)                                                                                          \
@@ -41,43 +42,45 @@ ZS_TICK_DECL(32)
 ZS_TICK_DECL(64)
 #undef ZS_TICK_DECL
 
-// k_fstep (zs_fstep.hpp): the step as one launch with tick, encoder and writer waves per workgroup
-#ifndef FS_TICK
-#define FS_TICK 4
-#endif
-#ifndef FS_ENC
-#define FS_ENC 8
-#endif
-#ifndef FS_WRT
-#define FS_WRT 3
-#endif
-#define FS_WAVES (FS_TICK + FS_ENC + FS_WRT)
+// k_fstep (zs_fstep.hpp): the step as one launch with tick, encoder and writer waves per workgroup.
+// Role shapes (tick, encoder, writer waves) per instance; FsShape picks one by name.
 #define FS_MAX_UNITS 512  // tick units per workgroup (ready flags in LDS)
+struct FsShape {
+    int nt, nen, nw;
+};
 
-// LDS of a k_fstep workgroup: the padded-table encoder's static tables, FS_ENC encoder regions, `us` ring
-// slots, FS_TICK tick regions (each the tick's image of one unit, or the reset image of one env), then the
-// ring protocol words, the units' ready flags and the unit counter.
+// LDS of a k_fstep workgroup: the padded-table encoder's static tables, nen encoder regions, `us` ring
+// slots, nt tick regions (each the tick's image of one unit, or the reset image of one env), the dirty
+// masks of the workgroup's envs (published by the tick waves), then the ring protocol words, the units'
+// ready flags and the unit counter.
 struct FsLayout {
+    int nt, nen;
     int off_enc, enc_bytes;
     int off_slots, slot_bytes, us;
     int off_tick, tick_bytes;
+    int off_dq;
     int off_state, off_ready, off_ctr;
     int bytes;
 };
 
-__host__ __device__ inline FsLayout fs_layout(int stat_bytes, int enc_bytes, int slot_bytes, int us, int tick_bytes) {
+__host__ __device__ inline FsLayout fs_layout(FsShape sh, int stat_bytes, int enc_bytes, int slot_bytes, int us,
+                                              int tick_bytes, int envs_per_wg) {
     FsLayout L;
+    L.nt = sh.nt;
+    L.nen = sh.nen;
     int o = ((stat_bytes + 15) / 16) * 16;
     L.off_enc = o;
     L.enc_bytes = ((enc_bytes + 15) / 16) * 16;
-    o += FS_ENC * L.enc_bytes;
+    o += sh.nen * L.enc_bytes;
     L.off_slots = o;
     L.slot_bytes = ((slot_bytes + 15) / 16) * 16;
     L.us = us;
     o += us * L.slot_bytes;
     L.off_tick = o;
     L.tick_bytes = ((tick_bytes + 15) / 16) * 16;
-    o += FS_TICK * L.tick_bytes;
+    o += sh.nt * L.tick_bytes;
+    L.off_dq = o;
+    o += ((8 * envs_per_wg + 15) / 16) * 16;
     L.off_state = o;
     o += 16 * 4;
     L.off_ready = o;
@@ -103,8 +106,9 @@ struct FsArgs {
     FsLayout L;
 };
 
-hipError_t launch_fstep(int G, int dtype, int nobs, unsigned grid, hipStream_t s, const Dev& d, const FsArgs& a);
-hipError_t fstep_attr(int G, int dtype, int nobs, int bytes);  // hipErrorNotSupported: no such instance
+// the instances of k.fstep.hip: shape `sh` for (G, dtype, observations per env); hipErrorNotSupported when none
+hipError_t launch_fstep(int G, int dtype, int nobs, FsShape sh, unsigned grid, hipStream_t s, const Dev& d, const FsArgs& a);
+hipError_t fstep_attr(int G, int dtype, int nobs, FsShape sh, int bytes);
 
 // observation kernels
 enum { OBSK_OBS = 0, OBSK_GATHER, OBSK_PIPE, OBSK_LDS, OBSK_PATCH, OBSK_RING, OBSK_BRING };

@@ -1934,11 +1934,11 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
     STAMP(7);
 }
 
-template <int G, int W = ZS_STEP_WAVES>
+template <int G, int W = ZS_STEP_WAVES, bool EARLY = false>
 __global__ void __launch_bounds__(64, W) k_tick(Dev d, const int32_t* actions, double* rew, uint8_t* done_out,
                                              uint8_t* trunc_out, uint8_t* listed_out, uint8_t* reset_out,
                                              int* reset_list, int* reset_count, void* obs_out, int env0, int env1) {
     extern __shared__ __align__(16) uint8_t smem[];
-    tick_wg<G>(d, xcd_remap(blockIdx.x, gridDim.x), actions, rew, done_out, trunc_out, listed_out, reset_out, reset_list,
+    tick_wg<G, EARLY>(d, xcd_remap(blockIdx.x, gridDim.x), actions, rew, done_out, trunc_out, listed_out, reset_out, reset_list,
                reset_count, obs_out, env0, env1, (lu8*)smem);
 }

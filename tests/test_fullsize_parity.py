@@ -303,7 +303,33 @@ def test_c5_65536_fstep_graph():
     run_full(lambda n: c5(n, max_steps=12), 65536, 30, launch={"fstep": 1}, min_resets=2 * 65536, after=_fstep)
 
 
-def test_c3_4097_fstep_odd():
-    """k_fstep over an env count that leaves the last unit and the last workgroup short."""
-    run_full(lambda n: c3(n, max_steps=10), 4097, 25, seed0=31,
-             launch={"fstep": 1, "fused": -1, "obs_lds": 1, "obs_ring": 1}, min_resets=1, after=_fstep)
+def test_c5_65535_fstep_odd():
+    """k_fstep over an odd env count (C5's shape: G = 16, int16 env pairs per ring unit): the last tick unit,
+    the last workgroup's range and its last ring unit (a single env) short."""
+    run_full(lambda n: c5(n, max_steps=10), 65535, 25, seed0=31, launch={"fstep": 1}, min_resets=1, after=_fstep)
+
+
+def test_c3_65533_fstep_odd():
+    """The same for C3's shape (G = 8, int64): 65 533 envs, the last tick unit holding five."""
+    run_full(lambda n: c3(n, max_steps=10), 65533, 25, seed0=77, launch={"fstep": 1}, min_resets=1, after=_fstep)
+
+
+def test_c3_65536_fstep_six_tick_waves():
+    """k_fstep's other role shape (six tick waves, seven encoders), TimeLimit 16."""
+    run_full(lambda n: c3(n, max_steps=16), 65536, 34, launch={"fstep": 1, "fs_tick": 6}, min_resets=2 * 65536,
+             after=_fstep)
+
+
+def test_c3_65536_tick_early():
+    """k_tick with the RNG window's first 4G words loaded in its first load round (zs_launch.tick_early),
+    TimeLimit 16."""
+    def early(eng):
+        desc = eng.describe()
+        assert desc["step_kernel"] == "k_tick" and desc["tick_waves"] == 5, desc
+    run_full(lambda n: c3(n, max_steps=16), 65536, 36, launch={"tick_early": 1}, min_resets=2 * 65536, after=early)
+
+
+def test_c5_65536_tick_early_five_waves():
+    """The same on C5's shape (G = 16, E = 24) at five waves per SIMD."""
+    run_full(lambda n: c5(n, max_steps=12), 65536, 28, launch={"tick_early": 1, "tick_waves": 5},
+             min_resets=2 * 65536)
