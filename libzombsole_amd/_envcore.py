@@ -30,11 +30,13 @@ class EnvCore(object):
         self.game = GameView(self.engine, 0, map_, rules_name, player_names, agent_ids, agent_weapons,
                              initial_zombies, minimum_zombies, debug)
         self._host_actions = np.zeros((1, self.engine.A, 3), dtype=np.int32)
-        self.new_world()
+        self.new_world(first=True)
 
     # Game.__initialize_world__ (game.py:151-169) on the engine, drawing from `random`
-    def new_world(self):
+    def new_world(self, first=False):
         eng = self.engine
+        if not first:
+            self.game.end_episode()  # objects of the ending episode keep their values
         eng.load_python_random(0)
         try:
             eng.reset()

@@ -888,8 +888,13 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
     // It needs the ring's shape (channels, padded-table encoders), respawns in the tick (no k_respawn),
     // an instance for (G, dtype, observations per env), and its tables, encoder regions, >= 2 ring slots
     // and FS_TICK tick / reset images in 160 KB.  zs_launch.fstep forces either.
-    if (h->ov.fstep > 0 && !h->fused && !d.defer_respawn && !d.fobs && h->obs_ring == 2 &&
-        d.obs_enc == ZS_ENC_CHANNELS) {
+    // One-round sizes (the fused step launch: 8 192-env shards) take eight tick waves, one unit each, with
+    // the reset work of the unit's pending envs after it (zs_launch.fs_tick = 8, 5 encoders and 3 writers;
+    // 86 = 6 encoders and 2 writers).
+    // k_obs_pipe's registered shape (surroundings of width 21, 1 / 2 / 4 observations, the prefetch sizes)
+    // with the padded-table encoder's limits
+    if (h->ov.fstep > 0 && !d.defer_respawn && !d.fobs && h->obs_pipe && d.obs_enc == ZS_ENC_CHANNELS &&
+        d.OW <= 64 && (long)(d.W + 20) * 21 < 65536 && d.H < 4096) {
         const int nobs = obs_count(d.obs_scope, d.reward_mode, d.A);
         const int ts = d.obs_dtype == ZS_DTYPE_I64 ? 8 : d.obs_dtype == ZS_DTYPE_I32 ? 4 : 2;
         const int pair = ring_pair(ts, nobs);
@@ -898,9 +903,18 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
         const int nunits = (d.N + 64 / h->G - 1) / (64 / h->G);
         const int grid = std::max(1, std::min(cus, nunits));
         const int upw = (nunits + grid - 1) / grid;
-        const int tick_b = (int)std::max(h->lds, h->reset_lds);
+        // the tick regions: the smallest image that holds the plain step's RNG window (the role shape, not the
+        // resident workgroups, sets the occupancy), candidates from HBM scratch, the spawn lists staged when
+        // they fit; the reset work's image of one env aliases the same region
+        int rw_need = 32;
+        while (rw_need < 512 && rw_need < 2 * d.E + 8) rw_need *= 2;
+        const int ne = 64 / h->G, lst = (d.nps + d.nzs <= 4096) ? d.nps + d.nzs : 0;
+        const int fs_tick_b = tick_layout(ne, d.E, d.DW, rw_need, 0, lst, d.A, 0).bytes;
+        const int fs_reset_b = reset_lds_bytes(d.E, d.DW, d.ncand, lst, 0);
+        const int tick_b = std::max(fs_tick_b, fs_reset_b);
         // role shape (tick / encoder / writer waves); zs_launch.fs_tick = 6 takes six tick waves
-        const FsShape sh = h->ov.fs_tick == 6 ? FsShape{6, 7, 3} : FsShape{4, 9, 3};
+        const FsShape sh = h->ov.fs_tick == 6 ? FsShape{6, 7, 3} : h->ov.fs_tick == 8 ? FsShape{8, 5, 3}
+                           : h->ov.fs_tick == 86 ? FsShape{8, 6, 2} : FsShape{4, 9, 3};
         FsLayout L;
         int us = 8 / pair;
         for (; us >= 2; us--) {
@@ -911,6 +925,13 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
         if (us >= 2 && upw <= FS_MAX_UNITS && fstep_attr(h->G, d.obs_dtype, nobs, sh, L.bytes) == hipSuccess) {
             TRY(dalloc(h, &h->d_fsctr, 1));
             h->fstep = 1;
+            h->fused = 0;  // the reset work is the tick waves'
+            d.rw_cap = rw_need;
+            d.rw_step = rw_need;
+            d.cand_cap = 0;
+            d.lists_cap = d.rlists_cap = lst;
+            h->lds = (size_t)fs_tick_b;
+            h->reset_lds = (size_t)fs_reset_b;
             h->fs_l = L;
             h->fs_sh = sh;
             h->fs_grid = grid;

@@ -61,7 +61,9 @@ __device__ __forceinline__ void fs_prefetch_env(const Dev& d, int e, zs_v2u dq, 
     }
 }
 
-template <int G, typename T, int NOBS, int NT, int NEN, int NW>
+// EARLY: the tick's RNG window loaded with its first load round (tick_wg; the one-round shapes, where each
+// tick wave takes one unit and the window's round trip is on the step's critical path)
+template <int G, typename T, int NOBS, int NT, int NEN, int NW, bool EARLY = false>
 __global__ void __launch_bounds__(64 * (NT + NEN + NW), 1) k_fstep(Dev d, FsArgs a) {
     extern __shared__ __align__(16) uint8_t smem[];
     typedef typename obs_stage<T>::type S;
@@ -98,7 +100,7 @@ __global__ void __launch_bounds__(64 * (NT + NEN + NW), 1) k_fstep(Dev d, FsArgs
             CDev* dp = (CDev*)__builtin_amdgcn_kernarg_segment_ptr();
             asm volatile("" : "+s"(dp));
             const Dev& dd = *(const Dev*)dp;
-            tick_wg<G>(dd, u0 + k, a.actions, a.rew, a.done, a.trunc, a.listed, a.reset_out, a.rlist, a.rcount, nullptr,
+            tick_wg<G, EARLY>(dd, u0 + k, a.actions, a.rew, a.done, a.trunc, a.listed, a.reset_out, a.rlist, a.rcount, nullptr,
                        0, d.N, reg, &pend);
             wave_sync();
             if (pend) {  // the unit's envs that ended at the previous step: World rebuilt (game.py:151-169)

@@ -224,6 +224,23 @@ class GameView(object):
         self._cache = None
 
     # -- objects ---------------------------------------------------------------
+    def end_episode(self):
+        """Before a reset: every object of the ending episode keeps the values it has now.  The reference
+        builds a new World and new player objects (game.py:151-169); the old objects are out of any world
+        and hold their last position and life, whatever the new episode puts in the same engine slot."""
+        views = getattr(self, "_views", None)
+        if not views:
+            return
+        st = self.engine.get_state(self.env)
+        for slot, v in views.items():
+            if v._gone:
+                continue
+            r = st.ent[slot]
+            if int(r[7]) == v._serial:
+                v._last = [int(x) for x in r]
+            v._gone = True
+        self._views = {}
+
     def new_episode(self):
         """Fresh objects after a reset (the reference builds a new World and new players,
         game.py:151-169)."""

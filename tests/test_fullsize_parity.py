@@ -333,3 +333,16 @@ def test_c5_65536_tick_early_five_waves():
     """The same on C5's shape (G = 16, E = 24) at five waves per SIMD."""
     run_full(lambda n: c5(n, max_steps=12), 65536, 28, launch={"tick_early": 1, "tick_waves": 5},
              min_resets=2 * 65536)
+
+
+def test_c3_8192_fstep_one_round():
+    """The N=8 shard through k_fstep's one-round shape (eight tick waves, one unit each, the RNG window
+    loaded early, the unit's resets after its tick), TimeLimit 15."""
+    run_full(lambda n: c3(n, max_steps=15), 8192, 40, seed0=6 * 8192, launch={"fstep": 1, "fs_tick": 8},
+             min_resets=2 * 8192, after=_fstep)
+
+
+def test_c5_8192_fstep_one_round():
+    """C5's shard (int16, 4 agents) through the one-round shape, TimeLimit 12."""
+    run_full(lambda n: c5(n, max_steps=12), 8192, 30, seed0=5 * 8192, launch={"fstep": 1, "fs_tick": 8},
+             min_resets=2 * 8192, after=_fstep)

@@ -250,3 +250,33 @@ def test_zombie_view_after_life_poke_and_slot_reuse():
     assert z.life <= 0 and not z.alive_in_world
     assert all(t is not z for t in env.game.world.things.values())
     assert isinstance(z.position, tuple) and z.weapon is not None
+
+
+def test_objects_held_across_reset_keep_their_values():
+    """Objects of an ending episode are out of the world after reset() and keep the values they had when
+    it ended (game.py:151-169 builds a new World and new players), whatever they last showed when read;
+    the map's obstacles stay shared (game.py:154-155)."""
+    random.seed(5)
+    env = MultiagentZombsoleEnv("extermination", [], "bridge", ["0", "1"], initial_zombies=6, minimum_zombies=0)
+    env.reset()
+    act = {"0": {"action_type": "attack_closest"}, "1": {"action_type": "move", "parameter": [1, 0]}}
+    env.step(act)
+    old_agents = list(env.game.agents)
+    old_zombies = [t for t in env.game.world.things.values() if isinstance(t, Zombie)]
+    [(z.position, z.life) for z in old_zombies + old_agents]  # read once: the views' cached rows
+    for _ in range(4):  # further steps the held objects are not read in
+        env.step(act)
+    st = env.game.engine.get_state(0)
+    truth = []
+    for v in old_zombies + old_agents:
+        r = st.ent[v._slot]
+        truth.append((int(r[2]), int(r[3]), int(r[4])) if int(r[7]) == v._serial else None)
+    wall = env.game.map.things[0]
+    env.reset()
+    for v, tr in zip(old_zombies + old_agents, truth):
+        if tr is not None:  # still in the world when the episode ended
+            assert (v.position[0], v.position[1], v.life) == tr
+    assert all(a is not b for a, b in zip(old_agents, env.game.agents))
+    new_things = list(env.game.world.things.values())
+    assert all(all(v is not n for n in new_things) for v in old_zombies + old_agents)
+    assert wall is env.game.map.things[0]
