@@ -113,7 +113,9 @@ extern "C" {
                               * stops World.step; without the flag kinds >= 7 are unknown (idle) */
 #define ZS_FLAG_DEATH_LOG 4u /* keep, per env, the things its last step's clean_dead_things removed, in
                               * removal order (zs_death_log; the drop-in views' decoration order and
-                              * the final values of a removed zombie whose slot a respawn reuses) */
+                              * the final values of a removed zombie whose slot a respawn reuses), and
+                              * the actions it executed, in execution order (zs_action_log; the drop-in
+                              * views' World.events) */
 
 /* ---- range flags (zs_overflow) -------------------------------------------
  * The reference's obstacle life is an unbounded Python int that carries over resets
@@ -304,6 +306,13 @@ int zs_debug_lists(zs_handle* h, int32_t out[4], void* stream);
  * removal), at most cap entries into out_host; *n_out = how many the step removed.  Needs
  * ZS_FLAG_DEATH_LOG; an env reset by that step reports none. */
 int zs_death_log(zs_handle* h, int32_t env, int32_t* out_host, int32_t cap, int32_t* n_out, void* stream);
+/* The actions env's last zs_step executed, in execution order (World.step's shuffled action list,
+ * core.py:76,103-119; replaces reading World.events, core.py:68-70, whose messages the drop-in views
+ * derive from it): per action {slot | kind << 8, target} with kind 1 move (target: destination
+ * x | y << 16), 2 attack, 3 heal (target: an entity slot, or -1 - obstacle index in map order); at most
+ * cap entries into out_host (2 int32 each); *n_out = how many.  Needs ZS_FLAG_DEATH_LOG; an env reset by
+ * that step, or stopped by a debug raise, reports none. */
+int zs_action_log(zs_handle* h, int32_t env, int32_t* out_host, int32_t cap, int32_t* n_out, void* stream);
 /* Diagnostic builds compiled with -DZS_STAMPS only (the product .so returns ZS_ESTATE):
  * per-phase k_tick cycle sums / maxima over all workgroup launches since the last call. */
 int zs_debug_stamps(zs_handle* h, uint64_t* sum_out, uint64_t* max_out, int32_t n);

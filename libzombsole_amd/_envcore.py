@@ -76,13 +76,15 @@ class EnvCore(object):
         rows = [(ACT_RAISE, 0, 0) if isinstance(t, ActionError) else t for t in triples]
         self._host_actions[0, :len(rows)] = np.asarray(rows, dtype=np.int32).reshape(-1, 3)
         eng.actions.copy_(self.torch.from_numpy(self._host_actions))
+        pre = self.game._state()  # the world the step starts from (its World.events are derived from it)
         eng.load_python_random(0)
         try:
             eng.step()
         finally:
             eng.store_python_random(0)
             self.game.invalidate()
-        self.game.after_step()
+        # a debug raise stops World.step inside get_actions: no action ran, nothing died (core.py:96-99)
+        self.game.after_step(None if raising is not None else pre)
         if raising is not None:
             raise raising.args[0]
         obs = eng.obs[0].cpu().numpy()

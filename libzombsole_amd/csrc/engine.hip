@@ -698,6 +698,8 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
     if (d.flags & ZS_FLAG_DEATH_LOG) {
         TRY(dalloc(h, &d.dlog, (size_t)N * E * 5));
         TRY(dalloc(h, &d.dlog_n, N));
+        TRY(dalloc(h, &d.alog, (size_t)N * E * 2));
+        TRY(dalloc(h, &d.alog_n, N));
     }
     TRY(dalloc(h, &d.resp_count, 1));
     {
@@ -1583,6 +1585,29 @@ extern "C" int zs_describe(zs_handle* h, char* buf, int32_t len) {
              h->fstep ? 0 : h->reset_side,
              h->reset_lds, d.defer_respawn ? "k_respawn" : "tick", h->fused ? ZS_FUSED_WAVES : h->tick_waves, d.rw_step,
              d.par_exec);
+    return ZS_OK;
+}
+
+// The actions env's last step executed, in execution order (the shuffled action list of World.step,
+// core.py:76,103-119): per action {slot | kind << 8, target}, kind 1 move (target: the destination,
+// x | y << 16), 2 attack, 3 heal (target: an entity slot, or -1 - obstacle index).  Needs ZS_FLAG_DEATH_LOG.
+extern "C" int zs_action_log(zs_handle* h, int32_t env, int32_t* out_host, int32_t cap, int32_t* n_out, void* stream) {
+    if (!h || !n_out || (cap > 0 && !out_host)) return fail(ZS_EINVAL, "null argument");
+    if (!h->d.alog) return fail(ZS_EINVAL, "the handle was created without ZS_FLAG_DEATH_LOG");
+    if (env < 0 || env >= h->d.N) return fail(ZS_EINVAL, "env out of range");
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(hipSetDevice(h->device));
+    int32_t n = 0;
+    HIPCHK(hipMemcpyAsync(&n, h->d.alog_n + env, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    n = std::max(0, std::min(n, h->d.E));
+    const int k = std::min(n, std::max(0, (int)cap));
+    if (k > 0) {
+        HIPCHK(hipMemcpyAsync(out_host, h->d.alog + (size_t)env * h->d.E * 2, sizeof(int32_t) * 2 * k,
+                              hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+    }
+    *n_out = n;
     return ZS_OK;
 }
 

@@ -183,6 +183,11 @@ struct Dev {
     // each in removal order ([N][E][5]), and their count ([N]); null = not kept
     int32_t* dlog;
     int32_t* dlog_n;
+    // with the death log: the actions the last tick executed, in execution order (the shuffled list of
+    // core.py:76), {slot | kind << 8, target} each ([N][E][2]), and their count ([N]); the drop-in views
+    // derive World.events from it (core.py:68-70, 103-119)
+    int32_t* alog;
+    int32_t* alog_n;
     // sticky range flags of the handle (zs_overflow): ZS_OVF_INT16 once an obstacle's life went below
     // the int16 range (int16 observations then saturate it), ZS_OVF_INT32 once one saturated at
     // ZS_HP_FLOOR (the engine then differs from the reference's unbounded int)

@@ -256,7 +256,8 @@ __device__ __forceinline__ void reset_env_wave(const Dev& d, const ResetLds& L, 
         // reset and clears the flag (it never reads this env's state).  Mask mode: done now.
         if (!list_mode) d.scal[S_NEEDRESET * N + e] = 0;
         d.rngst[e] = stf;
-        if (d.dlog_n) d.dlog_n[e] = 0;  // a reset removes nothing (ZS_FLAG_DEATH_LOG)
+        if (d.dlog_n) d.dlog_n[e] = 0;  // a reset removes nothing and executes nothing (ZS_FLAG_DEATH_LOG)
+        if (d.alog_n) d.alog_n[e] = 0;
     }
     wave_sync();
     RST(7);

@@ -1098,6 +1098,7 @@ __device__ __forceinline__ void env_step_leader(const Dev& d, Grp& c, const int3
             c.fin = 0;
             c.respawn = 0;
             MISC(c, MISC_NMOVED) = -1;  // no cleanup, no second leader part
+            if (d.alog) d.alog_n[c.e] = 0;
             return;
         }
         if (LK(c, s) == K_DEFER) {
@@ -1116,6 +1117,15 @@ __device__ __forceinline__ void env_step_leader(const Dev& d, Grp& c, const int3
         LPE(c, j) = tmp;
     }
     SUB(1);
+    if (d.alog) {  // the executed actions in execution order (drop-in views)
+        int32_t* al = d.alog + (size_t)c.e * d.E * 2;
+        for (int k = 0; k < nact; k++) {
+            const int s = LPE(c, k);
+            al[2 * k] = s | (LK(c, s) << 8);
+            al[2 * k + 1] = LT(c, s);
+        }
+        d.alog_n[c.e] = nact;
+    }
     // execute_actions (core.py:103-119).  The next action's actor, kind, target and position are read
     // ahead: nothing this action does changes them (every actor acts once, and only its own action moves it).
     int nmoved = 0;
@@ -1838,6 +1848,15 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
             int pos = 0, odirty = 0;
             grp_shuffle<G>(d, c, nact, pos);
             grp_execute<G>(d, c, nact, pos, nm0, odirty);
+            if (d.alog) {  // the executed actions in execution order (drop-in views)
+                int32_t* al = d.alog + (size_t)e * d.E * 2;
+                for (int k = j; k < nact; k += G) {
+                    const int s = LPE(c, k);
+                    al[2 * k] = s | (LK(c, s) << 8);
+                    al[2 * k + 1] = LT(c, s);
+                }
+                if (j == 0) d.alog_n[e] = nact;
+            }
             for (int q = j; q < nm0; q += G) LR(c, LM(c, q)) = 255;  // re-inserted at the end of the dict
             if (odirty && j == 0) MISC(c, MISC_ODIRTY) = 1;
             c.wpos = pos;

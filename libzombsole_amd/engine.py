@@ -14,7 +14,7 @@ from . import _abi
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_build", "libzombsole_mi355x.so")
 SYMBOLS = ["zs_last_error", "zs_create", "zs_destroy", "zs_obs_shape", "zs_seed", "zs_reset", "zs_step", "zs_observe",
            "zs_gen_actions", "zs_step_graph", "zs_step_graph_n", "zs_state_size", "zs_get_state", "zs_set_state", "zs_get_rng", "zs_set_rng", "zs_overflow", "zs_profile", "zs_profile_read", "zs_describe",
-           "zs_debug_stamps", "zs_debug_stamps_wg", "zs_debug_timeline", "zs_debug_lists", "zs_death_log"]
+           "zs_debug_stamps", "zs_debug_stamps_wg", "zs_debug_timeline", "zs_debug_lists", "zs_death_log", "zs_action_log"]
 
 _lib = None
 
@@ -62,6 +62,7 @@ def load_library(path=None):
     L.zs_describe.argtypes = [vp, C.c_char_p, i32]
     L.zs_debug_lists.argtypes = [vp, C.POINTER(i32), vp]
     L.zs_death_log.argtypes = [vp, i32, C.POINTER(i32), i32, C.POINTER(i32), vp]
+    L.zs_action_log.argtypes = [vp, i32, C.POINTER(i32), i32, C.POINTER(i32), vp]
     L.zs_debug_timeline.argtypes = [vp, vp, i32]
     L.zs_debug_stamps_wg.argtypes = [vp, vp, i32, i32]
     for s in SYMBOLS:
@@ -286,6 +287,18 @@ class Engine(object):
         if rc:
             _raise(self.L, rc, "zs_death_log")
         return [tuple(int(v) for v in out[5 * k:5 * k + 5]) for k in range(min(n.value, self.E))]
+
+    def action_log(self, env):
+        """The actions env's last step executed, in execution order (core.py:76,103-119): a list of
+        (slot, kind, target), kind 1 move (target: destination x | y << 16), 2 attack, 3 heal (target: an
+        entity slot, or -1 - obstacle index).  Needs a config with FLAG_DEATH_LOG."""
+        out = (C.c_int32 * (2 * max(1, self.E)))()
+        n = C.c_int32(0)
+        rc = self.L.zs_action_log(self.h, int(env), out, int(self.E), C.byref(n), self._stream())
+        if rc:
+            _raise(self.L, rc, "zs_action_log")
+        return [(int(out[2 * k]) & 0xff, (int(out[2 * k]) >> 8) & 0xff, int(out[2 * k + 1]))
+                for k in range(min(n.value, self.E))]
 
     def get_state(self, env):
         buf = np.zeros(self.state_words, dtype=np.int32)

@@ -9,7 +9,7 @@ re-evaluate the reference's predicates (`rules/*.py`) on that state so that
 """
 from . import _abi
 from .maps import Map, load_map  # noqa: F401  (reference: zombsole.game.Map)
-from .things import OBSTACLE_CLASSES, Agent, DeadBody, ObjectiveLocation, Player, Zombie
+from .things import OBSTACLE_CLASSES, Agent, DeadBody, ObjectiveLocation, Player, Zombie, weapon_for_code, weapon_r2
 
 BOT_NAMES = {v: k for k, v in _abi._BOTS.items()}
 
@@ -44,7 +44,9 @@ class WorldView(object):
         self._game = game
         self.size = tuple(game.map.size)
         self.debug = game.debug
-        self.events = []  # the reference's event log is not kept by the engine
+        # World.event's log (core.py:68-70): (t, thing, message) per idle actor, executed action and death,
+        # appended by GameView.after_step from the engine's action and death logs
+        self.events = []
 
     t = property(lambda s: s._game._state().t)
     deaths = property(lambda s: s._game._state().deaths)
@@ -258,16 +260,98 @@ class GameView(object):
             self._views[A + j] = p
         self.world = WorldView(self)
 
-    def after_step(self):
+    def after_step(self, pre=None):
         """Book-keeping of a step the env took (EnvCore.tick): the bodies its cleanup left, in the
-        order it removed the things (core.py:121-128), and the final values of the removed things
-        into their views (a removed zombie's slot may be reused by the same step's respawn)."""
-        for slot, serial, x, y, life in self.engine.death_log(self.env):
+        order it removed the things (core.py:121-128), the final values of the removed things into
+        their views (a removed zombie's slot may be reused by the same step's respawn), and, given the
+        state record from before the step (`pre`), the step's World.events."""
+        actors = {}
+        if pre is not None:  # the objects in the world while the step ran
+            for slot in pre.order[:pre.n_order]:
+                slot = int(slot)
+                v = self._views.get(slot)
+                if v is None or v._serial != int(pre.ent[slot][7]):
+                    v = Zombie(self, slot, row=pre.ent[slot])
+                    self._views[slot] = v
+                actors[slot] = v
+        deaths = self.engine.death_log(self.env)
+        for slot, serial, x, y, life in deaths:
             v = self._views.get(slot)
             if v is not None and v._serial == serial:
                 v._finalize(x, y, life)
             # things.py:64,118 (agents and bots always have a view; a zombie slot may have none)
             self._deco[(x, y)] = ("dead " + v.name) if isinstance(v, Player) else "zombie remains"
+        if pre is not None:
+            self._log_events(pre, actors, deaths)
+
+    def _log_events(self, pre, actors, deaths):
+        """The step's World.event records (core.py:68-70) in the reference's order: 'idle' for every actor
+        whose next_step gave no action, in dict order (core.py:80-101); each executed action's result in
+        execution order (core.py:103-119, the messages of thing_move / thing_attack / thing_heal,
+        core.py:140-202), with positions and occupancy followed through the step's moves; 'died' for every
+        thing the cleanup removed, obstacles first in map order, then the others in dict order
+        (core.py:121-138).  The actions and their order come from the engine (zs_action_log); the
+        messages are their outcomes against the state from before the step."""
+        t = pre.t + 1
+        W, H = self.world.size
+        alog = self.engine.action_log(self.env)
+        ev = []
+        acted = set(a[0] for a in alog)
+        for slot in pre.order[:pre.n_order]:
+            if int(slot) not in acted:
+                ev.append((t, actors[int(slot)], u"idle"))
+        pos, occ = {}, {}
+        for i, ob in enumerate(self._obstacles):
+            if pre.obst_present[i]:
+                occ[ob.position] = ob
+        for slot, v in actors.items():
+            r = pre.ent[slot]
+            pos[slot] = (int(r[2]), int(r[3]))
+            occ[pos[slot]] = v
+
+        def target(tgt):
+            return (self._obstacles[-1 - tgt], self._obstacles[-1 - tgt].position) if tgt < 0 else (actors[tgt], pos[tgt])
+
+        for slot, kind, tgt in alog:
+            me, (x, y) = actors[slot], pos[slot]
+            if kind == 1:  # thing_move (core.py:140-166)
+                dx, dy = tgt & 0xffff, tgt >> 16
+                dx = dx - 0x10000 if dx >= 0x8000 else dx
+                if 0 <= dx < W and 0 <= dy < H:
+                    if (dx, dy) in occ:
+                        msg = u"hit %s with his head" % occ[(dx, dy)].name
+                    elif (dx - x) ** 2 + (dy - y) ** 2 > 1:
+                        msg = u"tried to walk too fast, but physics forbade it"
+                    else:
+                        del occ[(x, y)]
+                        occ[(dx, dy)] = me
+                        pos[slot] = (dx, dy)
+                        msg = u"moved to " + str((dx, dy))
+                else:
+                    msg = u"Tried to move out of bounds to %s" % str((dx, dy))
+            elif kind == 2:  # thing_attack (core.py:168-184)
+                tg, (tx, ty) = target(tgt)
+                code = int(pre.ent[slot][5])
+                if (tx - x) ** 2 + (ty - y) ** 2 > weapon_r2(code):
+                    msg = u"tried to attack %s, but it is too far for a %s" % (tg.name, weapon_for_code(code).name)
+                else:
+                    msg = u"injured %s with a %s" % (tg.name, weapon_for_code(code).name)
+            else:  # thing_heal (core.py:186-202), HEALING_RANGE = 3
+                tg, (tx, ty) = target(tgt)
+                if (tx - x) ** 2 + (ty - y) ** 2 > 9:
+                    msg = u"tried to heal %s, but it is too far away" % tg.name
+                else:
+                    msg = u"healed " + tg.name
+            ev.append((t, me, msg))
+        post = self._state()
+        for i, ob in enumerate(self._obstacles):
+            if pre.obst_present[i] and not post.obst_present[i]:
+                ev.append((t, ob, u"died"))
+        for slot, serial, x, y, life in deaths:
+            v = actors.get(slot)
+            if v is not None and v._serial == serial:
+                ev.append((t, v, u"died"))
+        self.world.events.extend(ev)
 
     def _entity(self, slot):
         v = self._views.get(slot)

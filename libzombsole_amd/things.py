@@ -131,10 +131,10 @@ class Wall(_ObstacleView, Thing):
 class _EntityView(object):
     """An agent / bot / zombie slot of the engine env (entity record of include/zombsole_mi355x.h)."""
 
-    def __init__(self, game, slot):
+    def __init__(self, game, slot, row=None):
         self._game = game
         self._slot = slot
-        r = game._state().ent[slot]
+        r = game._state().ent[slot] if row is None else row
         self._serial = int(r[7])
         self._last = [int(v) for v in r]  # always holds a row of this thing (see _finalize)
         self._gone = False
@@ -187,6 +187,12 @@ class _EntityView(object):
     @property
     def alive_in_world(self):
         return bool(self._row()[1])
+
+
+def weapon_r2(code):
+    """The largest squared distance a weapon's max_range reaches (weapons.py:18-25; `distance > max_range`
+    in core.py:177 on integer positions)."""
+    return {_abi.WEAPON_GUN: 36, _abi.WEAPON_RIFLE: 100, _abi.WEAPON_SHOTGUN: 9}.get(int(code), 2)
 
 
 class Zombie(_EntityView, FightingThing):

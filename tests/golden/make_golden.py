@@ -143,6 +143,23 @@ CONFIGS = [
      dict(rules_name="safehouse", player_names=["terminator", "sniper"], map_name="fort", agent_id=0,
           initial_zombies=30, minimum_zombies=30, observation_scope="surroundings:11",
           observation_position_encoding="channels", agent_weapon="shotgun"), [33], 150, 1, 60, {"views": True}),
+    # World.events (core.py:68-70): idle actors, every executed action's message (moves out of bounds, into
+    # things, too fast; attacks and heals in and out of range) and deaths, per step.  The rich stream gives
+    # agents moves of any length, attacks and heals at any cell; the bots of the single-agent config draw in
+    # their decisions (the leader's serial execution), the fort config crowds 40 zombies around 8 agents
+    # (the lanes' chunked execution)
+    ("events_multi_bridge_a4_rich", "multi", "rich",
+     dict(rules_name="extermination", player_names=["terminator"], map_name="bridge",
+          agent_ids=["0", "1", "2", "3"], initial_zombies=15, minimum_zombies=10,
+          agent_weapons=["shotgun", "rifle", "knife", "gun"]), [41, 42], 100, 1, 0, {"events": True}),
+    ("events_single_boxed_bots_rich", "single", "rich",
+     dict(rules_name="extermination", player_names=["terminator", "sniper", "troll", "hamster"],
+          map_name="boxed", agent_id=0, initial_zombies=2, minimum_zombies=2, observation_scope="world",
+          observation_position_encoding="simple", agent_weapon="axe"), [43, 44], 120, 1, 40, {"events": True}),
+    ("events_multi_fort_a8_z40", "multi", "discrete",
+     dict(rules_name="extermination", player_names=[], map_name="fort",
+          agent_ids=[str(i) for i in range(8)], initial_zombies=40, minimum_zombies=20), [45], 60, 1, 0,
+     {"events": True}),
 ]
 
 

@@ -94,6 +94,32 @@ class ViewTracker(object):
             del self.held[k]
 
 
+def thing_kind(K, t):
+    """The family of an event's thing: zombie, agent, player (a bot), wall, box."""
+    for cls, name in ((K.Zombie, "zombie"), (K.Agent, "agent"), (K.Player, "player"), (K.Wall, "wall"),
+                      (K.Box, "box")):
+        if isinstance(t, cls):
+            return name
+    return type(t).__name__
+
+
+class EventTracker(object):
+    """extras["events"]: after a step, the World.event records it appended (core.py:68-70), each
+    [t, the thing's family, its name, the message]; a reset starts a new World (and log)."""
+
+    def __init__(self, K):
+        self.K = K
+        self.n = 0
+
+    def new_world(self, game):
+        self.n = len(game.world.events)
+
+    def record(self, game, rec):
+        evs = game.world.events
+        rec["events"] = [[int(t), thing_kind(self.K, th), getattr(th, "name", ""), msg] for t, th, msg in evs[self.n:]]
+        self.n = len(evs)
+
+
 def obs_bytes_single(obs):
     return np.ascontiguousarray(obs, dtype="<i4").tobytes()
 
@@ -132,6 +158,7 @@ def run_config(cfg, K):
             obstacles[i].life = life
         recs = []
         views = ViewTracker(K) if extras.get("views") else None
+        events = EventTracker(K) if extras.get("events") else None
         random.seed(seed)
         obs, _ = env.reset()
         need_reset = False
@@ -143,6 +170,8 @@ def run_config(cfg, K):
                     obs, _ = env.reset()
                 if views:
                     views.new_world()
+                if events:
+                    events.new_world(game)
                 rec["kind"] = "reset"
                 need_reset = False
                 elapsed = 0
@@ -209,6 +238,8 @@ def run_config(cfg, K):
             rec["state"] = canonical_state(game, obstacles, K)
             if views:
                 views.record(game, rec, rec["kind"] == "step")
+            if events and rec["kind"] == "step":
+                events.record(game, rec)
             recs.append(rec)
         out.append({"seed": seed, "calls": recs})
     res = {"name": name, "surface": surface, "stream": stream, "kwargs": dict(cfg[3]),
