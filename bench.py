@@ -22,6 +22,8 @@ import os
 import sys
 import time
 
+import libzombsole_amd  # noqa: F401  (HIP runtime settings, before the first HIP call)
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 

@@ -8,6 +8,8 @@ for p in (ROOT, os.path.join(ROOT, "tests")):
     if p not in sys.path:
         sys.path.insert(0, p)
 
+import libzombsole_amd  # noqa: E402,F401  (its HIP runtime settings, before any test's first HIP call)
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); run with -m gpu")
