@@ -421,6 +421,9 @@ __device__ __forceinline__ void respawn_env_wave(const Dev& d, const ResetLds& L
     int nz = 0;
     for (int b = Z0; b < E; b += 64) nz += __popcll(__ballot(b + lane < E && L.lpres[b + lane]));
     const int k = max(d.minimum_zombies - nz, 0);
+#ifdef ZS_STAMPS
+    if (lane == 0 && k > 0 && blockIdx.x < ZS_STAMP_WGS) g_stamp_wg[blockIdx.x * ZS_NPHASE + 19] += 1ull << 32;  // placing ones
+#endif
     int taken = 0;
     for (int b = Z0; b < E && taken < k; b += 64) {
         const int s = b + lane;

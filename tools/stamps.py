@@ -68,8 +68,8 @@ def main():
             else:
                 print("   %-10s mean %9.0f cyc   max %9d cyc" % (name, ssum[k] / (wgs * steps), smax[k]))
         if ssum[19]:  # k_respawn (its phases share the R: slots; resets are few where respawns are many)
-            nr = float(ssum[19])
-            print("respawns per step: %.1f" % (nr / steps))
+            nr = float(int(ssum[19]) & 0xffffffff)
+            print("respawns per step: %.1f (with zombies to place: %.1f)" % (nr / steps, (int(ssum[19]) >> 32) / steps))
             for i, name in enumerate(["loads+rows", "occupancy+rng", "lives draws", "spawn", "finish+out"]):
                 print("   P:%-14s per-respawn %9.0f cyc" % (name, ssum[13 + i] / nr))
         desc = eng.describe()
