@@ -174,7 +174,9 @@ typedef struct zs_launch {
     int32_t fs_tick;         /* k_fstep's tick waves per workgroup (4 or 6)                            */
     int32_t tick_early;      /* k_tick (5 waves per SIMD) loads the RNG window's first words with its
                               * first load round, overlapping their round trip with the decisions      */
-    int32_t reserved[7];
+    int32_t pol_tick;        /* zs_step_graph with the side-stream reset: 1 = the on-device policy inside
+                              * the tick launch instead of its own launch ahead of it                  */
+    int32_t reserved[6];
 } zs_launch;
 
 typedef struct zs_config {

@@ -1256,7 +1256,7 @@ extern "C" int zs_step(zs_handle* h, const int32_t* actions_dev, void* obs_dev, 
         // starts the policy first: C3 173 M env-steps/s, against 167 with the reset launch captured first
         // and 169 with the policy inside the step launch); otherwise inside the step launch (no launch,
         // no gap: 8 192 envs 110 -> 117 M env-steps/s)
-        if (h->graph_pol && side) {
+        if (h->graph_pol && side && h->ov.pol_tick <= 0) {
             const int n = h->d.N * h->d.A;
             hipLaunchKernelGGL(k_gen_actions_ctr, dim3((n + 255) / 256), dim3(256), 0, s, h->d,
                                (const uint64_t*)h->d_gstep, h->graph_pol, (int32_t*)actions_dev);
@@ -1273,7 +1273,7 @@ extern "C" int zs_step(zs_handle* h, const int32_t* actions_dev, void* obs_dev, 
             d.pol_step = st;
         }
         ~PolScope() { d.pol_n = 0, d.pol_step = nullptr; }
-    } pol(h->d, side ? 0 : h->graph_pol, side ? nullptr : h->d_gstep);
+    } pol(h->d, side && h->ov.pol_tick <= 0 ? 0 : h->graph_pol, side && h->ov.pol_tick <= 0 ? nullptr : h->d_gstep);
     // 2) tick every other env; envs that end now are queued on list[q] for the next call.
     // Work-list counters: between calls the list the next step appends to (list[1 - rpar]) and the
     // deferred-respawn list are empty.  This step appends to list[q] and resp_list, drains list[p] and
