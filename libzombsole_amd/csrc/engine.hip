@@ -749,7 +749,10 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
             int wgs = std::max(1, std::min(ts == 8 ? 2 : 4, (int)(160 * 1024 / lb)));
             if (h->ov.obs_wgs > 0) wgs = std::min(32, (int)h->ov.obs_wgs);
             const bool forced = h->ov.obs_lds > 0;
-            const bool pays = ts < 8 || (long)d.N >= 24L * 256 * 2 * 4;
+            // int64 from 48 envs per CU (C3 on one MI355X, k_obs_ring against k_obs_pipe: 12 288 envs 129.5 against
+            // 117.1 M env-steps/s, 16 384 123.7 / 121.4, 24 576 140.1 / 134.8, 32 768 153.6 / 147.1; 8 192 138.9
+            // against 143.9, 10 240 (fused) 150.9 / 154.9; profiles/r05c_mid_sizes.log)
+            const bool pays = ts < 8 || (long)d.N >= 48L * 256;
             if (lb <= 64 * 1024 && (pays || forced)) {
                 h->obs_lds = 1;
                 h->obs_lds_bytes = lb;
@@ -841,7 +844,21 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
     {
         const int obs_b = d.fobs ? d.obsl.bytes + 4 * d.obs_stat : 0;
         TRY(choose_layout(h, cfg->lanes_per_env, true, obs_b));
-        h->fused = h->ov.fused ? h->ov.fused > 0 : h->resident >= h->want;
+        // 8 lanes per env when 16 would take the fused launch past one resident round and 8 take fewer rounds
+        // (C3 on one MI355X: 16 384 envs, G = 16 two rounds 133.6 M env-steps/s, G = 8 one round 148.8 M;
+        // 24 576 envs fused, G = 16 140.3 M, G = 8 143.5 M; 8 192 envs stay at G = 16, one round either way;
+        // profiles/r05c_mid_sizes.log)
+        if (cfg->lanes_per_env <= 0 && h->G == 16 && d.E <= 16 && h->resident < h->want) {
+            const int r16 = (h->want + h->resident - 1) / h->resident;
+            TRY(choose_layout(h, 8, true, obs_b));
+            if ((h->want + h->resident - 1) / h->resident >= r16) TRY(choose_layout(h, 16, true, obs_b));
+        }
+        // up to two resident rounds the fused launch still wins: the side-stream reset work outlasts the tick
+        // (C3 16 384 envs: k_tick 38 us, k_reset 43 us) and the fused launch hides it under the ticks (C3 on one
+        // MI355X, fused against side stream: 12 288 envs 137.2 / 129.5 M, 16 384 133.1 / 123.7, 32 768 155.3 /
+        // 153.6, 49 152 165.1 / 165.5, 65 536 172.5 / 182.0; C5 16 384 153.7 / 148.3, 32 768 186.6 / 199.3;
+        // profiles/r05c_mid_sizes.log)
+        h->fused = h->ov.fused ? h->ov.fused > 0 : 2 * h->resident >= h->want;
         // the fused launch loads its window's first 4G words with its first load round (zs_tick.hpp EARLY): a
         // window that size costs no round trip, and the lanes' draws then reload it less often
         if (h->fused && h->ov.rw_need <= 0) d.rw_step = std::min(d.rw_cap, std::max(d.rw_step, 4 * h->G));

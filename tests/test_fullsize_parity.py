@@ -120,6 +120,26 @@ def test_c3_65536_graph():
     run_full(c3, 65536, 40)
 
 
+def _expect_launch(step_kernel, obs_kernel):
+    def check(eng):
+        d = eng.describe()
+        assert (d["step_kernel"], d["obs_kernel"]) == (step_kernel, obs_kernel), d
+    return check
+
+
+@pytest.mark.parametrize("n", [12288, 16384, 32768])
+def test_c3_strong_scaling_shards(n):
+    """The C3 shards of a strong-scaling run at N = 4 and 2 (16 384, 32 768 envs per GPU) and the ring's
+    lower bound (12 288: 48 envs per CU): the step launch with the reset work inside it over up to two
+    resident rounds, and k_obs_ring."""
+    run_full(c3, n, 40, seed0=3 * n, after=_expect_launch("k_step", "k_obs_ring"))
+
+
+def test_c5_16384_int16_fused_two_rounds():
+    """C5 at 16 384 envs: the fused step launch over two resident rounds, int16 ring."""
+    run_full(c5, 16384, 40, seed0=7, after=_expect_launch("k_step", "k_obs_ring"))
+
+
 def test_c3_65536_truncation_waves():
     """TimeLimit 16: every env truncates at steps 16 and 33 -> 65 536-env autoreset waves (k_reset list
     mode grid-striding far past 2 048 pending envs), plus a masked reset of 21 846 envs before step 1."""
