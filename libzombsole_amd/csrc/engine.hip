@@ -248,6 +248,7 @@ struct zs_handle {
     int obs_ring = 0;      // k_obs_ring: encoder and writer waves through an LDS ring (zs_launch.obs_ring)
     size_t obs_ring_bytes = 0;
     int obs_bring = 0;     // k_obs_bring: its unit slots (0: not used)
+    int obs_bring_pad = 0; // ... as k_obs_pbring (padded-table encoders)
     size_t obs_bring_bytes = 0;
     size_t obs_lds_bytes = 0;
     int obs_patch = 0;     // k_obs_lds's walk with the padded-table encoder (k_obs_patch, zs_launch.obs_patch)
@@ -820,6 +821,17 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
                 h->obs_bring = us;
                 h->obs_bring_bytes = bb;
             }
+            // k_obs_pbring: the things written over the windows instead of looked up per cell (C4 on one
+            // MI355X: observations 157.7 -> 151.1 us, 53.3 -> 54.0 M env-steps/s; profiles/r05f_ab_pbring.log);
+            // zs_launch.obs_ring_patch = -1 keeps k_obs_bring
+            const int usp = pbring_slots(d.DW, d.OW, ts, nobs, 160 * 1024);
+            const size_t pbb = (size_t)pbring_fixed_bytes(d.DW, d.OW) + (size_t)usp * bring_unit_bytes(ts, nobs);
+            if (h->obs_bring && usp >= 2 && h->ov.obs_ring_patch >= 0 &&
+                obs_attr(d.obs_dtype, OBSK_BRING, nobs, 1, (int)pbb) == hipSuccess) {
+                h->obs_bring = usp;
+                h->obs_bring_bytes = pbb;
+                h->obs_bring_pad = 1;
+            }
         }
         // with the store-stream kernel available the observations are its job (measured faster than
         // writing them from the tick workgroups at both 8192 and 65536 envs); zs_launch.fobs forces them
@@ -1058,6 +1070,7 @@ static int launch_obs(zs_handle* h, void* obs, const uint8_t* mask, hipStream_t 
         const int ts = d.obs_dtype == ZS_DTYPE_I64 ? 8 : d.obs_dtype == ZS_DTYPE_I32 ? 4 : 2;
         const int pair = ring_pair(ts, h->obs_gather);
         o.kind = OBSK_BRING;
+        o.patched = h->obs_bring_pad;
         o.nobs = h->obs_gather;
         o.grid = (unsigned)std::min((env1 - env0 + pair - 1) / pair, 256);
         o.block = 64 * (BRING_ENC + BRING_WRT);
@@ -1593,7 +1606,7 @@ extern "C" int zs_describe(zs_handle* h, char* buf, int32_t len) {
     const Dev& d = h->d;
     const char* obs_kernel = h->fstep ? "k_fstep" : d.fobs ? "step launch"
                              : h->obs_pipe ? (h->obs_ring ? "k_obs_ring" : h->obs_patch ? "k_obs_patch" : h->obs_lds ? "k_obs_lds" : "k_obs_pipe")
-                             : h->obs_bring ? "k_obs_bring" : h->obs_gather ? "k_obs_gather" : "k_obs";
+                             : h->obs_bring ? (h->obs_bring_pad ? "k_obs_pbring" : "k_obs_bring") : h->obs_gather ? "k_obs_gather" : "k_obs";
     snprintf(buf, (size_t)len,
              "{\"envs\": %d, \"entities\": %d, \"lanes_per_env\": %d, \"step_kernel\": \"%s\", \"step_lds\": %zu, "
              "\"step_wgs_per_cu\": %d, \"rng_window\": %d, \"obs_kernel\": \"%s\", \"reset_side_stream\": %d, "

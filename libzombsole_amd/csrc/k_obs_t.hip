@@ -26,7 +26,10 @@ static void launch_nb(const ObsLaunch& o, hipStream_t s, const Dev& d) {
         if (o.patched) hipLaunchKernelGGL((k_obs_ring<TT, NB, true>), g, b, o.lds, s, d, out, o.L, o.env0, o.env1);
         else hipLaunchKernelGGL((k_obs_ring<TT, NB, false>), g, b, o.lds, s, d, out, o.L, o.env0, o.env1);
         break;
-    case OBSK_BRING: hipLaunchKernelGGL((k_obs_bring<TT, NB>), g, b, o.lds, s, d, out, o.L, o.env0, o.env1, o.us); break;
+    case OBSK_BRING:
+        if (o.patched) hipLaunchKernelGGL((k_obs_pbring<TT, NB>), g, b, o.lds, s, d, out, o.env0, o.env1, o.us);
+        else hipLaunchKernelGGL((k_obs_bring<TT, NB>), g, b, o.lds, s, d, out, o.L, o.env0, o.env1, o.us);
+        break;
     case OBSK_PATCH: hipLaunchKernelGGL((k_obs_patch<TT, NB>), g, b, o.lds, s, d, out, o.env0, o.env1); break;
     case OBSK_LDS: hipLaunchKernelGGL((k_obs_lds<TT, NB>), g, b, o.lds, s, d, out, o.L, o.env0, o.env1); break;
     case OBSK_PIPE: hipLaunchKernelGGL((k_obs_pipe<TT, NB>), g, b, o.lds, s, d, out, o.L, o.env0, o.env1); break;
@@ -51,7 +54,7 @@ hipError_t ZS_OBS_FN(obs_lds_attr)(int kind, int nobs, int patched, int bytes) {
     if (kind == OBSK_PATCH) {
         fn = ZS_FN3(k_obs_patch);
     } else if (kind == OBSK_BRING) {
-        fn = ZS_FN3(k_obs_bring);
+        fn = patched ? ZS_FN3(k_obs_pbring) : ZS_FN3(k_obs_bring);
     } else if (kind == OBSK_RING) {
         if (patched)
             fn = nobs == 1 ? (const void*)k_obs_ring<TT, 1, true>

@@ -1652,3 +1652,201 @@ __global__ void __launch_bounds__(64 * (BRING_ENC + BRING_WRT), 1) k_obs_bring(D
         if (t + BRING_ENC < count) step(t + BRING_ENC, rb, qb, ra, qa);
     }
 }
+
+// ---------------------------------------------------------------------------
+// k_obs_pbring: k_obs_bring with the things written over the window afterwards instead of looked up per
+// cell.  k_obs_bring builds, per env, a map of every agent's window holding the slot of the thing on each
+// cell and reads it (and the thing's code, weapon and life) for every cell; here a cell costs its static
+// word (obstacle, Box, objective bits and obstacle rank: the LDS tables of obs_stage_static4), the present
+// bit of its obstacle, its dead-body bit and, for an obstacle, the HP its load round fetched
+// (gym/observation.py:57-90: present obstacle > dead body > objective > empty), and then each present thing's
+// lane (slot s on lane s) writes its code, life and weapon into every window it falls in (a thing takes
+// precedence over everything on its cell).  The encoder's LDS region holds only the dead-body and present
+// words.  Load rounds, ring and writers as k_obs_bring.
+// ---------------------------------------------------------------------------
+__host__ __device__ constexpr int pbring_enc_bytes(int DW, int OW) { return ((DW * 4 + 15) / 16) * 16 + ((OW * 4 + 15) / 16) * 16; }
+__host__ __device__ constexpr int pbring_fixed_bytes(int DW, int OW) { return 16 * DW + BRING_ENC * pbring_enc_bytes(DW, OW) + 128; }
+__host__ __device__ constexpr int pbring_slots(int DW, int OW, int tsize, int nobs, int budget) {
+    return (budget - pbring_fixed_bytes(DW, OW)) / bring_unit_bytes(tsize, nobs) < 8 / ring_pair(tsize, nobs)
+               ? (budget - pbring_fixed_bytes(DW, OW)) / bring_unit_bytes(tsize, nobs)
+               : 8 / ring_pair(tsize, nobs);
+}
+
+template <typename T, int NOBS>
+__global__ void __launch_bounds__(64 * (BRING_ENC + BRING_WRT), 1) k_obs_pbring(Dev d, T* out, int env0, int env1, int us) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) step_tail(d);  // a zs_step's tail (Dev::tail_*)
+    extern __shared__ __align__(16) uint8_t smem[];
+    typedef typename obs_stage<T>::type S;
+    constexpr int WW = 21, PLANE = WW * WW, PER = PLANE / 63, TS = (int)sizeof(T);
+    static_assert(PLANE % 63 == 0, "63 lanes x PER rows of three");
+    constexpr int PAIR = ring_pair(TS, NOBS), SLOT = obs_stage_slot_bytes(TS, NOBS * PAIR), BLK = NOBS * 3 * PLANE;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int encb = pbring_enc_bytes(d.DW, d.OW);
+    lv4u* st4 = (lv4u*)smem;
+    lu8* slots = (lu8*)(smem + 16 * d.DW + BRING_ENC * encb);
+    ZS_LDS int* state = (ZS_LDS int*)(slots + us * SLOT);  // state[PAIR * slot + h], at most 8 words
+    if (threadIdx.x < 8) state[threadIdx.x] = 0;
+    obs_stage_static4(d, st4, threadIdx.x, blockDim.x);
+    __syncthreads();
+    const int G = gridDim.x, n_units = (env1 - env0 + PAIR - 1) / PAIR;
+    const XcdDeal deal(blockIdx.x, G, n_units, BRING_WRT);
+    const int ucount = deal.ucount;
+    const int count = ucount ? PAIR * (ucount - 1) + min(PAIR, env1 - env0 - PAIR * deal.unit(ucount - 1)) : 0;
+    auto unit_env = [&](int u) { return env0 + PAIR * deal.unit(u); };
+    if (wave >= BRING_ENC) {  // writer
+        for (int u = wave - BRING_ENC; u < ucount; u += BRING_WRT) {
+            const int q = u % us, e = unit_env(u);
+            const bool whole = PAIR * u + PAIR <= count;
+            for (int h = 0; h < PAIR; h++)
+                if (PAIR * u + h < count) ring_wait(&state[PAIR * q + h], 2 * u + 1);
+            if (whole) obs_stage_flush<T, NOBS * PAIR, BRING_THR>(slots + q * SLOT, out + (size_t)e * BLK, lane);
+            else obs_stage_flush<T, NOBS, BRING_THR>(slots + q * SLOT, out + (size_t)e * BLK, lane);
+            for (int h = 0; h < PAIR; h++) ring_state_store(&state[PAIR * q + h], 2 * u + 2);
+        }
+        return;
+    }
+    // encoder
+    lu32* idead = (lu32*)(smem + 16 * d.DW + wave * encb);
+    lu32* iopres = (lu32*)(smem + 16 * d.DW + wave * encb + ((d.DW * 4 + 15) / 16) * 16);
+    const int code_s = lane < d.A ? d.agent_codes[lane < d.A ? lane : 0] : (lane < d.A + d.P ? ZS_THING_PLAYER : ZS_THING_ZOMBIE);
+    const int W = d.W, H = d.H, sl = lane < d.E ? lane : d.E - 1;
+    // a lane's window cells: lane + 63 i, row lr + 3 i, column lq (lane 63 repeats lane 0's next cell)
+    const int lr = lane / WW, lq = lane - lr * WW;
+    auto item_env = [&](int t) { return unit_env(t / PAIR) + t % PAIR; };
+    if (wave >= count) return;
+    struct R1 {  // entity slot `lane`, dirty masks
+        int32_t p, l, w, r;
+        uint32_t hd, dd;
+    };
+    struct R23 {  // dead-body and present words; the HP of the window cells' obstacles
+        uint32_t dv[BRING_D], ov[BRING_O];
+        int32_t hv[NOBS][PER];
+    };
+    auto envc = [&](int t) { return item_env(t < count ? t : wave); };
+    auto round1 = [&](int t, R1& r) {
+        const int e = envc(t);
+        r.p = d.pos[EIX(d, sl, e)];
+        r.l = d.life[EIX(d, sl, e)];
+        r.w = d.weapon[EIX(d, sl, e)];
+        r.r = d.present[EIX(d, sl, e)];
+        r.hd = d.hp_dirty[e];
+        r.dd = d.dead_dirty[e];
+    };
+    // every load unconditional, addresses clamped; a window cell's obstacle index from the LDS tables (the
+    // cell's rank among the map's obstacle cells, 0 where none: discarded by the encoding)
+    auto round23 = [&](int t, const R1& r, R23& q) {
+        const int e = envc(t);
+        const uint32_t* dr = d.dead + (size_t)e * d.DW;
+#pragma unroll
+        for (int i = 0; i < BRING_D; i++) {
+            const int w = min(lane + 64 * i, d.DW - 1);
+            q.dv[i] = (((r.dd >> chunk_of((uint32_t)w, d.dead_chunk_m32)) & 1u) ? dr : d.dead_zero)[w];
+        }
+        const uint32_t* orow = r.hd ? d.obst_present + (size_t)e * d.OW : d.opres_full;
+#pragma unroll
+        for (int i = 0; i < BRING_O; i++) q.ov[i] = orow[min(lane + 64 * i, max(d.OW - 1, 0))];
+        const int32_t* hrow = d.obst_hp + (size_t)e * d.O;
+#pragma unroll
+        for (int a = 0; a < NOBS; a++) {
+            const int32_t ap = __builtin_amdgcn_readlane(r.p, a);
+            const int ox = unpack_x(ap) - WW / 2, oy = unpack_y(ap) - WW / 2;
+            const bool xin = (unsigned)(ox + lq) < (unsigned)W;
+            const int c0 = (oy + lr) * W + ox + lq;
+#pragma unroll
+            for (int i = 0; i < PER; i++) {
+                const int y = oy + lr + 3 * i;
+                const bool inb = xin && (unsigned)y < (unsigned)H;
+                const int c = inb ? c0 + 3 * i * W : 0;
+                const uint32_t bit = 1u << (c & 31);
+                const zs_v4u sw = st4[c >> 5];
+                const int o = (sw.x & bit) ? (int)(sw.w + __popc(sw.x & (bit - 1u))) : 0;
+                q.hv[a][i] = (((r.hd >> chunk_of((uint32_t)o, d.hp_chunk_m32)) & 1u) ? hrow : d.hp_init)[o];
+            }
+        }
+    };
+    // the item's dead-body and present words into the wave's LDS region
+    auto build = [&](const R23& q) {
+#pragma unroll
+        for (int i = 0; i < BRING_D; i++)
+            if (lane + 64 * i < d.DW) idead[lane + 64 * i] = q.dv[i];
+#pragma unroll
+        for (int i = 0; i < BRING_O; i++)
+            if (lane + 64 * i < d.OW) iopres[lane + 64 * i] = q.ov[i];
+        wave_sync();
+    };
+    // every agent's block of item t into its unit's slot: the map pass, then the things over it
+    auto encode = [&](int t, const R1& r, const R23& q) {
+        const int u = t / PAIR, h = t % PAIR, e = item_env(t);
+        const int qs = u % us;
+        if (u >= us) ring_wait(&state[PAIR * qs + h], 2 * (u - us) + 2);
+        wave_sync();
+        ZS_LDS S* ot0 = (ZS_LDS S*)(slots + qs * SLOT) + (int)((uintptr_t)(out + (size_t)(e - h) * BLK) & 15) / TS + h * BLK;
+#pragma unroll
+        for (int a = 0; a < NOBS; a++) {
+            const int32_t ap = __builtin_amdgcn_readlane(r.p, a);
+            const int ox = unpack_x(ap) - WW / 2, oy = unpack_y(ap) - WW / 2;
+            ZS_LDS S* ot = ot0 + a * 3 * PLANE;
+            const bool xin = (unsigned)(ox + lq) < (unsigned)W;
+            const int c0 = (oy + lr) * W + ox + lq;
+#pragma unroll
+            for (int i = 0; i < PER; i++) {
+                const int cell = lane + 63 * i;
+                const int y = oy + lr + 3 * i;
+                const bool inb = xin && (unsigned)y < (unsigned)H;
+                const int c = inb ? c0 + 3 * i * W : 0;
+                const uint32_t bit = 1u << (c & 31);
+                const zs_v4u sw = st4[c >> 5];
+                const uint32_t isob = (sw.x & bit) ? 1u : 0u;
+                const int oi = isob ? (int)(sw.w + __popc(sw.x & (bit - 1u))) : 0;
+                const bool obp = (isob & (iopres[oi >> 5] >> (oi & 31))) & 1u;
+                int code = (idead[c >> 5] & bit) ? ZS_THING_DEADBODY : (sw.z & bit) ? ZS_THING_OBJECTIVE : ZS_THING_NONE;
+                code = obp ? ((sw.y & bit) ? ZS_THING_BOX : ZS_THING_WALL) : code;
+                code = inb ? code : ZS_THING_WALL;
+                int life = obp ? q.hv[a][i] : 0;
+                life = inb ? life : 200;
+                if (cell < PLANE) {
+                    ot[cell] = (S)code;
+                    ot[PLANE + cell] = obs_val<S>(life);
+                    ot[2 * PLANE + cell] = (S)0;
+                }
+            }
+        }
+        wave_sync();
+        // the present things, slot s on lane s, over every agent's window
+        if (lane < d.E && r.r) {
+            const int x = unpack_x(r.p), y = unpack_y(r.p);
+#pragma unroll
+            for (int a = 0; a < NOBS; a++) {
+                const int32_t ap = __builtin_amdgcn_readlane(r.p, a);
+                const int dx = x - (unpack_x(ap) - WW / 2), dy = y - (unpack_y(ap) - WW / 2);
+                if ((unsigned)dx < (unsigned)WW && (unsigned)dy < (unsigned)WW) {
+                    ZS_LDS S* ot = ot0 + a * 3 * PLANE;
+                    const int cc = dy * WW + dx;
+                    ot[cc] = (S)code_s;
+                    ot[PLANE + cc] = obs_val<S>(r.l);
+                    ot[2 * PLANE + cc] = (S)r.w;
+                }
+            }
+        }
+        ring_state_store(&state[PAIR * qs + h], 2 * u + 1);
+        wave_sync();  // the region is rebuilt for the next item
+    };
+    R1 ra, rb;
+    R23 qa, qb;
+    int t = wave;
+    round1(t, ra);
+    round1(t + BRING_ENC, rb);
+    round23(t, ra, qa);
+    // item t from set a while set b's later rounds run, then the roles swap
+    auto step = [&](int t, R1& rx, R23& qx, R1& ry, R23& qy) {
+        build(qx);
+        round23(t + BRING_ENC, ry, qy);
+        const R1 cur = rx;  // the item's entity row (its things and agent positions), then the row two items on
+        round1(t + 2 * BRING_ENC, rx);
+        encode(t, cur, qx);
+    };
+    for (; t < count; t += 2 * BRING_ENC) {
+        step(t, ra, qa, rb, qb);
+        if (t + BRING_ENC < count) step(t + BRING_ENC, rb, qb, ra, qa);
+    }
+}

@@ -225,13 +225,15 @@ def test_store_stream_every_phase(patch):
                64, 60, n_discrete=6, check_state_every=30, launch=lo)
 
 
-CITY128_OBS = {"bring": {}, "gather": {"obs_ring": -1}, "gather_scell": {"obs_ring": -1, "obs_gather_stat": -1}}
+CITY128_OBS = {"pbring": {}, "bring": {"obs_ring_patch": -1}, "gather": {"obs_ring": -1},
+               "gather_scell": {"obs_ring": -1, "obs_gather_stat": -1}}
 
 
 @pytest.mark.parametrize("path", sorted(CITY128_OBS))
 def test_city128_obs_paths(path):
-    """C4's observation kernels: k_obs_bring (default: window-only encoders, writer waves), k_obs_gather
-    with static words from the LDS tables or one global load per window cell."""
+    """C4's observation kernels: k_obs_pbring (default: window-only encoders, the things written over the
+    windows, writer waves), k_obs_bring (per-cell window maps), k_obs_gather with static words from the
+    LDS tables or one global load per window cell."""
     run_parity(lambda n: _abi.multi_env_config(n, "safehouse", [], "city128", ["0", "1", "2", "3"],
                                                initial_zombies=50, minimum_zombies=50),
                24, 30, check_state_every=15, launch=CITY128_OBS[path])

@@ -210,12 +210,19 @@ def test_c4_16384_graph():
     """C4: city128 safehouse, 4 agents + 50 zombies (minimum 50): k_obs_bring (window-only encoders and
     writer waves), k_respawn after zombie deaths and safehouse / all-dead autoresets, at full size."""
     def respawned(eng):
-        assert eng.describe()["obs_kernel"] == "k_obs_bring"
+        assert eng.describe()["obs_kernel"] == "k_obs_pbring"
         # every zombie death leaves a deficit under minimum 50 that the same step's respawn fills
         zd = sum(eng.get_state(e).zombie_deaths for e in range(0, 16384, 97))
         assert zd > 0, "no zombie died in the sampled envs: k_respawn untested"
         assert eng.describe()["respawn"] == "k_respawn"
     run_full(c4, 16384, 80, min_resets=1, after=respawned)
+
+
+def test_c4_16384_graph_bring():
+    """C4 through k_obs_bring (per-cell window maps of the things) at full size, respawns and autoresets."""
+    def bring(eng):
+        assert eng.describe()["obs_kernel"] == "k_obs_bring"
+    run_full(c4, 16384, 60, seed0=11, min_resets=1, launch={"obs_ring_patch": -1}, after=bring)
 
 
 def test_c4_4096_gather():

@@ -222,7 +222,7 @@ def test_raise_kind_only_in_debug_envs():
         eng.close()
 
 
-BIG_ENCODERS = {"k_obs_bring": {}, "k_obs_gather": {"obs_ring": -1}}
+BIG_ENCODERS = {"k_obs_pbring": {}, "k_obs_bring": {"obs_ring_patch": -1}, "k_obs_gather": {"obs_ring": -1}}
 
 
 @pytest.mark.gpu
