@@ -1792,19 +1792,58 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
     wave_sync();
     STAMP(1);
     if (stepping) {
-        // decisions (start-of-tick state), the group's lanes over the actors in dict order, and the action
-        // list of get_actions (core.py:80-101) compacted from them in the same pass when no decision was
-        // deferred to the leader (RNG-drawing) or raises: MISC_NMOVED = its length, else -1
+        // decisions (start-of-tick state), then the action list of get_actions (core.py:80-101) compacted from
+        // them in dict order, when no decision was deferred to the leader (RNG-drawing) or raises:
+        // MISC_NMOVED = its length, else -1.  A decision reads only the start-of-tick state.  With 32 or more
+        // lanes per env the lanes take the actors by slot class (agents, bots, zombies), so a wave runs each
+        // class's code once per pass instead of the agent path in every pass that holds an agent of one of its
+        // envs (C4, 54 actors: tick 124.2 -> 120.8 us); with fewer lanes the extra pass costs more than it
+        // saves (C3: 82.3 -> 86.4 us; profiles/r05e_ab_decide_by_class.log), and the lanes walk the dict order.
+        constexpr bool BYCLASS = G >= 32;
         int nact = 0;
         unsigned long long special = 0ull;
+        if constexpr (BYCLASS) {
+            for (int b0 = 0; b0 < A; b0 += G) {
+                const int s = b0 + j;
+                if (s < A && LPR(c, s)) {
+                    int kk = K_NONE, tgt = 0;
+                    decide_agent(d, c, s, kk, tgt);
+                    LK(c, s) = (uint8_t)kk;
+                    LT(c, s) = tgt;
+                }
+            }
+            for (int b0 = A; b0 < A + d.P; b0 += G) {
+                const int s = b0 + j;
+                if (s < A + d.P && LPR(c, s)) {
+                    int kk = K_NONE, tgt = 0;
+                    decide_bot(d, c, s, false, kk, tgt);
+                    LK(c, s) = (uint8_t)kk;
+                    LT(c, s) = tgt;
+                }
+            }
+            for (int b0 = A + d.P; b0 < E; b0 += G) {
+                const int s = b0 + j;
+                if (s < E && LPR(c, s)) {
+                    int kk = K_NONE, tgt = 0;
+                    decide_zombie(d, c, s, false, kk, tgt);
+                    LK(c, s) = (uint8_t)kk;
+                    LT(c, s) = tgt;
+                }
+            }
+            wave_sync();
+        }
         for (int b0 = 0; b0 < n_order; b0 += G) {
             const int k = b0 + j;
             int s = 0, kk = K_NONE, tgt = 0;
             if (k < n_order) {
                 s = LO(c, k);
-                decide(d, c, s, actions, false, kk, tgt);
-                LK(c, s) = (uint8_t)kk;
-                LT(c, s) = tgt;
+                if constexpr (BYCLASS) {
+                    kk = LK(c, s);
+                } else {
+                    decide(d, c, s, actions, false, kk, tgt);
+                    LK(c, s) = (uint8_t)kk;
+                    LT(c, s) = tgt;
+                }
             }
             const bool keep = kk == K_MOVE || kk == K_ATTACK || kk == K_HEAL;
             const unsigned long long sb = __ballot(kk == K_DEFER || kk == K_RAISE);
