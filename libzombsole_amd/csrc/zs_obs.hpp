@@ -724,6 +724,9 @@ __device__ __forceinline__ void obs_store_throttle() {
 #ifndef ZS_OBS_THR_NARROW
 #define ZS_OBS_THR_NARROW ZS_OBS_THR
 #endif
+#ifndef ZS_FLUSH_GLOBAL
+#define ZS_FLUSH_GLOBAL 1
+#endif
 template <typename T, int NBLK = 1, int THR = (sizeof(T) == 8 ? ZS_OBS_THR : ZS_OBS_THR_NARROW)>
 __device__ __forceinline__ void obs_stage_flush(const lu8* slot, T* o, int lane) {
     typedef typename obs_stage<T>::type S;
@@ -744,8 +747,18 @@ __device__ __forceinline__ void obs_stage_flush(const lu8* slot, T* o, int lane)
         } else {
             v = *(const ZS_LDS zs_v4u*)(sv + kr * VPC);
         }
-        __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)((k >= k0 && k < kend) ? (uint32_t)(16 * k - mis) : ZS_OOB), 0,
-                                               obs_aux<T>());
+        if (ZS_FLUSH_GLOBAL) {
+            // plain global stores of the whole 16-B chunks: on this part a stream of them runs 6 % faster than the
+            // same stream of raw buffer stores (tools/probe/storepat2.hip, profiles/r05k_storepat2.log)
+            if (k >= k0 && k < kend) {
+                zs_v4u* dst = (zs_v4u*)((uint8_t*)o - mis) + k;
+                if constexpr (obs_aux<T>() != 0) __builtin_nontemporal_store(v, dst);
+                else *dst = v;
+            }
+        } else {
+            __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)((k >= k0 && k < kend) ? (uint32_t)(16 * k - mis) : ZS_OOB), 0,
+                                                   obs_aux<T>());
+        }
         if (THR >= 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(THR < 0 ? 0 : THR) : "memory");
     }
     const int nhead = mis ? (16 - mis) / TS : 0, tail0 = (16 * kend - mis) / TS, ntail = (nb - 16 * kend) / TS;
