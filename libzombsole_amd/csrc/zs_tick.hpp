@@ -1570,17 +1570,38 @@ __device__ __forceinline__ void bcast_row(lu32* base, int w, uint32_t v) {
 // their round trip (it needs the stream state) overlaps the decisions instead of the stage-in
 // smem: this wave's LDS image (tick_layout); pend (optional): the ballot of the envs this call found
 // pending a reset (bit g * G for env base + g), which the caller's reset work rebuilds (k_fstep)
+#ifndef ZS_TICK_LAUNDER
+#define ZS_TICK_LAUNDER 1
+#endif
+// the launch's Dev (its first kernel argument, at kernarg offset 0) through a pointer the compiler cannot
+// see through, so the fields read after it are loaded where they are used (tick_wg)
+__device__ __forceinline__ const Dev* zs_launder_dev() {
+    typedef const __attribute__((address_space(4))) Dev CDev;
+    CDev* dp = (CDev*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(dp));
+    return (const Dev*)dp;
+}
+
 template <int G, bool EARLY = false>
-__device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* actions, double* rew, uint8_t* done_out,
+__device__ __forceinline__ void tick_wg(const Dev& d0, int wg, const int32_t* actions, double* rew, uint8_t* done_out,
                                         uint8_t* trunc_out, uint8_t* listed_out, uint8_t* reset_out, int* reset_list,
                                         int* reset_count, void* obs_out, int env0, int env1, lu8* smem,
                                         unsigned long long* pend = nullptr) {
+    // The Dev fields are read through a pointer re-derived from the kernarg segment at each phase (ZS_TICK_LAUNDER):
+    // read through the kernel's by-value argument, the compiler loads them all up front and keeps them in SGPRs
+    // for the whole tick (458 SGPR spills into VGPR lanes at G = 8, each use a v_readlane).
+    const Dev* dp = ZS_TICK_LAUNDER ? zs_launder_dev() : &d0;
+#if ZS_TICK_LAUNDER
+#define ZS_RELOAD_DEV() dp = zs_launder_dev()
+#else
+#define ZS_RELOAD_DEV() (void)0
+#endif
     constexpr int NE = 64 / G;
     const int lane = threadIdx.x & 63, g = lane / G, j = lane - g * G;
-    const int base = env0 + wg * NE, e = base + g, N = d.N, E = d.E, A = d.A;
+    const int base = env0 + wg * NE, e = base + g, N = dp->N, E = dp->E, A = dp->A;
     const bool active = e < env1;
     const bool leader = j == 0;
-    const TickLayout L = tick_layout(NE, E, d.DW, d.rw_cap, d.cand_cap, d.lists_cap, A, d.fobs ? d.obsl.bytes + 4 * d.obs_stat : 0);
+    const TickLayout L = tick_layout(NE, E, dp->DW, dp->rw_cap, dp->cand_cap, dp->lists_cap, A, dp->fobs ? dp->obsl.bytes + 4 * dp->obs_stat : 0);
     lu32* lst = (lu32*)(smem + L.off_lst);
     Grp c;
     c.e = e;
@@ -1604,8 +1625,8 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
     c.lact = (li32*)(smem + L.off_act);
     c.xs = (li32*)(smem + L.off_xs);
     c.lists = (li32*)(smem + L.off_lists);
-    if (d.lists_cap)  // the static spawn lists, staged once per workgroup
-        for (int i = lane; i < d.nps + d.nzs; i += 64) c.lists[i] = i < d.nps ? d.pspawn[i] : d.zspawn[i - d.nps];
+    if (dp->lists_cap)  // the static spawn lists, staged once per workgroup
+        for (int i = lane; i < dp->nps + dp->nzs; i += 64) c.lists[i] = i < dp->nps ? dp->pspawn[i] : dp->zspawn[i - dp->nps];
 
     STAMP_DECL
     STAMP(0);
@@ -1632,54 +1653,54 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
             off = 0;
             ready = 0;
         }
-        const int maxw = off >= ZS_MT_N ? 0 : (ready ? d.rw_cap : min(d.rw_cap, ZS_MT_N - (int)off));
-        return min(d.rw_step, maxw);
+        const int maxw = off >= ZS_MT_N ? 0 : (ready ? dp->rw_cap : min(dp->rw_cap, ZS_MT_N - (int)off));
+        return min(dp->rw_step, maxw);
     };
     const int nmisc = MISC_N + 2 * A;
     if (active) {
-        if (d.pol_n) {
-            pseed = d.seeds[e];
-            pstep = *d.pol_step;
+        if (dp->pol_n) {
+            pseed = dp->seeds[e];
+            pstep = *dp->pol_step;
         } else if (A) {
             av = actions[(size_t)e * A * 3 + min(j, 3 * A - 1)];
         }
-        needs_reset = d.scal[S_NEEDRESET * N + e];
-        n_order = d.scal[S_NORDER * N + e];
-        st = d.rngst[e];
+        needs_reset = dp->scal[S_NEEDRESET * N + e];
+        n_order = dp->scal[S_NORDER * N + e];
+        st = dp->rngst[e];
 #pragma unroll
         for (int u = 0; u < 4; u++) {
             const int s = j + u * G;
             if (s < E) {  // slots past E issue nothing (an all-lanes-false batch is skipped)
-                vp[u] = d.pos[EIX(d, s, e)];
-                vl[u] = d.life[EIX(d, s, e)];
-                vw[u] = d.weapon[EIX(d, s, e)];
-                vr[u] = d.present[EIX(d, s, e)];
-                vo[u] = d.order[EIX(d, s, e)];
+                vp[u] = dp->pos[EIX(*dp, s, e)];
+                vl[u] = dp->life[EIX(*dp, s, e)];
+                vw[u] = dp->weapon[EIX(*dp, s, e)];
+                vr[u] = dp->present[EIX(*dp, s, e)];
+                vo[u] = dp->order[EIX(*dp, s, e)];
             }
         }
-        mval = misc_load(d, min(j, nmisc - 1), e);
-        opw = d.obst_present[(size_t)e * d.OW + min(j, max(d.OW - 1, 0))];
+        mval = misc_load(*dp, min(j, nmisc - 1), e);
+        opw = dp->obst_present[(size_t)e * dp->OW + min(j, max(dp->OW - 1, 0))];
     }
     // occupancy is rebuilt here, not kept in HBM: the map's obstacle cells (static, shared by every env,
     // cache-resident; loaded once per wave, each word stored to all NE envs' rows), minus the obstacles
     // an env has lost, plus its present things
 #pragma unroll
     for (int u = 0; u < 8; u++)
-        if (64 * u < d.DW) bmv[u] = d.obstbits[min(lane + 64 * u, d.DW - 1)];
+        if (64 * u < dp->DW) bmv[u] = dp->obstbits[min(lane + 64 * u, dp->DW - 1)];
     stepping = active && needs_reset == 0;
-    if (active && d.pol_n) {
+    if (active && dp->pol_n) {
         // zs_step_graph: the policy's actions for this step (zs_gen_actions' stream), written out to the
         // caller's action buffer as the policy kernel would (envs reset by this call included)
         for (int k = j; k < 3 * A; k += G) {
-            const int32_t v = policy_action(pseed, pstep, d.pol_n, k);
+            const int32_t v = policy_action(pseed, pstep, dp->pol_n, k);
             ((int32_t*)actions)[(size_t)e * A * 3 + k] = v;
             if (stepping) LACT(c, k) = v;
         }
     }
 #pragma unroll
     for (int u = 0; u < 8; u++)
-        if (64 * u < d.DW && lane + 64 * u < d.DW) bcast_row<NE>(c.bm, lane + 64 * u, bmv[u]);
-    for (int w = 512 + lane; w < d.DW; w += 64) bcast_row<NE>(c.bm, w, d.obstbits[w]);  // maps past 128 x 128
+        if (64 * u < dp->DW && lane + 64 * u < dp->DW) bcast_row<NE>(c.bm, lane + 64 * u, bmv[u]);
+    for (int w = 512 + lane; w < dp->DW; w += 64) bcast_row<NE>(c.bm, w, dp->obstbits[w]);  // maps past 128 x 128
     if (stepping) {
 #pragma unroll
         for (int u = 0; u < 4; u++) {
@@ -1693,7 +1714,7 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
             }
         }
         if (j < nmisc) MISC(c, j) = mval;
-        if (!d.pol_n) {
+        if (!dp->pol_n) {
             if (j < 3 * A) LACT(c, j) = av;
             for (int k = j + G; k < 3 * A; k += G) LACT(c, k) = actions[(size_t)e * A * 3 + k];
         }
@@ -1708,11 +1729,11 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
 #pragma unroll
                 for (int u = 0; u < 4; u++) {
                     int s = min(b + u * G, E - 1);
-                    vp[u] = d.pos[EIX(d, s, e)];
-                    vl[u] = d.life[EIX(d, s, e)];
-                    vw[u] = d.weapon[EIX(d, s, e)];
-                    vr[u] = d.present[EIX(d, s, e)];
-                    vo[u] = d.order[EIX(d, s, e)];
+                    vp[u] = dp->pos[EIX(*dp, s, e)];
+                    vl[u] = dp->life[EIX(*dp, s, e)];
+                    vw[u] = dp->weapon[EIX(*dp, s, e)];
+                    vr[u] = dp->present[EIX(*dp, s, e)];
+                    vo[u] = dp->order[EIX(*dp, s, e)];
                 }
 #pragma unroll
                 for (int u = 0; u < 4; u++) {
@@ -1728,7 +1749,7 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
             }
         }
         // the rest of the per-env scalars and reward tracker / env.agents rows (more rows than lanes)
-        for (int f = j + G; f < nmisc; f += G) MISC(c, f) = misc_load(d, f, e);
+        for (int f = j + G; f < nmisc; f += G) MISC(c, f) = misc_load(*dp, f, e);
         // RNG window: the next words of this env's stream, tempered
         uint32_t off, slot, ready;
         int b0 = j;
@@ -1737,7 +1758,7 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
             // the window's first 4G words: issued now, into LDS only once the decisions are made (the first
             // reader is the shuffle), so their round trip, which needs the stream state of round 1, runs
             // under the decisions instead of lengthening the stage-in
-            const uint32_t* ringe = d.ring + (size_t)e * ZS_RING_WORDS;
+            const uint32_t* ringe = dp->ring + (size_t)e * ZS_RING_WORDS;
 #pragma unroll
             for (int u = 0; u < 4; u++) {
                 const uint32_t q = off + min(j + u * G, max(wlen - 1, 0));
@@ -1745,7 +1766,7 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
             }
             b0 = j + 4 * G;
         }
-        const uint32_t* ring = d.ring + (size_t)e * ZS_RING_WORDS;
+        const uint32_t* ring = dp->ring + (size_t)e * ZS_RING_WORDS;
         for (int b = b0; b < wlen; b += 8 * G) {
             uint32_t v[8];
 #pragma unroll
@@ -1766,31 +1787,32 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
         for (int k = j; k < n_order; k += G) LR(c, LO(c, k)) = (uint8_t)k;
         // the cells of obstacles this env has lost (cleaned up, core.py:121-138) are free
         auto lost = [&](int w, uint32_t pw) {
-            const int nb = min(32, d.O - 32 * w);
+            const int nb = min(32, dp->O - 32 * w);
             uint32_t gone = ~pw & (nb == 32 ? 0xffffffffu : ((1u << nb) - 1u));
             while (gone) {
-                const int32_t op = d.obst_xy[32 * w + __ffs(gone) - 1];
+                const int32_t op = dp->obst_xy[32 * w + __ffs(gone) - 1];
                 gone &= gone - 1;
-                const int cell = unpack_y(op) * d.W + unpack_x(op);
+                const int cell = unpack_y(op) * dp->W + unpack_x(op);
                 __hip_atomic_fetch_and(&c.bm[IX(c, cell >> 5)], ~(1u << (cell & 31)), __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_WORKGROUP);
             }
         };
-        if (j < d.OW) lost(j, opw);
-        for (int w = j + G; w < d.OW; w += G) lost(w, d.obst_present[(size_t)e * d.OW + w]);
+        if (j < dp->OW) lost(j, opw);
+        for (int w = j + G; w < dp->OW; w += G) lost(w, dp->obst_present[(size_t)e * dp->OW + w]);
     }
     wave_sync();
     if (stepping) {  // the present things' cells (one may stand where a lost obstacle was)
         for (int s = j; s < E; s += G)
             if (LPR(c, s)) {
                 const int32_t p = LP(c, s);
-                const int cell = unpack_y(p) * d.W + unpack_x(p);
+                const int cell = unpack_y(p) * dp->W + unpack_x(p);
                 __hip_atomic_fetch_or(&c.bm[IX(c, cell >> 5)], 1u << (cell & 31), __ATOMIC_RELAXED,
                                       __HIP_MEMORY_SCOPE_WORKGROUP);
             }
     }
     wave_sync();
     STAMP(1);
+    ZS_RELOAD_DEV();
     if (stepping) {
         // decisions (start-of-tick state), then the action list of get_actions (core.py:80-101) compacted from
         // them in dict order, when no decision was deferred to the leader (RNG-drawing) or raises:
@@ -1807,25 +1829,25 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
                 const int s = b0 + j;
                 if (s < A && LPR(c, s)) {
                     int kk = K_NONE, tgt = 0;
-                    decide_agent(d, c, s, kk, tgt);
+                    decide_agent(*dp, c, s, kk, tgt);
                     LK(c, s) = (uint8_t)kk;
                     LT(c, s) = tgt;
                 }
             }
-            for (int b0 = A; b0 < A + d.P; b0 += G) {
+            for (int b0 = A; b0 < A + dp->P; b0 += G) {
                 const int s = b0 + j;
-                if (s < A + d.P && LPR(c, s)) {
+                if (s < A + dp->P && LPR(c, s)) {
                     int kk = K_NONE, tgt = 0;
-                    decide_bot(d, c, s, false, kk, tgt);
+                    decide_bot(*dp, c, s, false, kk, tgt);
                     LK(c, s) = (uint8_t)kk;
                     LT(c, s) = tgt;
                 }
             }
-            for (int b0 = A + d.P; b0 < E; b0 += G) {
+            for (int b0 = A + dp->P; b0 < E; b0 += G) {
                 const int s = b0 + j;
                 if (s < E && LPR(c, s)) {
                     int kk = K_NONE, tgt = 0;
-                    decide_zombie(d, c, s, false, kk, tgt);
+                    decide_zombie(*dp, c, s, false, kk, tgt);
                     LK(c, s) = (uint8_t)kk;
                     LT(c, s) = tgt;
                 }
@@ -1840,7 +1862,7 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
                 if constexpr (BYCLASS) {
                     kk = LK(c, s);
                 } else {
-                    decide(d, c, s, actions, false, kk, tgt);
+                    decide(*dp, c, s, actions, false, kk, tgt);
                     LK(c, s) = (uint8_t)kk;
                     LT(c, s) = tgt;
                 }
@@ -1862,16 +1884,17 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
     }
     wave_sync();
     STAMP(2);
+    ZS_RELOAD_DEV();
     if (pend) *pend = __ballot(active && leader && !stepping);
     if (active && leader && !stepping) {  // this call is the env's reset; outputs as after env.reset()
-        int nr = d.reward_mode == ZS_REWARD_SINGLE ? 1 : A;
+        int nr = dp->reward_mode == ZS_REWARD_SINGLE ? 1 : A;
         for (int a = 0; a < nr; a++) rew[(size_t)e * nr + a] = 0.0;
         done_out[e] = 0;
         trunc_out[e] = 0;
         if (listed_out)
             for (int a = 0; a < A; a++) listed_out[(size_t)e * A + a] = 1;
         if (reset_out) reset_out[e] = 1;
-        d.scal[S_NEEDRESET * N + e] = 0;
+        dp->scal[S_NEEDRESET * N + e] = 0;
         lst[g] = 1u << 11;  // no MT refill for this env here
     }
     // the stream window, in every lane of a stepping env (the lanes' draws and the leader's continue it)
@@ -1881,20 +1904,20 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
     // the shuffle and execution by the env's lanes when no decision was deferred to the leader (grp_execute)
     bool par = false;
     int nm0 = 0;
-    if (stepping && d.par_exec) {
+    if (stepping && dp->par_exec) {
         const int nact = MISC(c, MISC_NMOVED);
         if (nact >= 0 && nact <= 2 * G) {
             int pos = 0, odirty = 0;
-            grp_shuffle<G>(d, c, nact, pos);
-            grp_execute<G>(d, c, nact, pos, nm0, odirty);
-            if (d.alog) {  // the executed actions in execution order (drop-in views)
-                int32_t* al = d.alog + (size_t)e * d.E * 2;
+            grp_shuffle<G>(*dp, c, nact, pos);
+            grp_execute<G>(*dp, c, nact, pos, nm0, odirty);
+            if (dp->alog) {  // the executed actions in execution order (drop-in views)
+                int32_t* al = dp->alog + (size_t)e * dp->E * 2;
                 for (int k = j; k < nact; k += G) {
                     const int s = LPE(c, k);
                     al[2 * k] = s | (LK(c, s) << 8);
                     al[2 * k + 1] = LT(c, s);
                 }
-                if (j == 0) d.alog_n[e] = nact;
+                if (j == 0) dp->alog_n[e] = nact;
             }
             for (int q = j; q < nm0; q += G) LR(c, LM(c, q)) = 255;  // re-inserted at the end of the dict
             if (odirty && j == 0) MISC(c, MISC_ODIRTY) = 1;
@@ -1904,6 +1927,7 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
     }
     wave_sync();
     STAMP(3);
+    ZS_RELOAD_DEV();
     if (leader && stepping) {
         c.n_order = n_order;
         c.t = MISC(c, MISC_T) + 1;
@@ -1918,15 +1942,15 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
             MISC(c, MISC_NORD) = c.n_order;
         } else {
             XEV(1);
-            env_step_leader(d, c, actions, rew, done_out, trunc_out, listed_out);
+            env_step_leader(*dp, c, actions, rew, done_out, trunc_out, listed_out);
         }
     }
     wave_sync();
-    env_cleanup_group<G>(d, c, stepping);
+    env_cleanup_group<G>(*dp, c, stepping);
     wave_sync();
     if (leader && stepping) {
-        if (MISC(c, MISC_NMOVED) >= 0) env_step_leader_b(d, c, rew, done_out, trunc_out, listed_out);
-        if (c.fin && (d.flags & ZS_FLAG_AUTORESET)) {
+        if (MISC(c, MISC_NMOVED) >= 0) env_step_leader_b(*dp, c, rew, done_out, trunc_out, listed_out);
+        if (c.fin && (dp->flags & ZS_FLAG_AUTORESET)) {
             needs_reset = 1;
             // rebuilt by the next call's reset work; a list holds each env at most once, so an index
             // past N means the counter was not zeroed for this call: never written out of bounds
@@ -1934,8 +1958,8 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
             if ((unsigned)k < (unsigned)N) reset_list[k] = e;
         }
         if (c.respawn) {  // k_respawn, after this launch
-            const int k = atomicAdd(d.resp_count, 1);
-            if ((unsigned)k < (unsigned)N) d.resp_list[k] = e;
+            const int k = atomicAdd(dp->resp_count, 1);
+            if ((unsigned)k < (unsigned)N) dp->resp_list[k] = e;
         }
         if (reset_out) reset_out[e] = 0;
         MISC(c, MISC_T) = c.t;
@@ -1945,51 +1969,55 @@ __device__ __forceinline__ void tick_wg(const Dev& d, int wg, const int32_t* act
         MISC(c, MISC_PREVZD) = c.prevzd;
         MISC(c, MISC_SERIAL) = c.serial;
         MISC(c, MISC_ODIRTY) = c.odirty;
-        d.scal[S_NORDER * N + e] = c.n_order;
-        d.scal[S_NEEDRESET * N + e] = needs_reset;
+        dp->scal[S_NORDER * N + e] = c.n_order;
+        dp->scal[S_NEEDRESET * N + e] = needs_reset;
         uint32_t stf = st_advance(c.st0, c.wpos);
-        d.rngst[e] = stf;
+        dp->rngst[e] = stf;
         lst[g] = stf;
     }
     wave_sync();
     STAMP(4);
+    ZS_RELOAD_DEV();
     // the MT refill first: its loads do not wait behind the stage-out's stores (one vmcnt for both)
-    coop_refill(d, base, min(NE, env1 - base), lst, (lu32*)(smem + L.off_bm));
+    coop_refill(*dp, base, min(NE, env1 - base), lst, (lu32*)(smem + L.off_bm));
     STAMP(5);
+    ZS_RELOAD_DEV();
     if (stepping) {
         for (int s = j; s < E; s += G) {
-            d.pos[EIX(d, s, e)] = LP(c, s);
-            d.life[EIX(d, s, e)] = LL(c, s);
-            d.weapon[EIX(d, s, e)] = LW(c, s);
-            d.present[EIX(d, s, e)] = LPR(c, s);
-            d.order[EIX(d, s, e)] = LO(c, s);
+            dp->pos[EIX(*dp, s, e)] = LP(c, s);
+            dp->life[EIX(*dp, s, e)] = LL(c, s);
+            dp->weapon[EIX(*dp, s, e)] = LW(c, s);
+            dp->present[EIX(*dp, s, e)] = LPR(c, s);
+            dp->order[EIX(*dp, s, e)] = LO(c, s);
         }
-        for (int f = j; f < MISC_N + 2 * A; f += G) misc_store(d, f, e, MISC(c, f));
+        for (int f = j; f < MISC_N + 2 * A; f += G) misc_store(*dp, f, e, MISC(c, f));
     }
     wave_sync();
     STAMP(6);
+    ZS_RELOAD_DEV();
     // observations of the envs ticked here (envs reset by this call get theirs from the reset work):
     // the whole wave encodes one env at a time, its image aliasing the dead tick region
-    if (d.fobs && obs_out && d.fobs_pipe) {
-        fobs_pipe<NE>(d, c, (uint8_t*)(smem + L.off_region), __ballot(stepping && leader), G, base, obs_out);
-    } else if (d.fobs && obs_out) {
+    if (dp->fobs && obs_out && dp->fobs_pipe) {
+        fobs_pipe<NE>(*dp, c, (uint8_t*)(smem + L.off_region), __ballot(stepping && leader), G, base, obs_out);
+    } else if (dp->fobs && obs_out) {
         const unsigned long long stepmask = __ballot(stepping && leader);  // bit g * G per stepping env
         lu8* img = (lu8*)(smem + L.off_region);
-        lu32* st = d.obs_stat ? (lu32*)(smem + L.off_region + d.obsl.bytes) : nullptr;
-        if (st && stepmask) obs_stage_static(d, st, lane, 64);
+        lu32* st = dp->obs_stat ? (lu32*)(smem + L.off_region + dp->obsl.bytes) : nullptr;
+        if (st && stepmask) obs_stage_static(*dp, st, lane, 64);
         for (int g2 = 0; g2 < NE; g2++) {
             if (!((stepmask >> (g2 * G)) & 1ull)) continue;
-            obs_build(d, d.obsl, img, base + g2, [&](int s, int& p, int& lf, int& wp, int& pr) {
+            obs_build(*dp, dp->obsl, img, base + g2, [&](int s, int& p, int& lf, int& wp, int& pr) {
                 p = c.lpos[s * NE + g2];
                 lf = c.llife[s * NE + g2];
                 wp = c.lweap[s * NE + g2];
                 pr = c.lpres[s * NE + g2];
             });
-            obs_stream_any(d, d.obsl, st, img, obs_out, base + g2);
+            obs_stream_any(*dp, dp->obsl, st, img, obs_out, base + g2);
             wave_sync();
         }
     }
     STAMP(7);
+#undef ZS_RELOAD_DEV
 }
 
 template <int G, int W = ZS_STEP_WAVES, bool EARLY = false>
