@@ -101,42 +101,54 @@ __device__ __forceinline__ uint32_t wave_rng_finish(WaveRng& r) {
     return stf;
 }
 
-__device__ __forceinline__ void reset_env_wave(const Dev& d, const ResetLds& L, int e, int list_mode, int* err_out) {
-    const int lane = threadIdx.x & 63, N = d.N, E = d.E, A = d.A, P = d.P;
+// The Dev fields are read through a pointer re-derived from the kernarg segment at each phase (as tick_wg
+// does): read through the kernel's by-value argument they are loaded once and held in SGPRs across the
+// whole rebuild, which spills.  The kernels calling this take their Dev as the first argument.
+#ifndef ZS_RESET_LAUNDER
+#define ZS_RESET_LAUNDER 1
+#endif
+#if ZS_RESET_LAUNDER
+#define ZS_RST_RELOAD() dp = zs_launder_dev()
+#else
+#define ZS_RST_RELOAD() (void)0
+#endif
+__device__ __forceinline__ void reset_env_wave(const Dev& d0, const ResetLds& L, int e, int list_mode, int* err_out) {
+    const Dev* dp = ZS_RESET_LAUNDER ? zs_launder_dev() : &d0;
+    const int lane = threadIdx.x & 63, N = dp->N, E = dp->E, A = dp->A, P = dp->P;
     RST_DECL
     RST(0);
-    const uint32_t st_in = d.rngst[e];
-    const int serial0 = d.scal[S_SERIAL * N + e];
+    const uint32_t st_in = dp->rngst[e];
+    const int serial0 = dp->scal[S_SERIAL * N + e];
     // the env's ring (both slots, independent of st_in) in the same round of loads as the rows below
     WaveRng r;
-    r.ring = d.ring + (size_t)e * ZS_RING_WORDS;
+    r.ring = dp->ring + (size_t)e * ZS_RING_WORDS;
     r.lr = L.tw;
     uint32_t rv[WR_STAGE_K];
     wave_rng_fetch(r, rv);
     // lane l's player (agents [0, A), bots [A, A + P)): its configured weapon / bot type
-    const int wsel = lane < A ? d.agent_weapons[lane] : lane < A + P ? d.bot_types[lane - A] : 0;
+    const int wsel = lane < A ? dp->agent_weapons[lane] : lane < A + P ? dp->bot_types[lane - A] : 0;
     // new World: the map's obstacles (all present, HP carried over), no things, no decoration
-    for (int w = lane; w < d.DW; w += 64) {
-        L.bm[w] = d.obstbits[w];
-        d.dead[(size_t)e * d.DW + w] = 0;
+    for (int w = lane; w < dp->DW; w += 64) {
+        L.bm[w] = dp->obstbits[w];
+        dp->dead[(size_t)e * dp->DW + w] = 0;
     }
-    if (lane == 0) d.dead_dirty[e] = 0u;
+    if (lane == 0) dp->dead_dirty[e] = 0u;
     int nonpos = 0;
-    for (int w = lane; w < d.OW; w += 64) {
-        int nb = min(32, d.O - 32 * w);
-        d.obst_present[(size_t)e * d.OW + w] = nb == 32 ? 0xffffffffu : ((1u << nb) - 1u);
-        nonpos |= d.obst_nonpos[(size_t)e * d.OW + w] != 0;
+    for (int w = lane; w < dp->OW; w += 64) {
+        int nb = min(32, dp->O - 32 * w);
+        dp->obst_present[(size_t)e * dp->OW + w] = nb == 32 ? 0xffffffffu : ((1u << nb) - 1u);
+        nonpos |= dp->obst_nonpos[(size_t)e * dp->OW + w] != 0;
     }
     for (int s = lane; s < E; s += 64) {
         L.lpres[s] = 0;
-        L.lpos[s] = d.pos[EIX(d, s, e)];
-        L.llife[s] = d.life[EIX(d, s, e)];
-        L.lweap[s] = d.weapon[EIX(d, s, e)];
+        L.lpos[s] = dp->pos[EIX(*dp, s, e)];
+        L.llife[s] = dp->life[EIX(*dp, s, e)];
+        L.lweap[s] = dp->weapon[EIX(*dp, s, e)];
     }
     const int odirty = __ballot(nonpos) != 0ull;
     wave_rng_put(r, rv);
     rng_block_load(r, st_in);
-    RST(1);
+    RST(1); ZS_RST_RELOAD();
     // players: Player() picks a random weapon unless its module gives one (things.py:113-116);
     // agents: WeaponFactory.create_player_weapon (weapons.py:28-45).  Each random pick is one
     // _randbelow(5), in bots-then-agents order.
@@ -169,13 +181,13 @@ __device__ __forceinline__ void reset_env_wave(const Dev& d, const ResetLds& L, 
         }
     } else {
     int nrw = 0;
-    for (int p = 0; p < P; p++) nrw += d.bot_types[p] != ZS_BOT_TERMINATOR && d.bot_types[p] != ZS_BOT_SNIPER;
-    for (int a = 0; a < A; a++) nrw += d.agent_weapons[a] == ZS_WEAPON_RANDOM;
+    for (int p = 0; p < P; p++) nrw += dp->bot_types[p] != ZS_BOT_TERMINATOR && dp->bot_types[p] != ZS_BOT_SNIPER;
+    for (int a = 0; a < A; a++) nrw += dp->agent_weapons[a] == ZS_WEAPON_RANDOM;
     if (nrw) wave_draws(r, 5, 0, nrw, nrw, [&](int t, uint32_t v) { L.jbuf[t] = v; });
     if (lane == 0) {
         int t = 0;
         for (int p = 0; p < P; p++) {
-            int bt = d.bot_types[p], w;
+            int bt = dp->bot_types[p], w;
             if (bt == ZS_BOT_TERMINATOR) w = ZS_WEAPON_SHOTGUN;  // terminator.py:40-42
             else if (bt == ZS_BOT_SNIPER) w = ZS_WEAPON_RIFLE;   // sniper.py:22-24
             else {                                               // choice([Gun, Shotgun, Rifle, Knife, Axe])
@@ -186,7 +198,7 @@ __device__ __forceinline__ void reset_env_wave(const Dev& d, const ResetLds& L, 
             L.llife[A + p] = 100;
         }
         for (int a = 0; a < A; a++) {
-            int w = d.agent_weapons[a];
+            int w = dp->agent_weapons[a];
             if (w == ZS_WEAPON_RANDOM) {  // choice([Knife(), Axe(), Gun(), Rifle(), Shotgun()])
                 int k = (int)L.jbuf[t++];
                 w = k == 0 ? ZS_WEAPON_KNIFE : k == 1 ? ZS_WEAPON_AXE : k == 2 ? ZS_WEAPON_GUN : k == 3 ? ZS_WEAPON_RIFLE : ZS_WEAPON_SHOTGUN;
@@ -199,22 +211,22 @@ __device__ __forceinline__ void reset_env_wave(const Dev& d, const ResetLds& L, 
     wave_sync();
     int n_order = 0, serial = serial0;
     int rc = ZS_OK;
-    RST(2);
+    RST(2); ZS_RST_RELOAD();
     // spawn_players, spawn_agents (game.py:181-187): fail_if_cant=True
     for (int i = lane; i < P; i += 64) L.lslots[i] = (uint8_t)(A + i);
     wave_sync();
-    if (wave_spawn(d, L, r, e, P, 0, d.nps, n_order, serial) < P) rc = ZS_ENOSPACE;
+    if (wave_spawn(*dp, L, r, e, P, 0, dp->nps, n_order, serial) < P) rc = ZS_ENOSPACE;
     if (rc == ZS_OK) {
         for (int i = lane; i < A; i += 64) L.lslots[i] = (uint8_t)i;
         wave_sync();
-        if (wave_spawn(d, L, r, e, A, 0, d.nps, n_order, serial) < A) rc = ZS_ENOSPACE;
+        if (wave_spawn(*dp, L, r, e, A, 0, dp->nps, n_order, serial) < A) rc = ZS_ENOSPACE;
     }
-    RST(3);
+    RST(3); ZS_RST_RELOAD();
     if (rc == ZS_OK) {
         // spawn_zombies(initial) (game.py:189-194): Zombie() draws randint(50, 100) first
-        int nz = d.initial_zombies;
-        for (int b0 = 0; b0 < nz; b0 += d.E + 8) {  // randint(50, 100) = 50 + _randbelow(51) each
-            int cnt = min(nz - b0, d.E + 8);
+        int nz = dp->initial_zombies;
+        for (int b0 = 0; b0 < nz; b0 += dp->E + 8) {  // randint(50, 100) = 50 + _randbelow(51) each
+            int cnt = min(nz - b0, dp->E + 8);
             wave_draws(r, 51, 0, cnt, cnt, [&](int t, uint32_t v) { L.jbuf[t] = v; });
             for (int i = lane; i < cnt; i += 64) {
                 L.llife[A + P + b0 + i] = 50 + (int)L.jbuf[i];
@@ -223,41 +235,41 @@ __device__ __forceinline__ void reset_env_wave(const Dev& d, const ResetLds& L, 
             }
             wave_sync();
         }
-        RST(4);
-        wave_spawn(d, L, r, e, nz, 1, d.nzs, n_order, serial);
+        RST(4); ZS_RST_RELOAD();
+        wave_spawn(*dp, L, r, e, nz, 1, dp->nzs, n_order, serial);
         RST(5);
     } else if (lane == 0 && err_out) {
         atomicMax(err_out, rc);
     }
-    RST(6);
+    RST(6); ZS_RST_RELOAD();
     const uint32_t stf = wave_rng_finish(r);
     // write the new world back
     for (int s = lane; s < E; s += 64) {
-        d.pos[EIX(d, s, e)] = L.lpos[s];
-        d.life[EIX(d, s, e)] = L.llife[s];
-        d.weapon[EIX(d, s, e)] = L.lweap[s];
-        d.present[EIX(d, s, e)] = L.lpres[s];
-        d.order[EIX(d, s, e)] = L.lorder[s];
+        dp->pos[EIX(*dp, s, e)] = L.lpos[s];
+        dp->life[EIX(*dp, s, e)] = L.llife[s];
+        dp->weapon[EIX(*dp, s, e)] = L.lweap[s];
+        dp->present[EIX(*dp, s, e)] = L.lpres[s];
+        dp->order[EIX(*dp, s, e)] = L.lorder[s];
     }
     for (int a = lane; a < A; a += 64) {  // reward_tracker.reset / env.agents = possible_agents
-        d.prev_life[(size_t)a * N + e] = L.llife[a];
-        d.listed[(size_t)a * N + e] = 1;
+        dp->prev_life[(size_t)a * N + e] = L.llife[a];
+        dp->listed[(size_t)a * N + e] = 1;
     }
     if (lane == 0) {
-        d.scal[S_T * N + e] = -1;
-        d.scal[S_DEATHS * N + e] = 0;
-        d.scal[S_ZD * N + e] = 0;
-        d.scal[S_EPSTEPS * N + e] = 0;
-        d.scal[S_NORDER * N + e] = n_order;
-        d.scal[S_PREVZD * N + e] = 0;
-        d.scal[S_SERIAL * N + e] = serial;
-        d.scal[S_ODIRTY * N + e] = odirty;
+        dp->scal[S_T * N + e] = -1;
+        dp->scal[S_DEATHS * N + e] = 0;
+        dp->scal[S_ZD * N + e] = 0;
+        dp->scal[S_EPSTEPS * N + e] = 0;
+        dp->scal[S_NORDER * N + e] = n_order;
+        dp->scal[S_PREVZD * N + e] = 0;
+        dp->scal[S_SERIAL * N + e] = serial;
+        dp->scal[S_ODIRTY * N + e] = odirty;
         // list mode (autoreset): the env stays pending; the tick of this same call reports it as
         // reset and clears the flag (it never reads this env's state).  Mask mode: done now.
-        if (!list_mode) d.scal[S_NEEDRESET * N + e] = 0;
-        d.rngst[e] = stf;
-        if (d.dlog_n) d.dlog_n[e] = 0;  // a reset removes nothing and executes nothing (ZS_FLAG_DEATH_LOG)
-        if (d.alog_n) d.alog_n[e] = 0;
+        if (!list_mode) dp->scal[S_NEEDRESET * N + e] = 0;
+        dp->rngst[e] = stf;
+        if (dp->dlog_n) dp->dlog_n[e] = 0;  // a reset removes nothing and executes nothing (ZS_FLAG_DEATH_LOG)
+        if (dp->alog_n) dp->alog_n[e] = 0;
     }
     wave_sync();
     RST(7);
@@ -340,41 +352,42 @@ __global__ void __launch_bounds__(64, ZS_RESET_WAVES) k_reset(Dev d, int list_mo
 // it: randint(50, 100) per new Zombie (things.py:61-68), then World.spawn_in_random's shuffle
 // (core.py:40-66) as wave work (wave_spawn), new zombies appended to the dict order.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void respawn_env_wave(const Dev& d, const ResetLds& L, int e) {
-    const int lane = threadIdx.x & 63, N = d.N, E = d.E, Z0 = d.A + d.P;
+__device__ __forceinline__ void respawn_env_wave(const Dev& d0, const ResetLds& L, int e) {
+    const Dev* dp = ZS_RESET_LAUNDER ? zs_launder_dev() : &d0;
+    const int lane = threadIdx.x & 63, N = dp->N, E = dp->E, Z0 = dp->A + dp->P;
     RST_DECL
     RST(0);
 #ifdef ZS_STAMPS
     if (lane == 0 && blockIdx.x < ZS_STAMP_WGS) g_stamp_wg[blockIdx.x * ZS_NPHASE + 19] += 1;  // respawns (slot 19)
 #endif
     WaveRng r;
-    r.ring = d.ring + (size_t)e * ZS_RING_WORDS;
+    r.ring = dp->ring + (size_t)e * ZS_RING_WORDS;
     r.lr = L.tw;
     // one round of loads for all the respawn reads: the env's ring (both slots) and stream state, its
     // counters, entity rows and obstacle-present words, the zombie spawn list, the static bitmap
     uint32_t rv[WR_STAGE_K];
     wave_rng_fetch(r, rv);
-    const uint32_t st_in = d.rngst[e];
-    const int n0 = d.scal[S_NORDER * N + e], serial0 = d.scal[S_SERIAL * N + e];
+    const uint32_t st_in = dp->rngst[e];
+    const int n0 = dp->scal[S_NORDER * N + e], serial0 = dp->scal[S_SERIAL * N + e];
     const int sl = min(lane, E - 1);
-    const int32_t vp = d.pos[EIX(d, sl, e)], vl = d.life[EIX(d, sl, e)];
-    const uint8_t vw = d.weapon[EIX(d, sl, e)], vr = d.present[EIX(d, sl, e)], vo = d.order[EIX(d, sl, e)];
+    const int32_t vp = dp->pos[EIX(*dp, sl, e)], vl = dp->life[EIX(*dp, sl, e)];
+    const uint8_t vw = dp->weapon[EIX(*dp, sl, e)], vr = dp->present[EIX(*dp, sl, e)], vo = dp->order[EIX(*dp, sl, e)];
     uint32_t opv[2];
 #pragma unroll
     for (int u = 0; u < 2; u++)
-        if (64 * u < d.OW) opv[u] = d.obst_present[(size_t)e * d.OW + min(lane + 64 * u, d.OW - 1)];
+        if (64 * u < dp->OW) opv[u] = dp->obst_present[(size_t)e * dp->OW + min(lane + 64 * u, dp->OW - 1)];
     int32_t zl[8];  // k_respawn stages only the zombie spawn list (reset_lds_carve's stage_lists false)
-    if (d.rlists_cap) {
+    if (dp->rlists_cap) {
 #pragma unroll
         for (int u = 0; u < 8; u++)
-            if (64 * u < d.nzs) zl[u] = d.zspawn[min(lane + 64 * u, d.nzs - 1)];
+            if (64 * u < dp->nzs) zl[u] = dp->zspawn[min(lane + 64 * u, dp->nzs - 1)];
     }
-    stage_in(d.obstbits, d.DW, lane, 64, L.bm, [](int w) { return w; });
-    if (d.rlists_cap) {
+    stage_in(dp->obstbits, dp->DW, lane, 64, L.bm, [](int w) { return w; });
+    if (dp->rlists_cap) {
 #pragma unroll
         for (int u = 0; u < 8; u++)
-            if (64 * u < d.nzs && lane + 64 * u < d.nzs) L.lists[d.nps + lane + 64 * u] = zl[u];
-        for (int i = 512 + lane; i < d.nzs; i += 64) L.lists[d.nps + i] = d.zspawn[i];
+            if (64 * u < dp->nzs && lane + 64 * u < dp->nzs) L.lists[dp->nps + lane + 64 * u] = zl[u];
+        for (int i = 512 + lane; i < dp->nzs; i += 64) L.lists[dp->nps + i] = dp->zspawn[i];
     }
     if (lane < E) {
         L.lpos[lane] = vp;
@@ -384,43 +397,43 @@ __device__ __forceinline__ void respawn_env_wave(const Dev& d, const ResetLds& L
         L.lorder[lane] = vo;
     }
     for (int s = 64 + lane; s < E; s += 64) {
-        L.lpos[s] = d.pos[EIX(d, s, e)];
-        L.llife[s] = d.life[EIX(d, s, e)];
-        L.lweap[s] = d.weapon[EIX(d, s, e)];
-        L.lpres[s] = d.present[EIX(d, s, e)];
-        L.lorder[s] = d.order[EIX(d, s, e)];
+        L.lpos[s] = dp->pos[EIX(*dp, s, e)];
+        L.llife[s] = dp->life[EIX(*dp, s, e)];
+        L.lweap[s] = dp->weapon[EIX(*dp, s, e)];
+        L.lpres[s] = dp->present[EIX(*dp, s, e)];
+        L.lorder[s] = dp->order[EIX(*dp, s, e)];
     }
-    RST(1);
+    RST(1); ZS_RST_RELOAD();
     // occupancy (as k_tick rebuilds it): the map's obstacle cells minus the lost obstacles, then the
     // present things
     wave_sync();
     auto lost = [&](int w, uint32_t pw) {
-        const int nb = min(32, d.O - 32 * w);
+        const int nb = min(32, dp->O - 32 * w);
         uint32_t gone = ~pw & (nb == 32 ? 0xffffffffu : ((1u << nb) - 1u));
         while (gone) {
-            const int32_t op = d.obst_xy[32 * w + __ffs(gone) - 1];
+            const int32_t op = dp->obst_xy[32 * w + __ffs(gone) - 1];
             gone &= gone - 1;
-            const int cell = unpack_y(op) * d.W + unpack_x(op);
+            const int cell = unpack_y(op) * dp->W + unpack_x(op);
             __hip_atomic_fetch_and(&L.bm[cell >> 5], ~(1u << (cell & 31)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
     };
 #pragma unroll
     for (int u = 0; u < 2; u++)
-        if (lane + 64 * u < d.OW) lost(lane + 64 * u, opv[u]);
-    for (int w = 128 + lane; w < d.OW; w += 64) lost(w, d.obst_present[(size_t)e * d.OW + w]);
+        if (lane + 64 * u < dp->OW) lost(lane + 64 * u, opv[u]);
+    for (int w = 128 + lane; w < dp->OW; w += 64) lost(w, dp->obst_present[(size_t)e * dp->OW + w]);
     wave_sync();
     for (int s = lane; s < E; s += 64)
         if (L.lpres[s]) {
-            const int cell = unpack_y(L.lpos[s]) * d.W + unpack_x(L.lpos[s]);
+            const int cell = unpack_y(L.lpos[s]) * dp->W + unpack_x(L.lpos[s]);
             __hip_atomic_fetch_or(&L.bm[cell >> 5], 1u << (cell & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
     wave_rng_put(r, rv);
     rng_block_load(r, st_in);
-    RST(2);
+    RST(2); ZS_RST_RELOAD();
     // Game.spawn_zombies(count): the deficit's Zombie()s go into the free zombie slots, lowest first
     int nz = 0;
     for (int b = Z0; b < E; b += 64) nz += __popcll(__ballot(b + lane < E && L.lpres[b + lane]));
-    const int k = max(d.minimum_zombies - nz, 0);
+    const int k = max(dp->minimum_zombies - nz, 0);
 #ifdef ZS_STAMPS
     if (lane == 0 && k > 0 && blockIdx.x < ZS_STAMP_WGS) g_stamp_wg[blockIdx.x * ZS_NPHASE + 19] += 1ull << 32;  // placing ones
 #endif
@@ -440,22 +453,22 @@ __device__ __forceinline__ void respawn_env_wave(const Dev& d, const ResetLds& L
         L.lweap[s] = ZS_WEAPON_CLAWS;
     });
     int n_order = n0, serial = serial0;
-    RST(3);
-    const int placed = wave_spawn(d, L, r, e, k, 1, d.nzs, n_order, serial);
-    RST(4);
+    RST(3); ZS_RST_RELOAD();
+    const int placed = wave_spawn(*dp, L, r, e, k, 1, dp->nzs, n_order, serial);
+    RST(4); ZS_RST_RELOAD();
     const uint32_t stf = wave_rng_finish(r);
     for (int m = lane; m < k; m += 64) {  // the new zombies (dropped ones keep their drawn life)
         const int s = L.lslots[m];
-        d.pos[EIX(d, s, e)] = L.lpos[s];
-        d.life[EIX(d, s, e)] = L.llife[s];
-        d.weapon[EIX(d, s, e)] = L.lweap[s];
-        d.present[EIX(d, s, e)] = L.lpres[s];
+        dp->pos[EIX(*dp, s, e)] = L.lpos[s];
+        dp->life[EIX(*dp, s, e)] = L.llife[s];
+        dp->weapon[EIX(*dp, s, e)] = L.lweap[s];
+        dp->present[EIX(*dp, s, e)] = L.lpres[s];
     }
-    for (int m = n0 + lane; m < n0 + placed; m += 64) d.order[EIX(d, m, e)] = L.lorder[m];
+    for (int m = n0 + lane; m < n0 + placed; m += 64) dp->order[EIX(*dp, m, e)] = L.lorder[m];
     if (lane == 0) {
-        d.scal[S_NORDER * N + e] = n_order;
-        d.scal[S_SERIAL * N + e] = serial;
-        d.rngst[e] = stf;
+        dp->scal[S_NORDER * N + e] = n_order;
+        dp->scal[S_SERIAL * N + e] = serial;
+        dp->rngst[e] = stf;
     }
     wave_sync();
     RST(5);
