@@ -194,6 +194,17 @@ struct Dev {
     uint32_t* ovf;
 };
 
+// the launch's Dev (its first kernel argument, at kernarg offset 0) through a pointer the compiler cannot
+// see through, so the fields read after it are loaded where they are used instead of held in SGPRs across
+// the whole kernel (tick_wg, reset_env_wave, k_obs_ring's encoders).  Only for kernels whose first argument
+// is the Dev.
+__device__ __forceinline__ const Dev* zs_launder_dev() {
+    typedef const __attribute__((address_space(4))) Dev CDev;
+    CDev* dp = (CDev*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(dp));
+    return (const Dev*)dp;
+}
+
 // lowest obstacle life the engine holds exactly; INT32_MIN itself marks an absent obstacle in the
 // observation kernels' compact images (ZS_HP_ABSENT, zs_obs.hpp)
 #define ZS_HP_FLOOR (-2147483647)

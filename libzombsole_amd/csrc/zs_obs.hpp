@@ -1323,8 +1323,12 @@ __device__ __forceinline__ void ring_wait(const ZS_LDS int* p, int v) {
 __host__ __device__ constexpr int ring_patch_lds_bytes(int static_bytes, int enc_bytes, int tsize, int nobs) {
     return ring_lds_bytes(static_bytes, enc_bytes, tsize, nobs);
 }
+#ifndef ZS_RING_LAUNDER
+#define ZS_RING_LAUNDER 1
+#endif
 template <typename T, int NOBS, bool PATCHED = false>
 __global__ void __launch_bounds__(64 * (RING_ENC + RING_WRT), 1) k_obs_ring(Dev d, T* out, ObsLayout L, int env0, int env1) {
+    const Dev& d0 = d;
     if (blockIdx.x == 0 && threadIdx.x == 0) step_tail(d);  // a zs_step's tail (Dev::tail_*)
     extern __shared__ __align__(16) uint8_t smem[];
     typedef typename obs_stage<T>::type S;
@@ -1386,6 +1390,8 @@ __global__ void __launch_bounds__(64 * (RING_ENC + RING_WRT), 1) k_obs_ring(Dev 
     // iterations later into f, with that item's dirty masks dq (loaded two iterations earlier), and
     // dq reloaded for the item two iterations after that
     auto encode = [&](int t, ObsPrefetch& f, zs_v2u& dq, int ahead) {
+        // the Dev fields reloaded per item (ZS_RING_LAUNDER), not held in SGPRs across the wave's items
+        const Dev& d = ZS_RING_LAUNDER ? *zs_launder_dev() : d0;
         const int u = t / PAIR, h = t % PAIR, e = item_env(t);
         if (PATCHED) pe.build(d, f);
         else obs_build_compact(d, L, img, f, code_s, lane);

@@ -1573,14 +1573,6 @@ __device__ __forceinline__ void bcast_row(lu32* base, int w, uint32_t v) {
 #ifndef ZS_TICK_LAUNDER
 #define ZS_TICK_LAUNDER 1
 #endif
-// the launch's Dev (its first kernel argument, at kernarg offset 0) through a pointer the compiler cannot
-// see through, so the fields read after it are loaded where they are used (tick_wg)
-__device__ __forceinline__ const Dev* zs_launder_dev() {
-    typedef const __attribute__((address_space(4))) Dev CDev;
-    CDev* dp = (CDev*)__builtin_amdgcn_kernarg_segment_ptr();
-    asm volatile("" : "+s"(dp));
-    return (const Dev*)dp;
-}
 
 template <int G, bool EARLY = false>
 __device__ __forceinline__ void tick_wg(const Dev& d0, int wg, const int32_t* actions, double* rew, uint8_t* done_out,
