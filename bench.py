@@ -14,6 +14,9 @@ index) and no data-path collective runs.
     python bench.py [--gpus N] [--steps K] [--warmup W] [--envs 65536]
     torchrun --nproc-per-node N bench.py --gpus N ...
 
+--gpus N decides the world size: without a launcher, N > 1 starts N rank processes of the same
+command (one per GPU, rendezvous on 127.0.0.1); under torchrun, WORLD_SIZE must equal N.
+
 Prints ONE JSON line (rank 0).
 """
 import argparse
@@ -89,6 +92,9 @@ def parse():
     p.add_argument("--launch", default="",
                    help="launch overrides for A/B runs, 'field=v,...' (zs_launch fields; 1 = on, -1 = off, n = size)")
     p.add_argument("--engine-lib", default=None, help="(tools) another build of the engine's sources, e.g. an A/B build")
+    p.add_argument("--dry-run", action="store_true",
+                   help="(tests) the multi-rank control flow only: rank processes, gloo rendezvous, env ranges, the "
+                        "barrier-bracketed timed loop on a no-op step and the slowest-rank time; no engine, no GPU")
     a = p.parse_args()
     a.launch = dict((kv.split("=")[0], int(kv.split("=")[1])) for kv in a.launch.split(",") if kv)
     for k, v in PRESETS[a.config].items():
@@ -254,8 +260,79 @@ def max_over_ranks(elapsed, device):
     return float(t.item())
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n):
+    """`--gpus N` without a launcher: N rank processes of this same command (RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_* as torchrun sets them, rendezvous on 127.0.0.1), started before this process
+    makes any HIP call, one per GPU.  Rank 0 prints the JSON line.  A rank that fails ends the others;
+    the exit status is the first failing rank's."""
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    while procs:
+        for p in list(procs):
+            code = p.poll()
+            if code is None:
+                continue
+            procs.remove(p)
+            if code and not rc:
+                rc = code
+                for q in procs:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+def dry_run(args, world, rank, distributed):
+    """--dry-run: the control flow of a multi-rank bench run on CPU (gloo), reported in the same JSON shape."""
+    import torch
+    import torch.distributed as dist
+    if distributed:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo")
+    n_local, env0, scaling, total_envs = env_range(rank, world, args.envs, args.envs_per_gpu)
+    elapsed = timed_loop(lambda: time.sleep(0.001), args.steps, args.warmup, lambda: None, distributed)
+    ranges = [(env0, n_local)]
+    if distributed:
+        elapsed = max_over_ranks(elapsed, torch.device("cpu"))
+        ranges = [None] * world
+        dist.all_gather_object(ranges, (env0, n_local))
+    out = {"metric": METRIC, "value": total_envs * args.steps / elapsed, "unit": "env-steps/s", "n_gpus": world,
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps,
+           "scaling": scaling, "dry_run": True, "rank_env_ranges": ranges, "total_envs": total_envs}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if distributed:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    # --gpus N decides the world size: N > 1 without a launcher spawns the N ranks here (before any HIP
+    # call in this process); under a launcher (torchrun: WORLD_SIZE set) the two must agree
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
+    if env_world is not None and int(env_world) != args.gpus:
+        sys.stderr.write("bench.py: --gpus %d but the launcher's WORLD_SIZE is %s\n" % (args.gpus, env_world))
+        sys.exit(2)
+    if args.dry_run:
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        dry_run(args, world, int(os.environ.get("RANK", "0")), world > 1)
+        return
     # ONE JSON line on stdout: anything else the process prints there (RCCL's version banner at its first
     # communicator, library notices) goes to stderr; the line itself is written to the saved stdout
     sys.stdout.flush()

@@ -313,8 +313,36 @@ int zs_death_log(zs_handle* h, int32_t env, int32_t* out_host, int32_t cap, int3
  * derive from it): per action {slot | kind << 8, target} with kind 1 move (target: destination
  * x | y << 16), 2 attack, 3 heal (target: an entity slot, or -1 - obstacle index in map order); at most
  * cap entries into out_host (2 int32 each); *n_out = how many.  Needs ZS_FLAG_DEATH_LOG; an env reset by
- * that step, or stopped by a debug raise, reports none. */
+ * that step reports none.  A step a debug raise stopped (ZS_ACT_RAISE) reports *n_out = -1 - k and, as its
+ * k entries, the actors before the raising one in dict order that decided an action (core.py:80-101: the
+ * others were idle). */
 int zs_action_log(zs_handle* h, int32_t env, int32_t* out_host, int32_t cap, int32_t* n_out, void* stream);
+
+/* ---- the drop-ins' per-call path ----------------------------------------------------------------
+ * ZombsoleGymEnv.step / reset / get_observation and the MultiagentZombsoleEnv equivalents
+ * (zombsole/gym_env.py:93-164, zombsole/gym/multiagent_env.py:87-184) run one env per Python call and
+ * read everything back on the host.  These calls do that in one host->device copy, the engine's
+ * launches, one device->host copy and one synchronisation, on engine-owned device outputs:
+ *   zs_host_step(h, actions_host [N][A][3], rng_host, rec_host)  = zs_set_rng + zs_step + read-back
+ *   zs_host_reset(h, rng_host, rec_host)                         = zs_set_rng + zs_reset (all envs) + read-back
+ *   zs_host_observe(h, rec_host)                                 = zs_observe + read-back
+ * rng_host: NULL, or [N][625] words of CPython random.getstate() form moved into the envs' streams
+ * before the call (the process-global stream the reference draws from).  rec_host: [N][words] int32
+ * records, each with the fixed header below and the sections zs_host_layout gives:
+ *   out[0] words per record, out[1] rewards (float64 [R]), out[2] action log (2E words, zs_action_log
+ *   form), out[3] death log (5E words, zs_death_log form), out[4] state record (zs_get_state form),
+ *   out[5] observation (out[6] bytes, zs_obs_shape of the config's dtype), out[7] R (1 single, A multi).
+ * The record always holds the env's stream after the call (rng section), so the caller moves it back into
+ * `random` even when zs_host_reset fails with ZS_ENOSPACE. */
+#define ZS_HOST_FLAGS 0  /* bit 0 done, bit 1 truncated, bit 2 autoreset by this call                 */
+#define ZS_HOST_ERR 1    /* the engine's error word for the call (ZS_ENOSPACE: players could not spawn) */
+#define ZS_HOST_ALOG_N 2 /* zs_action_log's n                                                           */
+#define ZS_HOST_DLOG_N 3 /* zs_death_log's n                                                            */
+#define ZS_HOST_RNG 4    /* 625 words: the env's stream in random.getstate() form                        */
+int zs_host_layout(zs_handle* h, int32_t out[8]);
+int zs_host_step(zs_handle* h, const int32_t* actions_host, const uint32_t* rng_host, int32_t* rec_host, void* stream);
+int zs_host_reset(zs_handle* h, const uint32_t* rng_host, int32_t* rec_host, void* stream);
+int zs_host_observe(zs_handle* h, int32_t* rec_host, void* stream);
 /* Diagnostic builds compiled with -DZS_STAMPS only (the product .so returns ZS_ESTATE):
  * per-phase k_tick cycle sums / maxima over all workgroup launches since the last call. */
 int zs_debug_stamps(zs_handle* h, uint64_t* sum_out, uint64_t* max_out, int32_t n);

@@ -4,97 +4,144 @@ process-global `random` stream.
 The reference's game draws every random number from CPython's module-global `random`
 (`zombsole/core.py:2`, `things.py:2`, `weapons.py:2`, `players/*.py`), so two envs in one
 process interleave on one stream and `random.seed(s)` before construction / `reset()`
-fixes an episode.  `EnvCore` keeps exactly that contract: around every engine call it
-moves `random.getstate()` into the env's MT19937 slot (`zs_set_rng`) and the advanced
-state back out (`zs_get_rng` -> `random.setstate`).  The tick itself always runs in the
-HIP engine; there is no host fallback.
+fixes an episode.  `EnvCore` keeps exactly that contract: every engine call takes
+`random.getstate()` into the env's MT19937 stream and hands the advanced stream back
+(`random.setstate`).  The tick itself always runs in the HIP engine; there is no host
+fallback.
+
+A call is one `zs_host_step` / `zs_host_reset` / `zs_host_observe` (include/zombsole_mi355x.h):
+the actions and the `random` state go in with one copy, and one record comes back with one
+copy and one synchronisation — the observation, rewards and flags, the advanced stream, the
+step's action and death logs and the env's state record, which `env.game` then reads without
+another device round trip.
 """
 import random
+import struct
 
 import numpy as np
 
 from . import _abi
 from .actions import ACT_RAISE, ActionError, encode_action
-from .engine import Engine
+from .engine import Engine, decode_action_log, decode_death_log
 from .game import GameView
+
+HOST_FLAGS, HOST_ERR, HOST_ALOG_N, HOST_DLOG_N, HOST_RNG = 0, 1, 2, 3, 4  # ZS_HOST_* header words
+MT_WORDS = 625
+_MT = struct.Struct("<625I")  # random.getstate()[1] <-> the engine's 625 uint32 words
+
+
+class HostRecord(object):
+    """One env's zs_host_* record (layout: zs_host_layout)."""
+
+    def __init__(self, eng, rec, lay, obs_dtype):
+        self.rec = rec
+        self.lay = lay
+        self.E = eng.E
+        self.flags = int(rec[HOST_FLAGS])
+        self.done = bool(self.flags & 1)
+        self.trunc = bool(self.flags & 2)
+        self.rewards = rec[lay["rew"]:lay["rew"] + 2 * lay["R"]].view(np.float64)
+        ob = lay["obs"]
+        nbytes = lay["obs_bytes"]
+        self.obs = rec[ob:ob + (nbytes + 3) // 4].view(np.uint8)[:nbytes].view(obs_dtype).reshape(eng.obs_shape)
+        self.state_buf = rec[lay["state"]:lay["state"] + eng.state_words]
+
+    def rng_state(self):
+        """The env's stream after the call, as a random.setstate() argument."""
+        return (3, _MT.unpack_from(self.rec, 4 * HOST_RNG), None)
+
+    def action_log(self):
+        return decode_action_log(self.rec[self.lay["alog"]:], int(self.rec[HOST_ALOG_N]), self.E)
+
+    def death_log(self):
+        return decode_death_log(self.rec[self.lay["dlog"]:], int(self.rec[HOST_DLOG_N]), self.E)
 
 
 class EnvCore(object):
     def __init__(self, builder, map_, rules_name, player_names, agent_ids, agent_weapons, initial_zombies,
                  minimum_zombies, debug, device=None):
-        # the per-step death log feeds the views' decoration order and removed things (game.py)
+        # the per-step death / action logs feed the views' decoration order, removed things and World.events
         builder.cfg.flags |= _abi.FLAG_DEATH_LOG
         self.engine = Engine(builder, device=device)
         self.torch = self.engine.torch
         self.debug = debug
+        self._lay = self.engine.host_layout()
+        self._np_obs = _abi.DTYPE_NP[builder.cfg.obs_dtype]
+        self._actions = np.zeros((1, self.engine.A, 3), dtype=np.int32)
+        self.last = None  # the last call's HostRecord
         self.game = GameView(self.engine, 0, map_, rules_name, player_names, agent_ids, agent_weapons,
                              initial_zombies, minimum_zombies, debug)
-        self._host_actions = np.zeros((1, self.engine.A, 3), dtype=np.int32)
         self.new_world(first=True)
+
+    @staticmethod
+    def _rng_in():
+        return _MT.pack(*random.getstate()[1])
+
+    def _record(self, rec):
+        self.last = HostRecord(self.engine, rec[0], self._lay, self._np_obs)
+        return self.last
 
     # Game.__initialize_world__ (game.py:151-169) on the engine, drawing from `random`
     def new_world(self, first=False):
         eng = self.engine
         if not first:
             self.game.end_episode()  # objects of the ending episode keep their values
-        eng.load_python_random(0)
+        rec = eng.host_record()
         try:
-            eng.reset()
-        finally:
-            eng.store_python_random(0)
-        self.game.new_episode()
+            eng.host_reset(self._rng_in(), rec)
+        except Exception as err:
+            if type(err) is Exception:  # ZS_ENOSPACE (core.py:62-64): the draws were taken, as in the reference
+                random.setstate(HostRecord(eng, rec[0], self._lay, self._np_obs).rng_state())
+            raise
+        r = self._record(rec)
+        random.setstate(r.rng_state())
+        self.game.new_episode(r.state_buf)
+        return r
 
     def encode(self, action):
-        """Agent.next_step's parse of one action dict; errors as World.get_actions treats them
-        (core.py:96-99): with debug the agent's action becomes ZS_ACT_RAISE (the tick stops there
-        and `tick` re-raises the exception), otherwise the agent idles."""
+        """Agent.next_step's parse of one action dict: an engine triple, or the ActionError the reference's
+        next_step raises for it (World.get_actions then logs it and, with debug, re-raises it;
+        core.py:96-99)."""
         try:
             return encode_action(action)
         except ActionError as err:
-            if self.debug:
-                return err
-            return (0, 0, 0)
+            return err
 
     def tick(self, triples):
-        """One World.step + env glue for the single engine env; returns host copies of
-        (obs[n_obs, C, H, W], rewards[A], done, truncated).
+        """One World.step + env glue for the single engine env; returns the call's HostRecord (obs
+        [n_obs, C, H, W], rewards [R], done, trunc).
 
-        An entry of `triples` may be the ActionError `encode` returned for a debug env: the engine
-        then runs World.step up to the first such agent in dict order — t += 1 and the decisions
-        (RNG draws included) of the actors before it — and this re-raises that agent's exception,
-        as the reference's World.step does (core.py:72-78, 96-99).  Agents that are not in the
-        world are never asked for an action, so their errors do not raise."""
+        An entry of `triples` may be the ActionError `encode` returned.  Without debug the agent idles and
+        World.events logs its error (core.py:96-97).  With debug the engine runs World.step up to the first
+        such agent in dict order — t += 1 and the decisions (RNG draws included) of the actors before it —
+        and this re-raises that agent's exception, as the reference's World.step does (core.py:72-78,
+        96-99).  Agents that are not in the world are never asked for an action, so their errors do not
+        raise."""
         eng = self.engine
         errors = {i: t for i, t in enumerate(triples) if isinstance(t, ActionError)}
-        raising = None
-        if errors:
-            st = eng.get_state(0)
-            for slot in st.order[:st.n_order]:
-                if int(slot) in errors:
-                    raising = errors[int(slot)]
-                    break
-        rows = [(ACT_RAISE, 0, 0) if isinstance(t, ActionError) else t for t in triples]
-        self._host_actions[0, :len(rows)] = np.asarray(rows, dtype=np.int32).reshape(-1, 3)
-        eng.actions.copy_(self.torch.from_numpy(self._host_actions))
         pre = self.game._state()  # the world the step starts from (its World.events are derived from it)
-        eng.load_python_random(0)
-        try:
-            eng.step()
-        finally:
-            eng.store_python_random(0)
-            self.game.invalidate()
-        # a debug raise stops World.step inside get_actions: no action ran, nothing died (core.py:96-99)
-        self.game.after_step(None if raising is not None else pre)
+        raising = None
+        if errors and self.debug:
+            for slot in pre.order[:pre.n_order]:
+                if int(slot) in errors:
+                    raising = int(slot)
+                    break
+        act = self._actions[0]
+        for i, t in enumerate(triples):
+            act[i] = (ACT_RAISE if self.debug else 0, 0, 0) if i in errors else t
+        rec = eng.host_record()
+        eng.host_step(self._actions, self._rng_in(), rec)
+        r = self._record(rec)
+        random.setstate(r.rng_state())
+        self.game.after_step(pre, r, errors, raising)
         if raising is not None:
-            raise raising.args[0]
-        obs = eng.obs[0].cpu().numpy()
-        rew = eng.rewards[0].cpu().numpy()
-        return obs, rew, bool(eng.done[0].item()), bool(eng.trunc[0].item())
+            raise errors[raising].args[0]
+        return r
 
     def observe(self):
-        eng = self.engine
-        eng.observe()
-        return eng.obs[0].cpu().numpy()
+        rec = self.engine.host_record()
+        self.engine.host_observe(rec)
+        return HostRecord(self.engine, rec[0], self._lay, self._np_obs).obs
 
     def close(self):
         self.engine.close()

@@ -102,44 +102,97 @@ __device__ __forceinline__ int state_words(const Dev& d) {
     return ZS_STATE_HEADER + ZS_STATE_ENTITY_WORDS * d.E + d.E + 2 * d.O + 2 * d.A + d.DW;
 }
 
-__global__ void k_get_state(Dev d, int e, int32_t* buf) {
-    if (threadIdx.x != 0) return;
+// env e's state record (layout: include/zombsole_mi355x.h), written by threads tid = 0..nt-1 of one workgroup
+__device__ void state_record(const Dev& d, int e, int32_t* b, int tid, int nt) {
     const int N = d.N, E = d.E;
-    int32_t* b = buf;
-    b[0] = d.scal[S_T * N + e];
-    b[1] = d.scal[S_DEATHS * N + e];
-    b[2] = d.scal[S_ZD * N + e];
-    b[3] = d.scal[S_EPSTEPS * N + e];
-    b[4] = d.scal[S_NORDER * N + e];
-    b[5] = d.scal[S_NEEDRESET * N + e];
-    b[6] = E;
-    b[7] = d.O;
-    b[8] = d.W;
-    b[9] = d.H;
-    b[10] = d.scal[S_PREVZD * N + e];
-    int nz = 0;
-    for (int s = d.A + d.P; s < E; s++) nz += d.present[EIX(d, s, e)];
-    b[11] = nz;
-    b[12] = d.scal[S_SERIAL * N + e];
-    b[13] = b[14] = b[15] = 0;
-    int32_t* r = b + ZS_STATE_HEADER;
-    for (int s = 0; s < E; s++, r += ZS_STATE_ENTITY_WORDS) {
-        int32_t p = d.pos[EIX(d, s, e)];
-        r[0] = s < d.A ? ZS_THING_AGENT : (s < d.A + d.P ? ZS_THING_PLAYER : ZS_THING_ZOMBIE);
-        r[1] = d.present[EIX(d, s, e)];
-        r[2] = unpack_x(p);
-        r[3] = unpack_y(p);
-        r[4] = d.life[EIX(d, s, e)];
-        r[5] = d.weapon[EIX(d, s, e)];
-        r[6] = s < d.A ? s : (s < d.A + d.P ? s - d.A : 0);
-        r[7] = (int32_t)d.serial[EIX(d, s, e)];
+    if (tid == 0) {
+        b[0] = d.scal[S_T * N + e];
+        b[1] = d.scal[S_DEATHS * N + e];
+        b[2] = d.scal[S_ZD * N + e];
+        b[3] = d.scal[S_EPSTEPS * N + e];
+        b[4] = d.scal[S_NORDER * N + e];
+        b[5] = d.scal[S_NEEDRESET * N + e];
+        b[6] = E;
+        b[7] = d.O;
+        b[8] = d.W;
+        b[9] = d.H;
+        b[10] = d.scal[S_PREVZD * N + e];
+        int nz = 0;
+        for (int s = d.A + d.P; s < E; s++) nz += d.present[EIX(d, s, e)];
+        b[11] = nz;
+        b[12] = d.scal[S_SERIAL * N + e];
+        b[13] = b[14] = b[15] = 0;
     }
-    for (int s = 0; s < E; s++) *r++ = d.order[EIX(d, s, e)];
-    for (int o = 0; o < d.O; o++) *r++ = d.obst_hp[(size_t)e * d.O + o];
-    for (int o = 0; o < d.O; o++) *r++ = (d.obst_present[(size_t)e * d.OW + (o >> 5)] >> (o & 31)) & 1u;
-    for (int a = 0; a < d.A; a++) *r++ = d.prev_life[(size_t)a * N + e];
-    for (int a = 0; a < d.A; a++) *r++ = d.listed[(size_t)a * N + e];
-    for (int w = 0; w < d.DW; w++) *r++ = (int32_t)d.dead[(size_t)e * d.DW + w];
+    int32_t* r = b + ZS_STATE_HEADER;
+    for (int s = tid; s < E; s += nt) {
+        int32_t* q = r + s * ZS_STATE_ENTITY_WORDS;
+        int32_t p = d.pos[EIX(d, s, e)];
+        q[0] = s < d.A ? ZS_THING_AGENT : (s < d.A + d.P ? ZS_THING_PLAYER : ZS_THING_ZOMBIE);
+        q[1] = d.present[EIX(d, s, e)];
+        q[2] = unpack_x(p);
+        q[3] = unpack_y(p);
+        q[4] = d.life[EIX(d, s, e)];
+        q[5] = d.weapon[EIX(d, s, e)];
+        q[6] = s < d.A ? s : (s < d.A + d.P ? s - d.A : 0);
+        q[7] = (int32_t)d.serial[EIX(d, s, e)];
+    }
+    r += ZS_STATE_ENTITY_WORDS * E;
+    for (int s = tid; s < E; s += nt) r[s] = d.order[EIX(d, s, e)];
+    r += E;
+    for (int o = tid; o < d.O; o += nt) r[o] = d.obst_hp[(size_t)e * d.O + o];
+    r += d.O;
+    for (int o = tid; o < d.O; o += nt) r[o] = (d.obst_present[(size_t)e * d.OW + (o >> 5)] >> (o & 31)) & 1u;
+    r += d.O;
+    for (int a = tid; a < d.A; a += nt) r[a] = d.prev_life[(size_t)a * N + e];
+    r += d.A;
+    for (int a = tid; a < d.A; a += nt) r[a] = d.listed[(size_t)a * N + e];
+    r += d.A;
+    for (int w = tid; w < d.DW; w += nt) r[w] = (int32_t)d.dead[(size_t)e * d.DW + w];
+}
+
+__global__ void k_get_state(Dev d, int e, int32_t* buf) { state_record(d, e, buf, threadIdx.x, blockDim.x); }
+
+// ---------------------------------------------------------------------------
+// the drop-ins' per-call path (zs_host_step / zs_host_reset / zs_host_observe): one workgroup per env
+// ---------------------------------------------------------------------------
+// the process-global `random` state moved in (rings[e]: the getstate() block and its successor, st[e])
+__global__ void k_host_unpack(Dev d, const uint32_t* rings, const uint32_t* st) {
+    const int e = blockIdx.x;
+    for (int k = threadIdx.x; k < ZS_RING_WORDS; k += blockDim.x)
+        d.ring[(size_t)e * ZS_RING_WORDS + k] = rings[(size_t)e * ZS_RING_WORDS + k];
+    if (threadIdx.x == 0) d.rngst[e] = st[e];
+}
+
+// Word offsets of a host record's sections (ZS_HOST_* in include/zombsole_mi355x.h, zs_host_layout)
+struct HostLayout {
+    int words, rew, alog, dlog, state, obs, obs_bytes, R;
+};
+
+// everything a call returns to the host, for env e: outputs, RNG stream, logs, state record, observation
+__global__ void k_host_pack(Dev d, HostLayout L, const uint8_t* obs, const double* rew, const uint8_t* done,
+                            const uint8_t* trunc, const uint8_t* rst, const int* err, int32_t* rec) {
+    const int e = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+    int32_t* r = rec + (size_t)e * L.words;
+    const uint32_t st = d.rngst[e];
+    if (tid == 0) {
+        r[ZS_HOST_FLAGS] = (done[e] ? 1 : 0) | (trunc[e] ? 2 : 0) | (rst && rst[e] ? 4 : 0);
+        r[ZS_HOST_ERR] = *err;
+        r[ZS_HOST_ALOG_N] = d.alog ? d.alog_n[e] : 0;
+        r[ZS_HOST_DLOG_N] = d.dlog ? d.dlog_n[e] : 0;
+        r[ZS_HOST_RNG + ZS_MT_N] = (int32_t)(st & 1023u);
+    }
+    const uint32_t* blk = d.ring + (size_t)e * ZS_RING_WORDS + ((st >> 10) & 1u) * ZS_MT_N;
+    for (int k = tid; k < ZS_MT_N; k += nt) r[ZS_HOST_RNG + k] = (int32_t)blk[k];
+    const int32_t* rw = (const int32_t*)(rew + (size_t)e * L.R);
+    for (int k = tid; k < 2 * L.R; k += nt) r[L.rew + k] = rw[k];
+    if (d.alog)
+        for (int k = tid; k < 2 * d.E; k += nt) r[L.alog + k] = d.alog[(size_t)e * d.E * 2 + k];
+    if (d.dlog)
+        for (int k = tid; k < 5 * d.E; k += nt) r[L.dlog + k] = d.dlog[(size_t)e * d.E * 5 + k];
+    state_record(d, e, r + L.state, tid, nt);
+    const uint16_t* src = (const uint16_t*)(obs + (size_t)e * L.obs_bytes);
+    uint16_t* dst = (uint16_t*)(r + L.obs);
+    for (int k = tid; k < L.obs_bytes / 2; k += nt) dst[k] = src[k];
 }
 
 __global__ void k_set_state(Dev d, int e, const int32_t* buf, int* err) {
@@ -294,6 +347,17 @@ struct zs_handle {
     int* d_fsctr = nullptr;  // k_fstep's finished-workgroup counter (zero between launches)
     int resident = 0;  // step-launch workgroups resident per CU (layout choice)
     int want = 0;      // workgroups per CU the launch has (capped at 32)
+    // the drop-ins' per-call path (zs_host_*), set up by its first call: one pinned input block
+    // (actions, then the `random` state as rings + st words) copied in, one pinned record block per env
+    // copied out, one synchronisation per call
+    HostLayout hl{};
+    int32_t* d_hin = nullptr;
+    int32_t* h_hin = nullptr;   // pinned
+    int32_t* d_hrec = nullptr;
+    int32_t* h_hrec = nullptr;  // pinned
+    uint8_t* d_hobs = nullptr;
+    double* d_hrew = nullptr;
+    uint8_t* d_hflags = nullptr;  // done [N], trunc [N], listed [N][A], reset [N]
     // diagnostics: HIP events bracketing every k_tick / k_obs launch on its stream
     int prof = 0;
     std::vector<hipEvent_t> ev_pool;
@@ -335,6 +399,9 @@ static int dupload(zs_handle* h, T** p, const std::vector<T>& v) {
 static void free_all(zs_handle* h) {
     for (void* p : h->allocs) (void)hipFree(p);
     h->allocs.clear();
+    if (h->h_hin) (void)hipHostFree(h->h_hin);
+    if (h->h_hrec) (void)hipHostFree(h->h_hrec);
+    h->h_hin = h->h_hrec = nullptr;
     if (h->ev_rfork) (void)hipEventDestroy(h->ev_rfork);
     if (h->ev_rjoin) (void)hipEventDestroy(h->ev_rjoin);
     h->ev_rfork = h->ev_rjoin = nullptr;
@@ -1180,10 +1247,8 @@ static int launch_respawn(zs_handle* h, hipStream_t s) {
     return ZS_OK;
 }
 
-extern "C" int zs_reset(zs_handle* h, const uint8_t* env_mask_dev, void* obs_dev, void* stream) {
-    if (!h) return fail(ZS_EINVAL, "null handle");
-    hipStream_t s = (hipStream_t)stream;
-    HIPCHK(hipSetDevice(h->device));
+// zs_reset's launches, queued on s (the caller synchronises and reads h->d_err)
+static int queue_reset(zs_handle* h, const uint8_t* env_mask_dev, void* obs_dev, hipStream_t s) {
     HIPCHK(hipMemsetAsync(h->d_err, 0, sizeof(int), s));
     int rc = launch_reset(h, 0, env_mask_dev, nullptr, s);
     if (rc) return rc;
@@ -1202,7 +1267,14 @@ extern "C" int zs_reset(zs_handle* h, const uint8_t* env_mask_dev, void* obs_dev
             h->rpar = q;
         }
     }
-    rc = launch_obs(h, obs_dev, env_mask_dev, s);
+    return launch_obs(h, obs_dev, env_mask_dev, s);
+}
+
+extern "C" int zs_reset(zs_handle* h, const uint8_t* env_mask_dev, void* obs_dev, void* stream) {
+    if (!h) return fail(ZS_EINVAL, "null handle");
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(hipSetDevice(h->device));
+    int rc = queue_reset(h, env_mask_dev, obs_dev, s);
     if (rc) return rc;
     int err = 0;
     HIPCHK(hipMemcpyAsync(&err, h->d_err, sizeof(int), hipMemcpyDeviceToHost, s));
@@ -1630,8 +1702,9 @@ extern "C" int zs_action_log(zs_handle* h, int32_t env, int32_t* out_host, int32
     int32_t n = 0;
     HIPCHK(hipMemcpyAsync(&n, h->d.alog_n + env, sizeof(int32_t), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
-    n = std::max(0, std::min(n, h->d.E));
-    const int k = std::min(n, std::max(0, (int)cap));
+    // n < 0: a debug raise stopped the step; -1 - n actors before the raising one decided an action
+    n = std::max(-1 - h->d.E, std::min(n, h->d.E));
+    const int k = std::min(n < 0 ? -1 - n : n, std::max(0, (int)cap));
     if (k > 0) {
         HIPCHK(hipMemcpyAsync(out_host, h->d.alog + (size_t)env * h->d.E * 2, sizeof(int32_t) * 2 * k,
                               hipMemcpyDeviceToHost, s));
@@ -1659,6 +1732,146 @@ extern "C" int zs_death_log(zs_handle* h, int32_t env, int32_t* out_host, int32_
     }
     *n_out = n;
     return ZS_OK;
+}
+
+// ---------------------------------------------------------------------------
+// The drop-ins' per-call path.  The reference's env.step / env.reset / env.get_observation run one env
+// per call on the host (gym_env.py:99-164, gym/multiagent_env.py:111-184) and share the process-global
+// `random` stream.  Here one call is: the caller's actions and `random` state packed into one pinned
+// block and copied in, the engine's launches, k_host_pack writing everything the host reads back
+// (outputs, the advanced stream, the action / death logs, the state record, the observation) into one
+// record per env, one copy out and one synchronisation.
+// ---------------------------------------------------------------------------
+static int obs_bytes_per_env(const zs_handle* h) {
+    int32_t shp[4];
+    zs_obs_shape(h, shp);
+    const int ts = h->d.obs_dtype == ZS_DTYPE_I64 ? 8 : h->d.obs_dtype == ZS_DTYPE_I32 ? 4 : 2;
+    return shp[0] * shp[1] * shp[2] * shp[3] * ts;
+}
+
+static HostLayout host_layout(const zs_handle* h) {
+    const Dev& d = h->d;
+    HostLayout L;
+    L.R = d.reward_mode == ZS_REWARD_SINGLE ? 1 : d.A;
+    L.obs_bytes = obs_bytes_per_env(h);
+    L.rew = ZS_HOST_RNG + ZS_MT_N + 2;  // even: the rewards are float64
+    L.alog = L.rew + 2 * L.R;
+    L.dlog = L.alog + 2 * d.E;
+    L.state = L.dlog + 5 * d.E;
+    L.obs = (L.state + h->state_words + 1) & ~1;  // 8-byte aligned
+    L.words = (L.obs + (L.obs_bytes + 3) / 4 + 1) & ~1;
+    return L;
+}
+
+static int host_init(zs_handle* h) {
+    if (h->d_hrec) return ZS_OK;
+    const Dev& d = h->d;
+    const size_t N = d.N;
+    HostLayout L = host_layout(h);
+    const size_t in_words = N * d.A * 3 + N * (ZS_RING_WORDS + 1);
+    int rc;
+    if ((rc = dalloc(h, &h->d_hin, in_words)) || (rc = dalloc(h, &h->d_hobs, N * L.obs_bytes)) ||
+        (rc = dalloc(h, &h->d_hrew, N * L.R)) || (rc = dalloc(h, &h->d_hflags, N * (3 + d.A))) ||
+        (rc = dalloc(h, &h->d_hrec, N * L.words)))
+        return rc;
+    HIPCHK(hipHostMalloc((void**)&h->h_hin, in_words * sizeof(int32_t), hipHostMallocDefault));
+    HIPCHK(hipHostMalloc((void**)&h->h_hrec, N * L.words * sizeof(int32_t), hipHostMallocDefault));
+    h->hl = L;
+    return ZS_OK;
+}
+
+// the `random` states of envs [0, N) (CPython getstate() form, 625 words each) into the pinned input
+// block after the actions: per env its ring (the block, then its successor) and its st word
+static int host_stage_rng(zs_handle* h, const uint32_t* rng_host, size_t* in_words) {
+    const size_t N = h->d.N;
+    uint32_t* rings = (uint32_t*)h->h_hin + N * h->d.A * 3;
+    uint32_t* st = rings + N * ZS_RING_WORDS;
+    for (size_t e = 0; e < N; e++) {
+        const uint32_t* g = rng_host + e * (ZS_MT_N + 1);
+        if (g[ZS_MT_N] > ZS_MT_N) return fail(ZS_EINVAL, "MT index out of range (0..624)");
+        uint32_t* r = rings + e * ZS_RING_WORDS;
+        std::memcpy(r, g, sizeof(uint32_t) * ZS_MT_N);
+        for (int k = 0; k < ZS_MT_N; k++) {  // x[k+624] = x[k+397] ^ f(x[k], x[k+1])
+            uint32_t a = r[k], b = r[k + 1], c = r[k + ZS_MT_M];
+            uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
+            r[ZS_MT_N + k] = c ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+        }
+        st[e] = g[ZS_MT_N] | (0u << 10) | (1u << 11);
+    }
+    *in_words = N * h->d.A * 3 + N * (ZS_RING_WORDS + 1);
+    return ZS_OK;
+}
+
+enum { HOST_STEP = 0, HOST_RESET = 1, HOST_OBSERVE = 2 };
+
+static int host_call(zs_handle* h, int op, const int32_t* actions_host, const uint32_t* rng_host, int32_t* rec_host,
+                     hipStream_t s) {
+    HIPCHK(hipSetDevice(h->device));
+    int rc = host_init(h);
+    if (rc) return rc;
+    const Dev& d = h->d;
+    const size_t N = d.N;
+    const HostLayout& L = h->hl;
+    size_t in_words = 0;
+    if (op == HOST_STEP) {
+        std::memcpy(h->h_hin, actions_host, sizeof(int32_t) * N * d.A * 3);
+        in_words = N * d.A * 3;
+    }
+    if (rng_host && (rc = host_stage_rng(h, rng_host, &in_words))) return rc;
+    if (in_words) HIPCHK(hipMemcpyAsync(h->d_hin, h->h_hin, in_words * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    if (rng_host) {
+        const uint32_t* rings = (const uint32_t*)h->d_hin + N * d.A * 3;
+        hipLaunchKernelGGL(k_host_unpack, dim3((unsigned)N), dim3(256), 0, s, h->d, rings, rings + N * ZS_RING_WORDS);
+        HIPCHK(hipGetLastError());
+    }
+    uint8_t *done = h->d_hflags, *trunc = done + N, *rst = trunc + N, *listed = rst + N;
+    if (op == HOST_STEP) {
+        HIPCHK(hipMemsetAsync(h->d_err, 0, sizeof(int), s));
+        rc = zs_step(h, h->d_hin, h->d_hobs, h->d_hrew, done, trunc, listed, rst, s);
+    } else if (op == HOST_RESET) {
+        HIPCHK(hipMemsetAsync(h->d_hflags, 0, N * 3, s));
+        HIPCHK(hipMemsetAsync(h->d_hrew, 0, N * L.R * sizeof(double), s));
+        rc = queue_reset(h, nullptr, h->d_hobs, s);
+    } else {
+        HIPCHK(hipMemsetAsync(h->d_err, 0, sizeof(int), s));
+        rc = launch_obs(h, h->d_hobs, nullptr, s);
+    }
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_host_pack, dim3((unsigned)N), dim3(256), 0, s, h->d, L, (const uint8_t*)h->d_hobs,
+                       (const double*)h->d_hrew, (const uint8_t*)done, (const uint8_t*)trunc,
+                       op == HOST_RESET ? nullptr : (const uint8_t*)rst, (const int*)h->d_err, h->d_hrec);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(h->h_hrec, h->d_hrec, N * L.words * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    std::memcpy(rec_host, h->h_hrec, N * L.words * sizeof(int32_t));
+    const int err = h->h_hrec[ZS_HOST_ERR];
+    if (err == ZS_ENOSPACE) return fail(ZS_ENOSPACE, "Not enough space to spawn players/agents");
+    if (err) return fail(err, "reset failed");
+    return ZS_OK;
+}
+
+extern "C" int zs_host_layout(zs_handle* h, int32_t out[8]) {
+    if (!h || !out) return fail(ZS_EINVAL, "null argument");
+    const HostLayout L = host_layout(h);
+    const int32_t v[8] = {L.words, L.rew, L.alog, L.dlog, L.state, L.obs, L.obs_bytes, L.R};
+    std::memcpy(out, v, sizeof(v));
+    return ZS_OK;
+}
+
+extern "C" int zs_host_step(zs_handle* h, const int32_t* actions_host, const uint32_t* rng_host, int32_t* rec_host,
+                            void* stream) {
+    if (!h || !actions_host || !rec_host) return fail(ZS_EINVAL, "null argument");
+    return host_call(h, HOST_STEP, actions_host, rng_host, rec_host, (hipStream_t)stream);
+}
+
+extern "C" int zs_host_reset(zs_handle* h, const uint32_t* rng_host, int32_t* rec_host, void* stream) {
+    if (!h || !rec_host) return fail(ZS_EINVAL, "null argument");
+    return host_call(h, HOST_RESET, nullptr, rng_host, rec_host, (hipStream_t)stream);
+}
+
+extern "C" int zs_host_observe(zs_handle* h, int32_t* rec_host, void* stream) {
+    if (!h || !rec_host) return fail(ZS_EINVAL, "null argument");
+    return host_call(h, HOST_OBSERVE, nullptr, nullptr, rec_host, (hipStream_t)stream);
 }
 
 // Diagnostics: the work-list counters as they stand after everything queued on `stream` (out[0..1]

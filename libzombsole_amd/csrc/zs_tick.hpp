@@ -1098,7 +1098,15 @@ __device__ __forceinline__ void env_step_leader(const Dev& d, Grp& c, const int3
             c.fin = 0;
             c.respawn = 0;
             MISC(c, MISC_NMOVED) = -1;  // no cleanup, no second leader part
-            if (d.alog) d.alog_n[c.e] = 0;
+            if (d.alog) {  // the actors before it that decided an action, in dict order; -1 - their count
+                int32_t* al = d.alog + (size_t)c.e * d.E * 2;
+                for (int j = 0; j < nact; j++) {
+                    const int sj = LPE(c, j);
+                    al[2 * j] = sj | (LK(c, sj) << 8);
+                    al[2 * j + 1] = LT(c, sj);
+                }
+                d.alog_n[c.e] = -1 - nact;
+            }
             return;
         }
         if (LK(c, s) == K_DEFER) {

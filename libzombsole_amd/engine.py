@@ -14,7 +14,8 @@ from . import _abi
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_build", "libzombsole_mi355x.so")
 SYMBOLS = ["zs_last_error", "zs_create", "zs_destroy", "zs_obs_shape", "zs_seed", "zs_reset", "zs_step", "zs_observe",
            "zs_gen_actions", "zs_step_graph", "zs_step_graph_n", "zs_state_size", "zs_get_state", "zs_set_state", "zs_get_rng", "zs_set_rng", "zs_overflow", "zs_profile", "zs_profile_read", "zs_describe",
-           "zs_debug_stamps", "zs_debug_stamps_wg", "zs_debug_timeline", "zs_debug_lists", "zs_death_log", "zs_action_log"]
+           "zs_debug_stamps", "zs_debug_stamps_wg", "zs_debug_timeline", "zs_debug_lists", "zs_death_log", "zs_action_log",
+           "zs_host_layout", "zs_host_step", "zs_host_reset", "zs_host_observe"]
 
 _lib = None
 
@@ -65,6 +66,10 @@ def load_library(path=None):
     L.zs_action_log.argtypes = [vp, i32, C.POINTER(i32), i32, C.POINTER(i32), vp]
     L.zs_debug_timeline.argtypes = [vp, vp, i32]
     L.zs_debug_stamps_wg.argtypes = [vp, vp, i32, i32]
+    L.zs_host_layout.argtypes = [vp, C.POINTER(i32)]
+    L.zs_host_step.argtypes = [vp, vp, vp, vp, vp]
+    L.zs_host_reset.argtypes = [vp, vp, vp, vp]
+    L.zs_host_observe.argtypes = [vp, vp, vp]
     for s in SYMBOLS:
         if s != "zs_last_error":
             getattr(L, s).restype = C.c_int
@@ -96,6 +101,28 @@ def _raise(L, rc, what):
 
 def _ptr(t):
     return C.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _np_ptr(a):
+    """A host buffer argument: None, bytes (e.g. struct-packed) or a numpy array."""
+    if a is None or isinstance(a, bytes):
+        return a
+    return C.c_void_p(a.ctypes.data)
+
+
+def decode_action_log(words, n, E):
+    """(actions, raised) from zs_action_log's words and count (n < 0: a debug raise, -1 - n entries)."""
+    raised = n < 0
+    k = min(-1 - n if raised else n, E)
+    w = words[:2 * k].tolist()
+    return [(w[2 * j] & 0xff, (w[2 * j] >> 8) & 0xff, w[2 * j + 1]) for j in range(k)], raised
+
+
+def decode_death_log(words, n, E):
+    """[(slot, serial, x, y, life)] from zs_death_log's words and count."""
+    k = max(0, min(n, E))
+    w = words[:5 * k].tolist()
+    return [tuple(w[5 * j:5 * j + 5]) for j in range(k)]
 
 
 class Engine(object):
@@ -286,19 +313,59 @@ class Engine(object):
         rc = self.L.zs_death_log(self.h, int(env), out, int(self.E), C.byref(n), self._stream())
         if rc:
             _raise(self.L, rc, "zs_death_log")
-        return [tuple(int(v) for v in out[5 * k:5 * k + 5]) for k in range(min(n.value, self.E))]
+        return decode_death_log(np.frombuffer(out, dtype=np.int32), n.value, self.E)
 
     def action_log(self, env):
         """The actions env's last step executed, in execution order (core.py:76,103-119): a list of
         (slot, kind, target), kind 1 move (target: destination x | y << 16), 2 attack, 3 heal (target: an
-        entity slot, or -1 - obstacle index).  Needs a config with FLAG_DEATH_LOG."""
+        entity slot, or -1 - obstacle index).  Needs a config with FLAG_DEATH_LOG.  Returns (actions, raised):
+        raised when a debug raise stopped the step, the actions then being the decided actions of the actors
+        before the raising one, in dict order."""
         out = (C.c_int32 * (2 * max(1, self.E)))()
         n = C.c_int32(0)
         rc = self.L.zs_action_log(self.h, int(env), out, int(self.E), C.byref(n), self._stream())
         if rc:
             _raise(self.L, rc, "zs_action_log")
-        return [(int(out[2 * k]) & 0xff, (int(out[2 * k]) >> 8) & 0xff, int(out[2 * k + 1]))
-                for k in range(min(n.value, self.E))]
+        return decode_action_log(np.frombuffer(out, dtype=np.int32), n.value, self.E)
+
+    # -- the drop-ins' per-call path (zs_host_*): one copy in, one copy out, one synchronisation ----------
+    def host_layout(self):
+        """Word offsets of a zs_host_* record's sections (zs_host_layout)."""
+        if getattr(self, "_hl", None) is None:
+            out = (C.c_int32 * 8)()
+            rc = self.L.zs_host_layout(self.h, out)
+            if rc:
+                _raise(self.L, rc, "zs_host_layout")
+            self._hl = dict(zip(("words", "rew", "alog", "dlog", "state", "obs", "obs_bytes", "R"), [int(v) for v in out]))
+        return self._hl
+
+    def host_record(self):
+        """A fresh record buffer for one zs_host_* call over all N envs (int32 [N][words])."""
+        return np.empty((self.N, self.host_layout()["words"]), dtype=np.int32)
+
+    def host_step(self, actions, rng, rec):
+        """zs_host_step: actions int32 [N, A, 3] (host), rng [N][625] uint32 words (random.getstate() form;
+        a numpy array or packed bytes) or None, rec from host_record() (filled)."""
+        a = np.ascontiguousarray(actions, dtype=np.int32)
+        rc = self.L.zs_host_step(self.h, C.c_void_p(a.ctypes.data), _np_ptr(rng), C.c_void_p(rec.ctypes.data),
+                                 self._stream())
+        if rc:
+            _raise(self.L, rc, "zs_host_step")
+        return rec
+
+    def host_reset(self, rng, rec):
+        """zs_host_reset: every env rebuilt (Game.__initialize_world__), record filled.  On ZS_ENOSPACE the
+        record still holds the envs' streams (the caller moves them back before re-raising)."""
+        rc = self.L.zs_host_reset(self.h, _np_ptr(rng), C.c_void_p(rec.ctypes.data), self._stream())
+        if rc:
+            _raise(self.L, rc, "zs_host_reset")
+        return rec
+
+    def host_observe(self, rec):
+        rc = self.L.zs_host_observe(self.h, C.c_void_p(rec.ctypes.data), self._stream())
+        if rc:
+            _raise(self.L, rc, "zs_host_observe")
+        return rec
 
     def get_state(self, env):
         buf = np.zeros(self.state_words, dtype=np.int32)
@@ -360,27 +427,37 @@ class Engine(object):
 
 class StepOutputs(object):
     """One set of zs_step output buffers, `rows` >= N rows (rows past N are padding the engine never
-    writes: equal-sized shards for a collective).  Rewards, done and truncated live in one flat byte
-    tensor (`flat`: float64 rewards [rows][R], then done [rows], then truncated [rows]) so a per-step
-    exchange moves them in one collective."""
+    writes: equal-sized shards for a collective).  Everything but the observations lives in one flat byte
+    tensor (`flat`), so a per-step exchange moves it in one collective (obs + reward +
+    done/trunc/alive): float64 rewards [rows][R], then done [rows], truncated [rows], listed [rows][A] (the
+    agents alive before the step: the keys of the reference's per-agent dicts, gym/multiagent_env.py:156-169)
+    and was_reset [rows] (the observation is a reset's)."""
+
+    @staticmethod
+    def row_bytes(eng):
+        R = eng.A if eng.multi else 1
+        return 8 * R + 3 + eng.A
 
     def __init__(self, eng, rows, obs=None, flat=None):
         torch = eng.torch
         kw = dict(device=eng.device)
         R = eng.A if eng.multi else 1
+        A = eng.A
         self.rows = rows
+        nb = rows * self.row_bytes(eng)
         if obs is not None:
             assert obs.shape == (rows,) + tuple(eng.obs_shape) and obs.dtype == eng.obs_dtype and obs.is_contiguous()
         if flat is not None:
-            assert flat.dim() == 1 and flat.numel() >= rows * (8 * R + 2) and flat.dtype == torch.uint8
+            assert flat.dim() == 1 and flat.numel() >= nb and flat.dtype == torch.uint8
             assert flat.is_contiguous() and flat.storage_offset() % 8 == 0
         self.obs = obs if obs is not None else torch.zeros((rows,) + eng.obs_shape, dtype=eng.obs_dtype, **kw)
-        self.flat = flat if flat is not None else torch.zeros(rows * (8 * R + 2), dtype=torch.uint8, **kw)
-        self.rewards = self.flat[:8 * R * rows].view(torch.float64).view(rows, R)
-        self.done = self.flat[8 * R * rows:(8 * R + 1) * rows]
-        self.trunc = self.flat[(8 * R + 1) * rows:(8 * R + 2) * rows]
-        self.listed = torch.zeros((rows, eng.A), dtype=torch.uint8, **kw)
-        self.was_reset = torch.zeros(rows, dtype=torch.uint8, **kw)
+        self.flat = flat if flat is not None else torch.zeros(nb, dtype=torch.uint8, **kw)
+        o = 8 * R * rows
+        self.rewards = self.flat[:o].view(torch.float64).view(rows, R)
+        self.done = self.flat[o:o + rows]
+        self.trunc = self.flat[o + rows:o + 2 * rows]
+        self.listed = self.flat[o + 2 * rows:o + (2 + A) * rows].view(rows, A)
+        self.was_reset = self.flat[o + (2 + A) * rows:o + (3 + A) * rows]
 
 
 class StateView(object):

@@ -8,6 +8,7 @@ re-evaluate the reference's predicates (`rules/*.py`) on that state so that
 `env.game.rules.game_won()` answers like the reference after a step.
 """
 from . import _abi
+from .engine import StateView
 from .maps import Map, load_map  # noqa: F401  (reference: zombsole.game.Map)
 from .things import OBSTACLE_CLASSES, Agent, DeadBody, ObjectiveLocation, Player, Zombie, weapon_for_code, weapon_r2
 
@@ -44,9 +45,24 @@ class WorldView(object):
         self._game = game
         self.size = tuple(game.map.size)
         self.debug = game.debug
-        # World.event's log (core.py:68-70): (t, thing, message) per idle actor, executed action and death,
-        # appended by GameView.after_step from the engine's action and death logs
-        self.events = []
+        # World.event's log (core.py:68-70): (t, thing, message) per idle actor, next_step error, executed
+        # action and death.  GameView.after_step queues each step's logs; the messages are formed when the
+        # log is read
+        self._events = []
+        self._pending = []
+
+    @property
+    def events(self):
+        if self._pending:
+            for p in self._pending:
+                self._events.extend(self._game._step_events(*p))
+            self._pending = []
+        return self._events
+
+    @events.setter
+    def events(self, value):
+        self._pending = []
+        self._events = value
 
     t = property(lambda s: s._game._state().t)
     deaths = property(lambda s: s._game._state().deaths)
@@ -233,7 +249,7 @@ class GameView(object):
         views = getattr(self, "_views", None)
         if not views:
             return
-        st = self.engine.get_state(self.env)
+        st = self._state()
         for slot, v in views.items():
             if v._gone:
                 continue
@@ -243,10 +259,10 @@ class GameView(object):
             v._gone = True
         self._views = {}
 
-    def new_episode(self):
+    def new_episode(self, state_buf=None):
         """Fresh objects after a reset (the reference builds a new World and new players,
-        game.py:151-169)."""
-        self._cache = None
+        game.py:151-169); `state_buf` is the reset's state record, when the caller has it."""
+        self._cache = None if state_buf is None else StateView(self.engine, state_buf)
         # World.decoration's keys in insertion order -> the name of the body on the cell (None: the
         # objective spawned there by the map, game.py:151-155)
         self._deco = {tuple(p): None for p in self.map.objectives}
@@ -260,46 +276,54 @@ class GameView(object):
             self._views[A + j] = p
         self.world = WorldView(self)
 
-    def after_step(self, pre=None):
-        """Book-keeping of a step the env took (EnvCore.tick): the bodies its cleanup left, in the
-        order it removed the things (core.py:121-128), the final values of the removed things into
-        their views (a removed zombie's slot may be reused by the same step's respawn), and, given the
-        state record from before the step (`pre`), the step's World.events."""
+    def after_step(self, pre, rec, errors=None, raising=None):
+        """Book-keeping of a step the env took (EnvCore.tick), from the state record `pre` of the world the
+        step started from and the step's host record `rec`: the bodies its cleanup left, in the order it
+        removed the things (core.py:121-128), the final values of the removed things into their views (a
+        removed zombie's slot may be reused by the same step's respawn), the state after the step, and the
+        step's World.events, queued (`errors`: the agents' next_step errors by slot; `raising`: the slot whose
+        error a debug env re-raised)."""
         actors = {}
-        if pre is not None:  # the objects in the world while the step ran
-            for slot in pre.order[:pre.n_order]:
-                slot = int(slot)
-                v = self._views.get(slot)
-                if v is None or v._serial != int(pre.ent[slot][7]):
-                    v = Zombie(self, slot, row=pre.ent[slot])
-                    self._views[slot] = v
-                actors[slot] = v
-        deaths = self.engine.death_log(self.env)
+        for slot in pre.order[:pre.n_order]:  # the objects in the world while the step ran
+            slot = int(slot)
+            v = self._views.get(slot)
+            if v is None or v._serial != int(pre.ent[slot][7]):
+                v = Zombie(self, slot, row=pre.ent[slot])
+                self._views[slot] = v
+            actors[slot] = v
+        deaths = rec.death_log()
         for slot, serial, x, y, life in deaths:
             v = self._views.get(slot)
             if v is not None and v._serial == serial:
                 v._finalize(x, y, life)
             # things.py:64,118 (agents and bots always have a view; a zombie slot may have none)
             self._deco[(x, y)] = ("dead " + v.name) if isinstance(v, Player) else "zombie remains"
-        if pre is not None:
-            self._log_events(pre, actors, deaths)
+        post = StateView(self.engine, rec.state_buf)
+        self._cache = post
+        self.world._pending.append((pre, post, actors, deaths, rec.action_log(), errors or {}, raising))
 
-    def _log_events(self, pre, actors, deaths):
-        """The step's World.event records (core.py:68-70) in the reference's order: 'idle' for every actor
-        whose next_step gave no action, in dict order (core.py:80-101); each executed action's result in
-        execution order (core.py:103-119, the messages of thing_move / thing_attack / thing_heal,
+    def _step_events(self, pre, post, actors, deaths, alog, errors, raising):
+        """One step's World.event records (core.py:68-70) in the reference's order: for every actor in dict
+        order whose next_step gave no action, 'idle', or 'error with next_step: <err>' when it raised
+        (core.py:80-101; a debug env stops at the first error, core.py:96-99); each executed action's result
+        in execution order (core.py:103-119, the messages of thing_move / thing_attack / thing_heal,
         core.py:140-202), with positions and occupancy followed through the step's moves; 'died' for every
         thing the cleanup removed, obstacles first in map order, then the others in dict order
-        (core.py:121-138).  The actions and their order come from the engine (zs_action_log); the
-        messages are their outcomes against the state from before the step."""
+        (core.py:121-138).  The actions and their order come from the engine (zs_action_log); the messages
+        are their outcomes against the state from before the step."""
         t = pre.t + 1
         W, H = self.world.size
-        alog = self.engine.action_log(self.env)
+        acts, _ = alog
         ev = []
-        acted = set(a[0] for a in alog)
+        acted = set(a[0] for a in acts)
         for slot in pre.order[:pre.n_order]:
-            if int(slot) not in acted:
-                ev.append((t, actors[int(slot)], u"idle"))
+            slot = int(slot)
+            if slot in errors:
+                ev.append((t, actors[slot], u"error with next_step: %s" % str(errors[slot].args[0])))
+                if slot == raising:
+                    return ev
+            elif slot not in acted:
+                ev.append((t, actors[slot], u"idle"))
         pos, occ = {}, {}
         for i, ob in enumerate(self._obstacles):
             if pre.obst_present[i]:
@@ -312,7 +336,7 @@ class GameView(object):
         def target(tgt):
             return (self._obstacles[-1 - tgt], self._obstacles[-1 - tgt].position) if tgt < 0 else (actors[tgt], pos[tgt])
 
-        for slot, kind, tgt in alog:
+        for slot, kind, tgt in acts:
             me, (x, y) = actors[slot], pos[slot]
             if kind == 1:  # thing_move (core.py:140-166)
                 dx, dy = tgt & 0xffff, tgt >> 16
@@ -343,7 +367,6 @@ class GameView(object):
                 else:
                     msg = u"healed " + tg.name
             ev.append((t, me, msg))
-        post = self._state()
         for i, ob in enumerate(self._obstacles):
             if pre.obst_present[i] and not post.obst_present[i]:
                 ev.append((t, ob, u"died"))
@@ -351,7 +374,7 @@ class GameView(object):
             v = actors.get(slot)
             if v is not None and v._serial == serial:
                 ev.append((t, v, u"died"))
-        self.world.events.extend(ev)
+        return ev
 
     def _entity(self, slot):
         v = self._views.get(slot)

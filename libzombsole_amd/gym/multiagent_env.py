@@ -68,7 +68,6 @@ class MultiagentZombsoleEnv(object):
         self._core = EnvCore(builder, builder.map, rules_name, player_names, self._ids, names,
                              initial_zombies, minimum_zombies, debug, device)
         self.frames_per_second = None
-        self._obs = self._core.engine.obs[0].cpu().numpy()
 
     @property
     def game(self):
@@ -110,23 +109,23 @@ class MultiagentZombsoleEnv(object):
             agent_action = agent_actions.get(agent.agent_id, {"action_type": "heal", "parameter": [0, 0]})
             agent.set_action(agent_action)
             triples.append(self._core.encode(agent_action))
-        obs, rew, doneflag, truncatedflag = self._core.tick(triples)
+        r = self._core.tick(triples)
 
         rewards = {}
         for i, aid in enumerate(self._ids):
             if aid in self.agents:
-                rewards[aid] = float(rew[i])
-        observations = self._observations(obs)
-        done = {agent_id: doneflag for agent_id in self.agents}
-        truncated = {agent_id: truncatedflag for agent_id in self.agents}
+                rewards[aid] = float(r.rewards[i])
+        observations = self._observations(r.obs)
+        done = {agent_id: r.done for agent_id in self.agents}
+        truncated = {agent_id: r.trunc for agent_id in self.agents}
         self.agents = [agent.agent_id for agent in self.game.agents if agent.life > 0]
         return observations, rewards, done, truncated, {}
 
     def reset(self, seed=None, options=None):
         """gym/multiagent_env.py:173-184"""
         self.agents = self.possible_agents
-        self._core.new_world()
-        return self._observations(self._core.engine.obs[0].cpu().numpy()), {}
+        r = self._core.new_world()
+        return self._observations(r.obs), {}
 
     def render(self):
         if self.render_mode == 'human':

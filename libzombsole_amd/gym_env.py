@@ -79,17 +79,16 @@ class ZombsoleGymEnv(Env):
     def step(self, action):
         """gym_env.py:99-145: set_action, World.step, reward, respawn, obs, rules, end reward."""
         self.game.agents[0].set_action(action)
-        triple = self._core.encode(action)
-        obs, rew, done, truncated = self._core.tick([triple])
+        r = self._core.tick([self._core.encode(action)])
         self._check_id()
-        return obs[0], float(rew[0]), done, truncated, {}
+        return r.obs[0], float(r.rewards[0]), r.done, r.trunc, {}
 
     def reset(self, seed=None, options=None):
         """gym_env.py:148-164"""
         super().reset(seed=seed)
-        self._core.new_world()
+        r = self._core.new_world()
         self._check_id()
-        return self._core.engine.obs[0, 0].cpu().numpy(), {}
+        return r.obs[0], {}
 
     def render(self):
         if self.render_mode == 'human':

@@ -162,12 +162,14 @@ class StepGather(object):
     """C5's per-step exchange for a centralised learner, overlapped with the next
     step's compute.
 
-    Every rank's observation shard plus its rewards / done / truncated are all-gathered into node-wide
-    tensors.  The engine writes each step into one of `depth` output sets (Engine.outputs) whose storage
+    Every rank's observation shard plus its rewards / done / truncated / listed / was_reset are
+    all-gathered into node-wide tensors (obs + reward + done/trunc/alive; `listed` says
+    which agents' rewards and observations are valid — the agents alive before the step, whose keys the
+    reference's dicts carry, gym/multiagent_env.py:156-169 — and `was_reset` which observations are a reset's).
+    The engine writes each step into one of `depth` output sets (Engine.outputs) whose storage
     is this rank's slice of that set's gather buffers, padded to the longest shard, so the exchange copies
     nothing: the collectives run in place (a rank receives the other ranks' slices only), the observations
-    one collective and rewards / done / truncated (one flat byte tensor per set, engine.StepOutputs) a
-    second.  Step t
+    one collective and the rest (one flat byte tensor per set, engine.StepOutputs) a second.  Step t
     writes set t % depth on the caller's stream; its collectives are issued on a communication stream
     that waits for that step only, so they run while step t + 1 computes into the next set; before a
     set is written again the caller's stream waits for the collectives that read it.  With gloo (CPU
@@ -176,6 +178,7 @@ class StepGather(object):
         g = StepGather(eng)
         g.step(lambda out: eng.step_graph(t, 7, out=out))   # per step
         g.obs(), g.rewards(), g.done(), g.truncated()      # the last step's node-wide tensors
+        g.listed(), g.was_reset()
 
     The tensors obs() returns are the exchange buffers themselves when every shard has the same size
     (no copy): they hold step t's values until the exchange of step t + depth overwrites them, and are
@@ -199,7 +202,9 @@ class StepGather(object):
         dev = engine.device
         rank = dist.get_rank(group)
         shape = tuple(engine.obs_shape)
-        nflat = (self.m * (8 * self.R + 2) + 15) // 16 * 16  # a rank's segment; the float64 rewards 8-B aligned
+        self.A = engine.A
+        # a rank's segment of the flat exchange buffer (engine.StepOutputs); the float64 rewards 8-B aligned
+        nflat = (self.m * (8 * self.R + 3 + self.A) + 15) // 16 * 16
         self.g_obs = [torch.zeros((self.world * self.m,) + shape, dtype=engine.obs_dtype, device=dev)
                       for _ in range(self.depth)]
         self.g_flat = [torch.zeros(self.world * nflat, dtype=torch.uint8, device=dev) for _ in range(self.depth)]
@@ -282,3 +287,13 @@ class StepGather(object):
 
     def truncated(self):
         return self._flat(8 * self.R + 1, 8 * self.R + 2).view(-1)
+
+    def listed(self):
+        """[N, A] uint8: agent a of env e was alive before the step (its reward and observation are valid)."""
+        o = 8 * self.R + 2
+        return self._flat(o, o + self.A)
+
+    def was_reset(self):
+        """[N] uint8: env e's observation is the one its autoreset produced this step."""
+        o = 8 * self.R + 2 + self.A
+        return self._flat(o, o + 1).view(-1)

@@ -160,6 +160,26 @@ CONFIGS = [
      dict(rules_name="extermination", player_names=[], map_name="fort",
           agent_ids=[str(i) for i in range(8)], initial_zombies=40, minimum_zombies=20), [45], 60, 1, 0,
      {"events": True}),
+    # C1 (BASELINE.json configs[0]): the real bridge, extermination, agents ["0", "1"], 10 zombies, through
+    # MultiagentZombsoleEnv(DiscreteAction) — the uniform Discrete(7) stream and the rich dict stream
+    ("multi_bridge_a2_z10", "multi", "discrete",
+     dict(rules_name="extermination", player_names=[], map_name="bridge",
+          agent_ids=["0", "1"], initial_zombies=10, minimum_zombies=0), [0, 1, 2], 200, 2, 0),
+    ("multi_bridge_a2_z10_rich", "multi", "rich",
+     dict(rules_name="extermination", player_names=[], map_name="bridge",
+          agent_ids=["0", "1"], initial_zombies=10, minimum_zombies=0), [3, 4], 150, 2, 0, {"events": True}),
+    # next_step errors in World.events (core.py:96-99): without debug the agent's error is logged in place of
+    # 'idle' and the step goes on; with debug the actors before it are logged, then its error, and the step
+    # stops (that step's events land in the next recorded step's slice of the log)
+    ("events_multi_bridge_a3_bad", "multi", "bad",
+     dict(rules_name="extermination", player_names=["terminator"], map_name="bridge",
+          agent_ids=["0", "1", "2"], initial_zombies=10, minimum_zombies=5), [51, 52], 100, 1, 0,
+     {"events": True}),
+    ("events_single_easyexit_debug_bad", "single", "bad",
+     dict(rules_name="survival", player_names=["hamster", "randoman", "troll"], map_name="easy_exit",
+          agent_id=0, initial_zombies=6, minimum_zombies=4, observation_scope="surroundings:7",
+          observation_position_encoding="channels", agent_weapon="random", debug=True), [53], 120, 1, 50,
+     {"events": True}),
 ]
 
 

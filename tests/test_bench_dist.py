@@ -89,3 +89,35 @@ def test_bench_two_rank_control_flow():
     # every rank reports the slowest rank's time; the closing barrier already stretches the fast rank's
     # window over the slow rank's 20 steps of 4 ms
     assert m0 == m1 == max(e0, e1) and min(e0, e1) >= 20 * 0.004
+
+
+def _bench(argv, env_extra=None, drop=("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT", "TORCHELASTIC_RUN_ID")):
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in drop}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(root, "bench.py")] + argv, cwd=root, env=env,
+                          capture_output=True, text=True, timeout=240)
+
+
+def test_bench_gpus_flag_spawns_the_ranks():
+    """`bench.py --gpus 2` with no launcher starts the two rank processes itself (RANK / WORLD_SIZE /
+    MASTER_* as torchrun sets them); rank 0's JSON line reports both ranks' env ranges and n_gpus 2."""
+    import json
+    r = _bench(["--gpus", "2", "--dry-run", "--steps", "6", "--warmup", "2", "--envs", "65537"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["dry_run"] and out["total_envs"] == 65537
+    assert [tuple(x) for x in out["rank_env_ranges"]] == [(0, 32769), (32769, 32768)]
+
+
+def test_bench_gpus_flag_must_match_launcher():
+    """Under a launcher (WORLD_SIZE set) a different --gpus is an error, not a silent 1-rank run."""
+    r = _bench(["--gpus", "4", "--dry-run", "--steps", "2", "--warmup", "0"],
+               {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0 and "WORLD_SIZE" in r.stderr
+    r = _bench(["--gpus", "1", "--dry-run", "--steps", "2", "--warmup", "0"])
+    assert r.returncode == 0, r.stderr[-2000:]

@@ -5,8 +5,8 @@ how envs are split over ranks: each rank runs its `shard_range` of the bench wor
 through the C oracle (test infrastructure) and the all-reduced checksum must equal the
 single-rank run.  The optional observation gather (`gather_observations`) is checked with
 rank-tagged tensors, on shards of unequal size (25 envs over 2 ranks: 13 + 12), and C5's
-per-step, double-buffered `StepGather` (rewards / done / truncated in one flat byte buffer beside the
-observations, padded output sets) over several steps, each step's gathered values checked.
+per-step, double-buffered `StepGather` (rewards / done / truncated / listed / was_reset in one flat byte
+buffer beside the observations, padded output sets) over several steps, each step's gathered values checked.
 """
 import os
 import socket
@@ -67,6 +67,8 @@ def _worker(rank, world, port, q):
                 out.rewards[:n] = ((gl.double() / 4) + t).view(-1, 1).repeat(1, 2)
                 out.done[:n] = ((gl + t) % 2).to(torch.uint8)
                 out.trunc[:n] = ((gl + t) % 3 == 0).to(torch.uint8)
+                out.listed[:n] = torch.stack([(gl + t) % 5 != 0, (gl + 2 * t) % 7 != 0], 1).to(torch.uint8)
+                out.was_reset[:n] = ((gl * 3 + t) % 4 == 0).to(torch.uint8)
             return fill
 
         sg = StepGather(Fake())
@@ -80,7 +82,10 @@ def _worker(rank, world, port, q):
             ok = ok and (torch.equal(sg.obs()[:, 0, 0, 0, 0], ga.int() * 10 + 1000 * t)
                          and torch.equal(sg.rewards()[:, 1], ga.double() / 4 + t)
                          and torch.equal(sg.done(), ((ga + t) % 2).to(torch.uint8))
-                         and torch.equal(sg.truncated(), ((ga + t) % 3 == 0).to(torch.uint8)))
+                         and torch.equal(sg.truncated(), ((ga + t) % 3 == 0).to(torch.uint8))
+                         and torch.equal(sg.listed(), torch.stack([(ga + t) % 5 != 0, (ga + 2 * t) % 7 != 0],
+                                                                  1).to(torch.uint8))
+                         and torch.equal(sg.was_reset(), ((ga * 3 + t) % 4 == 0).to(torch.uint8)))
         if rank == 0:
             q.put((sum(c for c, _ in parts), sum(s for _, s in parts) % (1 << 64), g[:, 0, 0, 0, 0].tolist(), ok))
     finally:

@@ -97,6 +97,8 @@ def test_rccl_world1_gather(self_exchange):
             assert torch.equal(g.rewards(), ref.rewards)
             assert torch.equal(g.done(), ref.done)
             assert torch.equal(g.truncated(), ref.trunc)
+            assert torch.equal(g.listed(), ref.listed)
+            assert torch.equal(g.was_reset(), ref.was_reset)
             assert torch.equal(gather_observations(ref.obs), ref.obs)
             assert torch.equal(gather_observations(ref.obs, sizes=[2048]), ref.obs)
         ref.close()
@@ -110,7 +112,8 @@ def test_rccl_world1_gather_in_flight(self_exchange):
     """C5's exchange with steps in flight: 8 gathered steps issued back to back with no host sync and no
     wait on the caller's stream, so step t + 1 computes while step t's collectives run, and a set is
     written again only after the collectives of two steps earlier.  A consumer on the communication stream
-    (StepGather.step(after=...)) hashes every step's gathered observations, rewards and flags there; the
+    (StepGather.step(after=...)) hashes every step's gathered observations, rewards and flags (done, truncated, listed,
+    was_reset) there; the
     hashes, and the last two sets' gathered tensors, equal those of a reference engine stepped alone
     (gym/multiagent_env.py:111-171)."""
     import torch
@@ -149,7 +152,7 @@ def test_rccl_world1_gather_in_flight(self_exchange):
             exp[t - 1, 0] = (ref.obs.reshape(-1).to(torch.int64) * wts).sum()
             exp[t - 1, 1] = (ref.out.flat.to(torch.int64) * wts[:ref.out.flat.numel()]).sum()
             if t > steps - 2:
-                last[t] = (ref.obs.clone(), ref.rewards.clone(), ref.done.clone(), ref.trunc.clone())
+                last[t] = (ref.obs.clone(), ref.out.flat.clone())
         torch.cuda.synchronize()
         g.wait()
         torch.cuda.synchronize()
@@ -157,7 +160,8 @@ def test_rccl_world1_gather_in_flight(self_exchange):
         for t in (steps - 1, steps):
             k = (t - 1) % g.depth
             assert torch.equal(g.g_obs[k], last[t][0]), t
-            assert torch.equal(g.g_flat[k], torch.cat([last[t][1].view(-1).view(torch.uint8), last[t][2], last[t][3]])), t
+            # rewards, done, truncated, listed, was_reset (engine.StepOutputs)
+            assert torch.equal(g.g_flat[k], last[t][1]), t
         assert torch.equal(g.obs(copy=True), last[steps][0])
         ref.close()
         eng.close()
