@@ -50,6 +50,10 @@ class HostRecord(object):
         """The env's stream after the call, as a random.setstate() argument."""
         return (3, _MT.unpack_from(self.rec, 4 * HOST_RNG), None)
 
+    def rng_bytes(self):
+        """The same stream as the packed words EnvCore._rng_in produces."""
+        return self.rec[HOST_RNG:HOST_RNG + MT_WORDS].tobytes()
+
     def action_log(self):
         return decode_action_log(self.rec[self.lay["alog"]:], int(self.rec[HOST_ALOG_N]), self.E)
 
@@ -69,6 +73,7 @@ class EnvCore(object):
         self._np_obs = _abi.DTYPE_NP[builder.cfg.obs_dtype]
         self._actions = np.zeros((1, self.engine.A, 3), dtype=np.int32)
         self.last = None  # the last call's HostRecord
+        self._rng_last = None  # its stream, packed
         self.game = GameView(self.engine, 0, map_, rules_name, player_names, agent_ids, agent_weapons,
                              initial_zombies, minimum_zombies, debug)
         self.new_world(first=True)
@@ -79,6 +84,7 @@ class EnvCore(object):
 
     def _record(self, rec):
         self.last = HostRecord(self.engine, rec[0], self._lay, self._np_obs)
+        self._rng_last = self.last.rng_bytes()
         return self.last
 
     # Game.__initialize_world__ (game.py:151-169) on the engine, drawing from `random`
@@ -130,7 +136,9 @@ class EnvCore(object):
         for i, t in enumerate(triples):
             act[i] = (ACT_RAISE if self.debug else 0, 0, 0) if i in errors else t
         rec = eng.host_record()
-        eng.host_step(self._actions, self._rng_in(), rec)
+        rng = self._rng_in()
+        # the stream the engine already holds (nothing drew from `random` since the last call): not moved in
+        eng.host_step(self._actions, None if rng == self._rng_last else rng, rec)
         r = self._record(rec)
         random.setstate(r.rng_state())
         self.game.after_step(pre, r, errors, raising)

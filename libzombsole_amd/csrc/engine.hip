@@ -103,8 +103,15 @@ __device__ __forceinline__ int state_words(const Dev& d) {
 }
 
 // env e's state record (layout: include/zombsole_mi355x.h), written by threads tid = 0..nt-1 of one workgroup
+// (every thread of the workgroup calls it)
 __device__ void state_record(const Dev& d, int e, int32_t* b, int tid, int nt) {
     const int N = d.N, E = d.E;
+    __shared__ int nz;  // present zombies
+    if (tid == 0) nz = 0;
+    __syncthreads();
+    for (int s = d.A + d.P + tid; s < E; s += nt)
+        if (d.present[EIX(d, s, e)]) atomicAdd(&nz, 1);
+    __syncthreads();
     if (tid == 0) {
         b[0] = d.scal[S_T * N + e];
         b[1] = d.scal[S_DEATHS * N + e];
@@ -117,8 +124,6 @@ __device__ void state_record(const Dev& d, int e, int32_t* b, int tid, int nt) {
         b[8] = d.W;
         b[9] = d.H;
         b[10] = d.scal[S_PREVZD * N + e];
-        int nz = 0;
-        for (int s = d.A + d.P; s < E; s++) nz += d.present[EIX(d, s, e)];
         b[11] = nz;
         b[12] = d.scal[S_SERIAL * N + e];
         b[13] = b[14] = b[15] = 0;
@@ -156,11 +161,18 @@ __global__ void k_get_state(Dev d, int e, int32_t* buf) { state_record(d, e, buf
 // the drop-ins' per-call path (zs_host_step / zs_host_reset / zs_host_observe): one workgroup per env
 // ---------------------------------------------------------------------------
 // the process-global `random` state moved in (rings[e]: the getstate() block and its successor, st[e])
+// (host memory read in place: one round of 16-B loads, 1 248 words = 312 per env)
 __global__ void k_host_unpack(Dev d, const uint32_t* rings, const uint32_t* st) {
-    const int e = blockIdx.x;
-    for (int k = threadIdx.x; k < ZS_RING_WORDS; k += blockDim.x)
-        d.ring[(size_t)e * ZS_RING_WORDS + k] = rings[(size_t)e * ZS_RING_WORDS + k];
-    if (threadIdx.x == 0) d.rngst[e] = st[e];
+    const int e = blockIdx.x, t = threadIdx.x;
+    static_assert(ZS_RING_WORDS % 4 == 0, "16-B copies");
+    const uint4* src = (const uint4*)(rings + (size_t)e * ZS_RING_WORDS);
+    uint4* dst = (uint4*)(d.ring + (size_t)e * ZS_RING_WORDS);
+    const int n4 = ZS_RING_WORDS / 4;  // 312: two per thread at most (blockDim 256)
+    uint4 a = t < n4 ? src[t] : uint4{}, b = t + 256 < n4 ? src[t + 256] : uint4{};
+    const uint32_t sv = t == 0 ? st[e] : 0u;
+    if (t < n4) dst[t] = a;
+    if (t + 256 < n4) dst[t + 256] = b;
+    if (t == 0) d.rngst[e] = sv;
 }
 
 // Word offsets of a host record's sections (ZS_HOST_* in include/zombsole_mi355x.h, zs_host_layout)
@@ -170,13 +182,14 @@ struct HostLayout {
 
 // everything a call returns to the host, for env e: outputs, RNG stream, logs, state record, observation
 __global__ void k_host_pack(Dev d, HostLayout L, const uint8_t* obs, const double* rew, const uint8_t* done,
-                            const uint8_t* trunc, const uint8_t* rst, const int* err, int32_t* rec) {
+                            const uint8_t* trunc, const uint8_t* rst, int* err, int32_t* rec) {
     const int e = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
     int32_t* r = rec + (size_t)e * L.words;
     const uint32_t st = d.rngst[e];
     if (tid == 0) {
         r[ZS_HOST_FLAGS] = (done[e] ? 1 : 0) | (trunc[e] ? 2 : 0) | (rst && rst[e] ? 4 : 0);
         r[ZS_HOST_ERR] = *err;
+        *err = 0;  // the next call's error word starts clear (no memset launch)
         r[ZS_HOST_ALOG_N] = d.alog ? d.alog_n[e] : 0;
         r[ZS_HOST_DLOG_N] = d.dlog ? d.dlog_n[e] : 0;
         r[ZS_HOST_RNG + ZS_MT_N] = (int32_t)(st & 1023u);
@@ -190,9 +203,14 @@ __global__ void k_host_pack(Dev d, HostLayout L, const uint8_t* obs, const doubl
     if (d.dlog)
         for (int k = tid; k < 5 * d.E; k += nt) r[L.dlog + k] = d.dlog[(size_t)e * d.E * 5 + k];
     state_record(d, e, r + L.state, tid, nt);
-    const uint16_t* src = (const uint16_t*)(obs + (size_t)e * L.obs_bytes);
-    uint16_t* dst = (uint16_t*)(r + L.obs);
-    for (int k = tid; k < L.obs_bytes / 2; k += nt) dst[k] = src[k];
+    // the observation: 16-B copies when the env's block allows (L.obs is 16-B aligned), else 2-B ones
+    const uint8_t* src = obs + (size_t)e * L.obs_bytes;
+    uint8_t* dst = (uint8_t*)(r + L.obs);
+    if (L.obs_bytes % 16 == 0 && ((size_t)e * L.obs_bytes) % 16 == 0 && (L.words % 4) == 0) {
+        for (int k = tid; k < L.obs_bytes / 16; k += nt) ((uint4*)dst)[k] = ((const uint4*)src)[k];
+    } else {
+        for (int k = tid; k < L.obs_bytes / 2; k += nt) ((uint16_t*)dst)[k] = ((const uint16_t*)src)[k];
+    }
 }
 
 __global__ void k_set_state(Dev d, int e, const int32_t* buf, int* err) {
@@ -347,14 +365,14 @@ struct zs_handle {
     int* d_fsctr = nullptr;  // k_fstep's finished-workgroup counter (zero between launches)
     int resident = 0;  // step-launch workgroups resident per CU (layout choice)
     int want = 0;      // workgroups per CU the launch has (capped at 32)
-    // the drop-ins' per-call path (zs_host_*), set up by its first call: one pinned input block
-    // (actions, then the `random` state as rings + st words) copied in, one pinned record block per env
-    // copied out, one synchronisation per call
+    // the drop-ins' per-call path (zs_host_*), set up by its first call: one pinned, device-mapped input
+    // block (actions, then the `random` state as rings + st words) the kernels read in place, one pinned,
+    // device-mapped record block k_host_pack writes in place, one synchronisation per call
     HostLayout hl{};
-    int32_t* d_hin = nullptr;
-    int32_t* h_hin = nullptr;   // pinned
+    int32_t* h_hin = nullptr;   // pinned host memory ...
+    int32_t* d_hin = nullptr;   // ... and its device address
+    int32_t* h_hrec = nullptr;
     int32_t* d_hrec = nullptr;
-    int32_t* h_hrec = nullptr;  // pinned
     uint8_t* d_hobs = nullptr;
     double* d_hrew = nullptr;
     uint8_t* d_hflags = nullptr;  // done [N], trunc [N], listed [N][A], reset [N]
@@ -1278,6 +1296,7 @@ extern "C" int zs_reset(zs_handle* h, const uint8_t* env_mask_dev, void* obs_dev
     if (rc) return rc;
     int err = 0;
     HIPCHK(hipMemcpyAsync(&err, h->d_err, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemsetAsync(h->d_err, 0, sizeof(int), s));  // every reader leaves the error word clear
     HIPCHK(hipStreamSynchronize(s));
     if (err == ZS_ENOSPACE) return fail(ZS_ENOSPACE, "Not enough space to spawn players/agents");
     if (err) return fail(err, "reset failed");
@@ -1568,6 +1587,7 @@ extern "C" int zs_set_state(zs_handle* h, int32_t env, const int32_t* buf_host, 
     HIPCHK(hipGetLastError());
     int err = 0;
     HIPCHK(hipMemcpyAsync(&err, h->d_err, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemsetAsync(h->d_err, 0, sizeof(int), s));
     HIPCHK(hipStreamSynchronize(s));
     if (err) return fail(ZS_EINVAL, "state record's needs_reset [5] differs from the engine's (pending resets are not settable)");
     return ZS_OK;
@@ -1737,10 +1757,10 @@ extern "C" int zs_death_log(zs_handle* h, int32_t env, int32_t* out_host, int32_
 // ---------------------------------------------------------------------------
 // The drop-ins' per-call path.  The reference's env.step / env.reset / env.get_observation run one env
 // per call on the host (gym_env.py:99-164, gym/multiagent_env.py:111-184) and share the process-global
-// `random` stream.  Here one call is: the caller's actions and `random` state packed into one pinned
-// block and copied in, the engine's launches, k_host_pack writing everything the host reads back
-// (outputs, the advanced stream, the action / death logs, the state record, the observation) into one
-// record per env, one copy out and one synchronisation.
+// `random` stream.  Here one call is: the caller's actions and `random` state written into one pinned,
+// device-mapped block that the kernels read in place, the engine's launches, k_host_pack writing
+// everything the host reads back (outputs, the advanced stream, the action / death logs, the state
+// record, the observation) into one pinned, device-mapped record per env, and one synchronisation.
 // ---------------------------------------------------------------------------
 static int obs_bytes_per_env(const zs_handle* h) {
     int32_t shp[4];
@@ -1758,8 +1778,8 @@ static HostLayout host_layout(const zs_handle* h) {
     L.alog = L.rew + 2 * L.R;
     L.dlog = L.alog + 2 * d.E;
     L.state = L.dlog + 5 * d.E;
-    L.obs = (L.state + h->state_words + 1) & ~1;  // 8-byte aligned
-    L.words = (L.obs + (L.obs_bytes + 3) / 4 + 1) & ~1;
+    L.obs = (L.state + h->state_words + 3) & ~3;  // 16-byte aligned
+    L.words = (L.obs + (L.obs_bytes + 3) / 4 + 3) & ~3;
     return L;
 }
 
@@ -1770,19 +1790,23 @@ static int host_init(zs_handle* h) {
     HostLayout L = host_layout(h);
     const size_t in_words = N * d.A * 3 + N * (ZS_RING_WORDS + 1);
     int rc;
-    if ((rc = dalloc(h, &h->d_hin, in_words)) || (rc = dalloc(h, &h->d_hobs, N * L.obs_bytes)) ||
-        (rc = dalloc(h, &h->d_hrew, N * L.R)) || (rc = dalloc(h, &h->d_hflags, N * (3 + d.A))) ||
-        (rc = dalloc(h, &h->d_hrec, N * L.words)))
+    if ((rc = dalloc(h, &h->d_hobs, N * L.obs_bytes)) || (rc = dalloc(h, &h->d_hrew, N * L.R)) ||
+        (rc = dalloc(h, &h->d_hflags, N * (3 + d.A))))
         return rc;
-    HIPCHK(hipHostMalloc((void**)&h->h_hin, in_words * sizeof(int32_t), hipHostMallocDefault));
-    HIPCHK(hipHostMalloc((void**)&h->h_hrec, N * L.words * sizeof(int32_t), hipHostMallocDefault));
+    // coherent (uncached on the device) so the kernels see this call's input and the host the record
+    // without copies; the blocks are a few KB per env
+    const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
+    HIPCHK(hipHostMalloc((void**)&h->h_hin, in_words * sizeof(int32_t), fl));
+    HIPCHK(hipHostMalloc((void**)&h->h_hrec, N * L.words * sizeof(int32_t), fl));
+    HIPCHK(hipHostGetDevicePointer((void**)&h->d_hin, h->h_hin, 0));
+    HIPCHK(hipHostGetDevicePointer((void**)&h->d_hrec, h->h_hrec, 0));
     h->hl = L;
     return ZS_OK;
 }
 
 // the `random` states of envs [0, N) (CPython getstate() form, 625 words each) into the pinned input
 // block after the actions: per env its ring (the block, then its successor) and its st word
-static int host_stage_rng(zs_handle* h, const uint32_t* rng_host, size_t* in_words) {
+static int host_stage_rng(zs_handle* h, const uint32_t* rng_host) {
     const size_t N = h->d.N;
     uint32_t* rings = (uint32_t*)h->h_hin + N * h->d.A * 3;
     uint32_t* st = rings + N * ZS_RING_WORDS;
@@ -1798,7 +1822,6 @@ static int host_stage_rng(zs_handle* h, const uint32_t* rng_host, size_t* in_wor
         }
         st[e] = g[ZS_MT_N] | (0u << 10) | (1u << 11);
     }
-    *in_words = N * h->d.A * 3 + N * (ZS_RING_WORDS + 1);
     return ZS_OK;
 }
 
@@ -1812,36 +1835,28 @@ static int host_call(zs_handle* h, int op, const int32_t* actions_host, const ui
     const Dev& d = h->d;
     const size_t N = d.N;
     const HostLayout& L = h->hl;
-    size_t in_words = 0;
-    if (op == HOST_STEP) {
-        std::memcpy(h->h_hin, actions_host, sizeof(int32_t) * N * d.A * 3);
-        in_words = N * d.A * 3;
-    }
-    if (rng_host && (rc = host_stage_rng(h, rng_host, &in_words))) return rc;
-    if (in_words) HIPCHK(hipMemcpyAsync(h->d_hin, h->h_hin, in_words * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    if (op == HOST_STEP) std::memcpy(h->h_hin, actions_host, sizeof(int32_t) * N * d.A * 3);
+    if (rng_host && (rc = host_stage_rng(h, rng_host))) return rc;
     if (rng_host) {
         const uint32_t* rings = (const uint32_t*)h->d_hin + N * d.A * 3;
         hipLaunchKernelGGL(k_host_unpack, dim3((unsigned)N), dim3(256), 0, s, h->d, rings, rings + N * ZS_RING_WORDS);
         HIPCHK(hipGetLastError());
     }
     uint8_t *done = h->d_hflags, *trunc = done + N, *rst = trunc + N, *listed = rst + N;
-    if (op == HOST_STEP) {
-        HIPCHK(hipMemsetAsync(h->d_err, 0, sizeof(int), s));
+    if (op == HOST_STEP) {  // (d_err is clear: k_host_pack clears it, and zs_reset / zs_set_state before use)
         rc = zs_step(h, h->d_hin, h->d_hobs, h->d_hrew, done, trunc, listed, rst, s);
     } else if (op == HOST_RESET) {
         HIPCHK(hipMemsetAsync(h->d_hflags, 0, N * 3, s));
         HIPCHK(hipMemsetAsync(h->d_hrew, 0, N * L.R * sizeof(double), s));
         rc = queue_reset(h, nullptr, h->d_hobs, s);
     } else {
-        HIPCHK(hipMemsetAsync(h->d_err, 0, sizeof(int), s));
         rc = launch_obs(h, h->d_hobs, nullptr, s);
     }
     if (rc) return rc;
     hipLaunchKernelGGL(k_host_pack, dim3((unsigned)N), dim3(256), 0, s, h->d, L, (const uint8_t*)h->d_hobs,
                        (const double*)h->d_hrew, (const uint8_t*)done, (const uint8_t*)trunc,
-                       op == HOST_RESET ? nullptr : (const uint8_t*)rst, (const int*)h->d_err, h->d_hrec);
+                       op == HOST_RESET ? nullptr : (const uint8_t*)rst, h->d_err, h->d_hrec);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(h->h_hrec, h->d_hrec, N * L.words * sizeof(int32_t), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     std::memcpy(rec_host, h->h_hrec, N * L.words * sizeof(int32_t));
     const int err = h->h_hrec[ZS_HOST_ERR];
