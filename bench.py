@@ -487,8 +487,8 @@ def main():
     tick_ms = prof["tick_ms"] / prof_steps
     obs_ms = prof["obs_ms"] / prof_steps
     reset_ms = prof["reset_ms"] / prof_steps
-    fused = prof["reset_n"] == 0  # reset work runs inside the step launch (k_step, k_fstep)
-    fobs = prof["obs_n"] == 0      # the step launch writes the observations itself (k_fstep: its writer waves)
+    fused = prof["reset_n"] == 0  # reset work runs inside the step launch (k_step)
+    fobs = prof["obs_n"] == 0      # the step launch writes the observations itself (zs_launch.fobs)
     step_name = launch["step_kernel"]
     step_b = tick_b + (obs_b if fobs else 0)
     if fobs or tick_ms >= obs_ms:

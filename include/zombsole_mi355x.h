@@ -147,7 +147,8 @@ typedef struct zs_map_desc {
  * no environment variable selects a kernel. */
 typedef struct zs_launch {
     int32_t fused;           /* reset work inside the step launch (k_step) instead of its own launch  */
-    int32_t fobs;            /* observations written by the step launch itself                        */
+    int32_t fobs;            /* observations written by the step launch itself (the default for small
+                              * images without a store-stream kernel; -1 off, 1 on)                    */
     int32_t tick_waves;      /* k_tick's register budget: 5 or 6 waves per SIMD                        */
     int32_t lds_budget;      /* -1: largest optional LDS copies instead of the most resident workgroups */
     int32_t rw_need;         /* RNG window words a plain step prefetches (32..512)                    */
@@ -158,10 +159,13 @@ typedef struct zs_launch {
     int32_t defer_respawn;   /* 1: zombie respawn by k_respawn, -1: by the tick's leader               */
     int32_t respawn_grid;    /* k_respawn workgroups                                                   */
     int32_t obs_pipe;        /* -1: no prefetching store-stream observation kernel (k_obs_pipe family) */
-    int32_t obs_lds;         /* k_obs_lds's LDS-staged 16-B stores (and its patch / ring variants)     */
-    int32_t obs_patch;       /* the padded-table encoder kernel k_obs_patch                            */
-    int32_t obs_ring;        /* encoder / writer waves through an LDS ring (k_obs_ring)                */
-    int32_t obs_ring_patch;  /* k_obs_ring with the padded-table encoders                              */
+    int32_t obs_lds;         /* the LDS-staged 16-B store kernels (k_obs_patch, k_obs_ring): -1 keeps
+                              * k_obs_pipe, 1 takes them at any env count                              */
+    int32_t obs_patch;       /* -1: no padded-table encoder kernel k_obs_patch                         */
+    int32_t obs_ring;        /* encoder / writer waves through an LDS ring (k_obs_ring, k_obs_pbring);
+                              * -1 keeps k_obs_patch / k_obs_pipe / k_obs_gather                       */
+    int32_t obs_ring_patch;  /* -1: k_obs_ring with the select-chain encoders instead of the
+                              * padded-table ones (its fallback when the tables do not fit)            */
     int32_t obs_gather;      /* -1: no k_obs_gather (large maps then use k_obs)                        */
     int32_t obs_gather_stat; /* -1: k_obs_gather reads static words from HBM instead of LDS tables     */
     int32_t obs_stat;        /* -1: per-cell static words instead of LDS bitmaps                       */
@@ -169,14 +173,9 @@ typedef struct zs_launch {
     int32_t obs_wgs;         /* observation workgroups per CU (store-stream kernels)                   */
     int32_t par_exec;        /* -1: the leader lane executes the shuffled actions serially instead of
                               * the env's lanes in parallel (core.py:103-119)                          */
-    int32_t fstep;           /* the step as one launch (k_fstep): tick, observation encoder and writer
-                              * waves in every workgroup, the tick overlapping the observation stream  */
-    int32_t fs_tick;         /* k_fstep's tick waves per workgroup (4 or 6)                            */
-    int32_t tick_early;      /* k_tick (5 waves per SIMD) loads the RNG window's first words with its
-                              * first load round, overlapping their round trip with the decisions      */
-    int32_t pol_tick;        /* zs_step_graph with the side-stream reset: 1 = the on-device policy inside
-                              * the tick launch instead of its own launch ahead of it                  */
-    int32_t reserved[6];
+    int32_t reserved[10];    /* zero (round 6 removed four switches of alternatives measured slower:
+                              * the one-launch step k_fstep and its shapes, the early RNG window in
+                              * k_tick, the policy inside the side-stream tick)          */
 } zs_launch;
 
 typedef struct zs_config {

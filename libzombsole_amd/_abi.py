@@ -53,13 +53,12 @@ class zs_map_desc(C.Structure):
 
 LAUNCH_FIELDS = ["fused", "fobs", "tick_waves", "lds_budget", "rw_need", "reset_wgs", "reset_stream", "reset_lists",
                  "reset_grid", "defer_respawn", "respawn_grid", "obs_pipe", "obs_lds", "obs_patch", "obs_ring",
-                 "obs_ring_patch", "obs_gather", "obs_gather_stat", "obs_stat", "obs_win", "obs_wgs", "par_exec",
-                 "fstep", "fs_tick", "tick_early", "pol_tick"]
+                 "obs_ring_patch", "obs_gather", "obs_gather_stat", "obs_stat", "obs_win", "obs_wgs", "par_exec"]
 
 
 class zs_launch(C.Structure):
     """Launch overrides (include/zombsole_mi355x.h): 0 = automatic; switches 1 = on, -1 = off."""
-    _fields_ = [(f, C.c_int32) for f in LAUNCH_FIELDS] + [("reserved", C.c_int32 * 6)]
+    _fields_ = [(f, C.c_int32) for f in LAUNCH_FIELDS] + [("reserved", C.c_int32 * 10)]
 
 
 class zs_config(C.Structure):

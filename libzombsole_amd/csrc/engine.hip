@@ -3,7 +3,7 @@
 // A step (zs_step) is: k_reset (zs_reset.hpp, one wave per env that ended at the previous step, on
 // a side stream concurrent with the tick, or fused with it into k_step), k_tick (zs_tick.hpp, 64/G
 // envs per wave with G lanes per env and the env's hot state in LDS), k_respawn (deferred zombie
-// respawns, one wave per env) and the observation kernel (zs_obs.hpp: k_obs_lds / k_obs_pipe
+// respawns, one wave per env) and the observation kernel (zs_obs.hpp: k_obs_ring / k_obs_pipe
 // persistent store streams, k_obs_gather for large maps, k_obs in general).  zs_step_graph replays
 // a step as a hipGraph.  k_seed / k_gen_actions / k_get_state / k_set_state are the small helpers
 // behind the ABI.
@@ -315,14 +315,11 @@ struct zs_handle {
     ObsLayout obs_l;  // k_obs per-wave LDS image
     int obs_wpg;      // k_obs waves (envs) per workgroup
     int obs_pipe = 0;      // k_obs_pipe<NOBS> usable (NOBS = 1, 2, 4), else 0
-    int obs_lds = 0;       // k_obs_pipe's walk with LDS-staged 16-B stores (k_obs_lds), channels encoding
     int obs_ring = 0;      // k_obs_ring: encoder and writer waves through an LDS ring (zs_launch.obs_ring)
     size_t obs_ring_bytes = 0;
-    int obs_bring = 0;     // k_obs_bring: its unit slots (0: not used)
-    int obs_bring_pad = 0; // ... as k_obs_pbring (padded-table encoders)
+    int obs_bring = 0;     // k_obs_pbring: its unit slots (0: not used)
     size_t obs_bring_bytes = 0;
-    size_t obs_lds_bytes = 0;
-    int obs_patch = 0;     // k_obs_lds's walk with the padded-table encoder (k_obs_patch, zs_launch.obs_patch)
+    int obs_patch = 0;     // k_obs_pipe's walk with the padded-table encoder and the staged flush (k_obs_patch)
     size_t obs_patch_bytes = 0;
     int obs_patch_wgs = 2;  // its workgroups (PATCH_WPG waves) per CU
     int obs_gather = 0;    // else k_obs_gather<NOBS> usable (NOBS = 1, 2, 4), else 0 (k_obs)
@@ -341,7 +338,7 @@ struct zs_handle {
     uint64_t gclock = 0;
     uint64_t* d_gstep = nullptr;  // [0] policy step counter (the step's policy reads it, the step's tail advances it)
     int graph_pol = 0;            // zs_step_graph is capturing a step with this policy (n_discrete), else 0
-    int obs_pipe_wgs = 8;  // k_obs_pipe / k_obs_lds workgroups per CU
+    int obs_pipe_wgs = 8;  // k_obs_pipe workgroups per CU
     // next-step reset work on a side stream, concurrent with the tick (the two touch disjoint envs);
     // the caller's stream joins it before the observations
     int reset_side = 0;
@@ -358,11 +355,6 @@ struct zs_handle {
     int rpar = 0;
     size_t reset_lds = 0;
     int fused = 0;  // zs_step runs reset work and the tick in one launch (k_step)
-    int fstep = 0;  // zs_step is one k_fstep launch (tick, encoder and writer waves per workgroup, zs_fstep.hpp)
-    FsLayout fs_l;
-    FsShape fs_sh;
-    int fs_grid = 0;
-    int* d_fsctr = nullptr;  // k_fstep's finished-workgroup counter (zero between launches)
     int resident = 0;  // step-launch workgroups resident per CU (layout choice)
     int want = 0;      // workgroups per CU the launch has (capped at 32)
     // the drop-ins' per-call path (zs_host_*), set up by its first call: one pinned, device-mapped input
@@ -823,31 +815,21 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
             h->obs_pipe_wgs = std::max(1, std::min(2, 160 * 1024 / (d.obs_stat * 4 + 4 * L.bytes)));
             if (h->ov.obs_wgs > 0) h->obs_pipe_wgs = std::min(32, (int)h->ov.obs_wgs);
         }
-        // k_obs_lds: the same walk with each observation block staged in LDS and streamed out as 16-B
-        // stores (channels encoding).  Measured on one MI355X: int16 blocks (C5) 341 -> 264 us per
-        // launch at 4 workgroups per CU (2: 334, 3: 278, 5: 307); int64 blocks (staged as int32) at
-        // up to 4 per CU.  It pays when every wave walks several envs (C3 65536 envs; at 8192, one env
-        // per wave, k_obs_pipe's per-cell stores measured 33 vs 36 us).  zs_launch.obs_lds forces either,
-        // zs_launch.obs_wgs sets the workgroups per CU.
+        // The LDS-staged 16-B store kernels (k_obs_patch, k_obs_ring; zs_obs.hpp) for k_obs_pipe's shape,
+        // channels encoding.  They pay when every wave walks several envs (at 8192 envs, one env per wave,
+        // k_obs_pipe's per-cell stores measured 33 vs 36 us): int64 blocks from 48 envs per CU (C3 on one
+        // MI355X, k_obs_ring against k_obs_pipe: 12 288 envs 129.5 against 117.1 M env-steps/s, 16 384 123.7 /
+        // 121.4, 24 576 140.1 / 134.8, 32 768 153.6 / 147.1; 8 192 138.9 against 143.9, 10 240 (fused) 150.9 /
+        // 154.9; profiles/r05c_mid_sizes.log), narrower blocks at any count.  zs_launch.obs_lds = -1 keeps
+        // k_obs_pipe, 1 takes them at any count.
+        bool staged = false;
         if (h->obs_pipe && d.obs_enc == ZS_ENC_CHANNELS && h->ov.obs_lds >= 0) {
             const int ts = d.obs_dtype == ZS_DTYPE_I64 ? 8 : d.obs_dtype == ZS_DTYPE_I32 ? 4 : 2;
-            const size_t lb = (size_t)d.obs_stat * 4 + 4 * ((size_t)L.bytes + (size_t)obs_stage_slot_bytes(ts));
-            int wgs = std::max(1, std::min(ts == 8 ? 2 : 4, (int)(160 * 1024 / lb)));
-            if (h->ov.obs_wgs > 0) wgs = std::min(32, (int)h->ov.obs_wgs);
-            const bool forced = h->ov.obs_lds > 0;
-            // int64 from 48 envs per CU (C3 on one MI355X, k_obs_ring against k_obs_pipe: 12 288 envs 129.5 against
-            // 117.1 M env-steps/s, 16 384 123.7 / 121.4, 24 576 140.1 / 134.8, 32 768 153.6 / 147.1; 8 192 138.9
-            // against 143.9, 10 240 (fused) 150.9 / 154.9; profiles/r05c_mid_sizes.log)
-            const bool pays = ts < 8 || (long)d.N >= 48L * 256;
-            if (lb <= 64 * 1024 && (pays || forced)) {
-                h->obs_lds = 1;
-                h->obs_lds_bytes = lb;
-                h->obs_pipe_wgs = wgs;
-            }
+            staged = ts < 8 || (long)d.N >= 48L * 256 || h->ov.obs_lds > 0;
         }
-        // k_obs_patch: k_obs_lds with the padded-table encoder (maps up to 4095 x 4095, rows of the
-        // padded table in the workgroup's LDS).  zs_launch.obs_patch forces either.
-        if (h->obs_lds && d.OW <= 64 && (long)(d.W + 20) * 21 < 65536 && d.H < 4096) {
+        // k_obs_patch: k_obs_pipe's walk with the padded-table encoder and the staged flush (maps up to
+        // 4095 x 4095, rows of the padded table in the workgroup's LDS).  zs_launch.obs_patch = -1 disables.
+        if (staged && d.OW <= 64 && (long)(d.W + 20) * 21 < 65536 && d.H < 4096) {
             const int ts = d.obs_dtype == ZS_DTYPE_I64 ? 8 : d.obs_dtype == ZS_DTYPE_I32 ? 4 : 2;
             const size_t pb = (size_t)patch_static_bytes(d.opad_n, d.O) +
                               PATCH_WPG * (size_t)patch_wave_bytes(d.DW, d.O, obs_stage_slot_bytes(ts));
@@ -861,10 +843,10 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
                 if (h->ov.obs_wgs > 0) h->obs_patch_wgs = std::min(32, (int)h->ov.obs_wgs);
             }
         }
-        // k_obs_ring (zs_obs.hpp): the k_obs_lds shape with dedicated writer waves.  Measured on one
-        // MI355X (2 runs each): C3 (int64) observations 292 / 280 -> 285 / 273 us; C5 (int16) even.
-        // Default for int64 blocks; zs_launch.obs_ring forces either.
-        if (h->obs_lds && d.obs_enc == ZS_ENC_CHANNELS) {
+        // k_obs_ring (zs_obs.hpp): the staged flush with dedicated writer waves.  Measured on one MI355X
+        // (2 runs each): C3 (int64) observations 292 / 280 -> 285 / 273 us against its predecessor without
+        // writer waves; C5 (int16) even.  Default for int64 blocks; zs_launch.obs_ring forces either.
+        if (staged) {
             const int ts = d.obs_dtype == ZS_DTYPE_I64 ? 8 : d.obs_dtype == ZS_DTYPE_I32 ? 4 : 2;
             // the ring's encoders are k_obs_patch's when its tables fit (zs_launch.obs_ring_patch forces either)
             const bool patched = h->obs_patch && h->ov.obs_ring_patch >= 0;
@@ -894,28 +876,18 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
                 h->obs_gather_stat = d.obs_stat && gb + 16 * (size_t)d.DW <= 64 * 1024 && h->ov.obs_gather_stat >= 0;
             }
         }
-        // k_obs_bring: k_obs_gather's window-only fetches as the encoders of a k_obs_ring-style ring, when
-        // the dead-body and present rows fit the encoders' load rounds and two unit slots fit beside the
-        // static tables and the encoder images.  zs_launch.obs_ring = -1 keeps k_obs_gather.
+        // k_obs_pbring: k_obs_gather's window-only fetches as the encoders of a k_obs_ring-style ring, the
+        // things written over the windows (C4 on one MI355X: observations 180-184 us with k_obs_gather, 151 us
+        // with k_obs_pbring), when the dead-body and present rows fit the encoders' load rounds and two unit
+        // slots fit beside the static tables and the encoder regions.  zs_launch.obs_ring = -1 keeps k_obs_gather.
         if (h->obs_gather && d.obs_stat && d.obs_enc == ZS_ENC_CHANNELS && d.E <= 64 && d.DW <= 64 * BRING_D &&
             d.OW <= 64 * BRING_O && h->ov.obs_ring >= 0) {
             const int ts = d.obs_dtype == ZS_DTYPE_I64 ? 8 : d.obs_dtype == ZS_DTYPE_I32 ? 4 : 2;
-            const int us = bring_slots(d.DW, h->obs_gl.bytes, ts, nobs, 160 * 1024);
-            const size_t bb = (size_t)bring_fixed_bytes(d.DW, h->obs_gl.bytes) + (size_t)us * bring_unit_bytes(ts, nobs);
-            if (us >= 2 && obs_attr(d.obs_dtype, OBSK_BRING, nobs, 0, (int)bb) == hipSuccess) {
-                h->obs_bring = us;
-                h->obs_bring_bytes = bb;
-            }
-            // k_obs_pbring: the things written over the windows instead of looked up per cell (C4 on one
-            // MI355X: observations 157.7 -> 151.1 us, 53.3 -> 54.0 M env-steps/s; profiles/r05f_ab_pbring.log);
-            // zs_launch.obs_ring_patch = -1 keeps k_obs_bring
             const int usp = pbring_slots(d.DW, d.OW, ts, nobs, 160 * 1024);
             const size_t pbb = (size_t)pbring_fixed_bytes(d.DW, d.OW) + (size_t)usp * bring_unit_bytes(ts, nobs);
-            if (h->obs_bring && usp >= 2 && h->ov.obs_ring_patch >= 0 &&
-                obs_attr(d.obs_dtype, OBSK_BRING, nobs, 1, (int)pbb) == hipSuccess) {
+            if (usp >= 2 && obs_attr(d.obs_dtype, OBSK_BRING, nobs, 1, (int)pbb) == hipSuccess) {
                 h->obs_bring = usp;
                 h->obs_bring_bytes = pbb;
-                h->obs_bring_pad = 1;
             }
         }
         // with the store-stream kernel available the observations are its job (measured faster than
@@ -925,13 +897,6 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
         d.fobs = L.bytes + 4 * d.obs_stat <= 16 * 1024 && h->ov.fobs >= 0;
         if (h->obs_pipe && h->ov.fobs <= 0) d.fobs = 0;
         if (d.defer_respawn) d.fobs = 0;  // the observations must see k_respawn's zombies
-        // the tick's part of them by k_obs_pipe's walk over its own envs (zs_tick.hpp fobs_pipe) for the
-        // shape k_obs_pipe serves, else the generic per-cell encoder
-        d.fobs_pipe = d.fobs && !world && d.obs_w == 21 && (nobs == 1 || nobs == 2 || nobs == 4) && d.obs_stat &&
-                              L.hp_cap && L.win && d.O > 0 && d.E <= 64 && d.DW <= 64 * OBS_PF_D &&
-                              d.O <= 64 * OBS_PF_H && d.OW <= 64
-                          ? nobs
-                          : 0;
     }
     // Fused step launch (reset work + tick in one) when the whole launch is resident at once: then
     // the step is one latency-bound round and the reset work hides under the ticks (measured: 8192
@@ -999,63 +964,6 @@ extern "C" int zs_create(const zs_config* cfg, int device, zs_handle** out) {
         delete h;
         return fail(ZS_EHIP, "cannot raise k_reset's dynamic LDS limit");
     }
-    // k_fstep (zs_fstep.hpp): the multi-round step (reset work on the side stream, k_tick, the padded-table
-    // k_obs_ring) as one launch, one workgroup per CU, its tick waves overlapping its observation stream.
-    // It needs the ring's shape (channels, padded-table encoders), respawns in the tick (no k_respawn),
-    // an instance for (G, dtype, observations per env), and its tables, encoder regions, >= 2 ring slots
-    // and FS_TICK tick / reset images in 160 KB.  zs_launch.fstep forces either.
-    // One-round sizes (the fused step launch: 8 192-env shards) take eight tick waves, one unit each, with
-    // the reset work of the unit's pending envs after it (zs_launch.fs_tick = 8, 5 encoders and 3 writers;
-    // 86 = 6 encoders and 2 writers).
-    // k_obs_pipe's registered shape (surroundings of width 21, 1 / 2 / 4 observations, the prefetch sizes)
-    // with the padded-table encoder's limits
-    if (h->ov.fstep > 0 && !d.defer_respawn && !d.fobs && h->obs_pipe && d.obs_enc == ZS_ENC_CHANNELS &&
-        d.OW <= 64 && (long)(d.W + 20) * 21 < 65536 && d.H < 4096) {
-        const int nobs = obs_count(d.obs_scope, d.reward_mode, d.A);
-        const int ts = d.obs_dtype == ZS_DTYPE_I64 ? 8 : d.obs_dtype == ZS_DTYPE_I32 ? 4 : 2;
-        const int pair = ring_pair(ts, nobs);
-        int cus = 256;
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
-        const int nunits = (d.N + 64 / h->G - 1) / (64 / h->G);
-        const int grid = std::max(1, std::min(cus, nunits));
-        const int upw = (nunits + grid - 1) / grid;
-        // the tick regions: the smallest image that holds the plain step's RNG window (the role shape, not the
-        // resident workgroups, sets the occupancy), candidates from HBM scratch, the spawn lists staged when
-        // they fit; the reset work's image of one env aliases the same region
-        int rw_need = 32;
-        while (rw_need < 512 && rw_need < 2 * d.E + 8) rw_need *= 2;
-        const int ne = 64 / h->G, lst = (d.nps + d.nzs <= 4096) ? d.nps + d.nzs : 0;
-        const int fs_tick_b = tick_layout(ne, d.E, d.DW, rw_need, 0, lst, d.A, 0).bytes;
-        const int fs_reset_b = reset_lds_bytes(d.E, d.DW, d.ncand, lst, 0);
-        const int tick_b = std::max(fs_tick_b, fs_reset_b);
-        // role shape (tick / encoder / writer waves); zs_launch.fs_tick = 6 takes six tick waves
-        const FsShape sh = h->ov.fs_tick == 6 ? FsShape{6, 7, 3} : h->ov.fs_tick == 8 ? FsShape{8, 5, 3}
-                           : h->ov.fs_tick == 86 ? FsShape{8, 6, 2} : FsShape{4, 9, 3};
-        FsLayout L;
-        int us = 8 / pair;
-        for (; us >= 2; us--) {
-            L = fs_layout(sh, patch_static_bytes(d.opad_n, d.O), patch_enc_bytes(d.DW, d.O),
-                          obs_stage_slot_bytes(ts, nobs * pair), us, tick_b, upw * (64 / h->G));
-            if (L.bytes <= 160 * 1024) break;
-        }
-        if (us >= 2 && upw <= FS_MAX_UNITS && fstep_attr(h->G, d.obs_dtype, nobs, sh, L.bytes) == hipSuccess) {
-            TRY(dalloc(h, &h->d_fsctr, 1));
-            h->fstep = 1;
-            h->fused = 0;  // the reset work is the tick waves'
-            d.rw_cap = rw_need;
-            d.rw_step = rw_need;
-            d.cand_cap = 0;
-            d.lists_cap = d.rlists_cap = lst;
-            h->lds = (size_t)fs_tick_b;
-            h->reset_lds = (size_t)fs_reset_b;
-            h->fs_l = L;
-            h->fs_sh = sh;
-            h->fs_grid = grid;
-        }
-    }
-    if (getenv("ZS_VERBOSE") && h->fstep)
-        fprintf(stderr, "zs_create: k_fstep shape %d/%d/%d, %d ring slots, %d B of LDS, grid %d\n", h->fs_sh.nt,
-                h->fs_sh.nen, h->fs_sh.nw, h->fs_l.us, h->fs_l.bytes, h->fs_grid);
     if (getenv("ZS_VERBOSE"))
         fprintf(stderr, "zs_create: N=%d E=%d G=%d step_lds=%zu resident=%d reset_lds=%zu rw_cap=%d cand_cap=%d "
                         "lists_cap=%d fused=%d fobs=%d obs_img=%d k_obs_img=%d x%d pipe=%d gather=%d pipe_wgs=%d reset_side=%d defer_respawn=%d\n",
@@ -1147,15 +1055,14 @@ static int launch_obs(zs_handle* h, void* obs, const uint8_t* mask, hipStream_t 
         o.block = 64 * PATCH_WPG;
         o.lds = h->obs_patch_bytes;
     } else if (!mask && h->obs_pipe) {  // every env of [env0, env1), registered shape: the prefetching store stream
-        o.kind = h->obs_lds ? OBSK_LDS : OBSK_PIPE;
+        o.kind = OBSK_PIPE;
         o.grid = (unsigned)std::min((env1 - env0 + 3) / 4, 256 * h->obs_pipe_wgs);
         o.block = 256;
-        o.lds = h->obs_lds ? h->obs_lds_bytes : (size_t)d.obs_stat * 4 + 4 * (size_t)h->obs_l.bytes;
+        o.lds = (size_t)d.obs_stat * 4 + 4 * (size_t)h->obs_l.bytes;
     } else if (!mask && h->obs_bring) {  // every env of [env0, env1): window-only encoders, writer waves
         const int ts = d.obs_dtype == ZS_DTYPE_I64 ? 8 : d.obs_dtype == ZS_DTYPE_I32 ? 4 : 2;
         const int pair = ring_pair(ts, h->obs_gather);
         o.kind = OBSK_BRING;
-        o.patched = h->obs_bring_pad;
         o.nobs = h->obs_gather;
         o.grid = (unsigned)std::min((env1 - env0 + pair - 1) / pair, 256);
         o.block = 64 * (BRING_ENC + BRING_WRT);
@@ -1214,7 +1121,6 @@ static int launch_tick(zs_handle* h, const int32_t* actions, double* rew, uint8_
     a.cur_list = (const int*)h->d_rlist[p];
     a.cur_count = (const int*)(h->d_rcount + p);
     a.err = h->d_err;
-    a.early = h->ov.tick_early > 0;
     hipError_t le;
     switch (h->G) {
     case 1: le = launch_tick_g1(h->fused, h->tick_waves, grid, h->lds, s, d, a); break;
@@ -1312,54 +1218,11 @@ extern "C" int zs_observe(zs_handle* h, const uint8_t* env_mask_dev, void* obs_d
     return launch_obs(h, obs_dev, env_mask_dev, s);
 }
 
-// zs_step as one k_fstep launch (zs_fstep.hpp): the envs pending a reset (S_NEEDRESET, i.e. list[p]) are
-// rebuilt by the tick waves that find them, the ticks append this step's ended envs to list[q], and the
-// launch's last workgroup empties list[p] and advances the policy's step counter (the step's tail).  The
-// policy of zs_step_graph runs inside the tick, as in the fused step launch.
-static int step_fstep(zs_handle* h, const int32_t* actions_dev, void* obs_dev, double* rewards_dev, uint8_t* done_dev,
-                      uint8_t* trunc_dev, uint8_t* listed_dev, uint8_t* reset_dev, hipStream_t s) {
-    Dev& d = h->d;
-    const int p = h->rpar, q = 1 - p;
-    d.pol_n = h->graph_pol;
-    d.pol_step = h->graph_pol ? h->d_gstep : nullptr;
-    d.tail_cnt0 = h->d_rcount + p;
-    d.tail_cnt1 = nullptr;
-    d.tail_step = h->graph_pol ? h->d_gstep : nullptr;
-    FsArgs a;
-    a.actions = actions_dev;
-    a.rew = rewards_dev;
-    a.done = done_dev;
-    a.trunc = trunc_dev;
-    a.listed = listed_dev;
-    a.reset_out = reset_dev;
-    a.rlist = h->d_rlist[q];
-    a.rcount = h->d_rcount + q;
-    a.err = h->d_err;
-    a.obs = obs_dev;
-    a.done_ctr = h->d_fsctr;
-    a.L = h->fs_l;
-    int i0 = -1, i1 = -1;
-    if (h->prof) HIPCHK(hipEventRecord(prof_event(h, &i0), s));
-    const hipError_t le = launch_fstep(h->G, d.obs_dtype, obs_count(d.obs_scope, d.reward_mode, d.A), h->fs_sh,
-                                       (unsigned)h->fs_grid, s, d, a);
-    d.pol_n = 0, d.pol_step = nullptr;
-    d.tail_cnt0 = d.tail_cnt1 = nullptr, d.tail_step = nullptr;
-    if (le != hipSuccess) return fail(ZS_EHIP, std::string("k_fstep: ") + hipGetErrorString(le));
-    if (h->prof) {
-        HIPCHK(hipEventRecord(prof_event(h, &i1), s));
-        h->ev_tick.push_back({i0, i1});
-    }
-    h->rpar = q;
-    return ZS_OK;
-}
-
 extern "C" int zs_step(zs_handle* h, const int32_t* actions_dev, void* obs_dev, double* rewards_dev, uint8_t* done_dev,
                        uint8_t* trunc_dev, uint8_t* listed_dev, uint8_t* reset_dev, void* stream) {
     if (!h || !actions_dev || !rewards_dev || !done_dev || !trunc_dev) return fail(ZS_EINVAL, "null argument");
     hipStream_t s = (hipStream_t)stream;
     HIPCHK(hipSetDevice(h->device));
-    if (h->fstep && obs_dev) return step_fstep(h, actions_dev, obs_dev, rewards_dev, done_dev, trunc_dev, listed_dev,
-                                               reset_dev, s);
     // 1) rebuild the envs that ended at the previous call (list[p]); fused into the tick launch
     //    when the LDS images allow, else a k_reset launch first
     int q = 1 - h->rpar, rc = ZS_OK;
@@ -1377,7 +1240,7 @@ extern "C" int zs_step(zs_handle* h, const int32_t* actions_dev, void* obs_dev, 
         // starts the policy first: C3 173 M env-steps/s, against 167 with the reset launch captured first
         // and 169 with the policy inside the step launch); otherwise inside the step launch (no launch,
         // no gap: 8 192 envs 110 -> 117 M env-steps/s)
-        if (h->graph_pol && side && h->ov.pol_tick <= 0) {
+        if (h->graph_pol && side) {
             const int n = h->d.N * h->d.A;
             hipLaunchKernelGGL(k_gen_actions_ctr, dim3((n + 255) / 256), dim3(256), 0, s, h->d,
                                (const uint64_t*)h->d_gstep, h->graph_pol, (int32_t*)actions_dev);
@@ -1394,7 +1257,7 @@ extern "C" int zs_step(zs_handle* h, const int32_t* actions_dev, void* obs_dev, 
             d.pol_step = st;
         }
         ~PolScope() { d.pol_n = 0, d.pol_step = nullptr; }
-    } pol(h->d, side && h->ov.pol_tick <= 0 ? 0 : h->graph_pol, side && h->ov.pol_tick <= 0 ? nullptr : h->d_gstep);
+    } pol(h->d, side ? 0 : h->graph_pol, side ? nullptr : h->d_gstep);
     // 2) tick every other env; envs that end now are queued on list[q] for the next call.
     // Work-list counters: between calls the list the next step appends to (list[1 - rpar]) and the
     // deferred-respawn list are empty.  This step appends to list[q] and resp_list, drains list[p] and
@@ -1696,15 +1559,15 @@ extern "C" int zs_profile_read(zs_handle* h, double* out) {
 extern "C" int zs_describe(zs_handle* h, char* buf, int32_t len) {
     if (!h || !buf || len <= 0) return fail(ZS_EINVAL, "null argument");
     const Dev& d = h->d;
-    const char* obs_kernel = h->fstep ? "k_fstep" : d.fobs ? "step launch"
-                             : h->obs_pipe ? (h->obs_ring ? "k_obs_ring" : h->obs_patch ? "k_obs_patch" : h->obs_lds ? "k_obs_lds" : "k_obs_pipe")
-                             : h->obs_bring ? (h->obs_bring_pad ? "k_obs_pbring" : "k_obs_bring") : h->obs_gather ? "k_obs_gather" : "k_obs";
+    const char* obs_kernel = d.fobs ? "step launch"
+                             : h->obs_pipe ? (h->obs_ring ? "k_obs_ring" : h->obs_patch ? "k_obs_patch" : "k_obs_pipe")
+                             : h->obs_bring ? "k_obs_pbring" : h->obs_gather ? "k_obs_gather" : "k_obs";
     snprintf(buf, (size_t)len,
              "{\"envs\": %d, \"entities\": %d, \"lanes_per_env\": %d, \"step_kernel\": \"%s\", \"step_lds\": %zu, "
              "\"step_wgs_per_cu\": %d, \"rng_window\": %d, \"obs_kernel\": \"%s\", \"reset_side_stream\": %d, "
              "\"reset_lds\": %zu, \"respawn\": \"%s\", \"tick_waves\": %d, \"rng_step\": %d, \"par_exec\": %d}",
-             d.N, d.E, h->G, h->fstep ? "k_fstep" : h->fused ? "k_step" : "k_tick", h->lds, h->resident, d.rw_cap, obs_kernel,
-             h->fstep ? 0 : h->reset_side,
+             d.N, d.E, h->G, h->fused ? "k_step" : "k_tick", h->lds, h->resident, d.rw_cap, obs_kernel,
+             h->reset_side,
              h->reset_lds, d.defer_respawn ? "k_respawn" : "tick", h->fused ? ZS_FUSED_WAVES : h->tick_waves, d.rw_step,
              d.par_exec);
     return ZS_OK;

@@ -26,12 +26,8 @@ static void launch_nb(const ObsLaunch& o, hipStream_t s, const Dev& d) {
         if (o.patched) hipLaunchKernelGGL((k_obs_ring<TT, NB, true>), g, b, o.lds, s, d, out, o.L, o.env0, o.env1);
         else hipLaunchKernelGGL((k_obs_ring<TT, NB, false>), g, b, o.lds, s, d, out, o.L, o.env0, o.env1);
         break;
-    case OBSK_BRING:
-        if (o.patched) hipLaunchKernelGGL((k_obs_pbring<TT, NB>), g, b, o.lds, s, d, out, o.env0, o.env1, o.us);
-        else hipLaunchKernelGGL((k_obs_bring<TT, NB>), g, b, o.lds, s, d, out, o.L, o.env0, o.env1, o.us);
-        break;
+    case OBSK_BRING: hipLaunchKernelGGL((k_obs_pbring<TT, NB>), g, b, o.lds, s, d, out, o.env0, o.env1, o.us); break;
     case OBSK_PATCH: hipLaunchKernelGGL((k_obs_patch<TT, NB>), g, b, o.lds, s, d, out, o.env0, o.env1); break;
-    case OBSK_LDS: hipLaunchKernelGGL((k_obs_lds<TT, NB>), g, b, o.lds, s, d, out, o.L, o.env0, o.env1); break;
     case OBSK_PIPE: hipLaunchKernelGGL((k_obs_pipe<TT, NB>), g, b, o.lds, s, d, out, o.L, o.env0, o.env1); break;
     default: hipLaunchKernelGGL((k_obs_gather<TT, NB>), g, b, o.lds, s, d, out, o.mask, o.L, o.stat); break;
     }
@@ -47,14 +43,14 @@ hipError_t ZS_OBS_FN(launch_obs)(const ObsLaunch& o, hipStream_t s, const Dev& d
     return hipGetLastError();
 }
 
-// raise a kernel's dynamic-LDS limit past 64 KiB (k_obs_ring / k_obs_patch / k_obs_bring)
+// raise a kernel's dynamic-LDS limit past 64 KiB (k_obs_ring / k_obs_patch / k_obs_pbring)
 hipError_t ZS_OBS_FN(obs_lds_attr)(int kind, int nobs, int patched, int bytes) {
     const void* fn = nullptr;
 #define ZS_FN3(K) (nobs == 1 ? (const void*)K<TT, 1> : nobs == 2 ? (const void*)K<TT, 2> : (const void*)K<TT, 4>)
     if (kind == OBSK_PATCH) {
         fn = ZS_FN3(k_obs_patch);
     } else if (kind == OBSK_BRING) {
-        fn = patched ? ZS_FN3(k_obs_pbring) : ZS_FN3(k_obs_bring);
+        fn = ZS_FN3(k_obs_pbring);
     } else if (kind == OBSK_RING) {
         if (patched)
             fn = nobs == 1 ? (const void*)k_obs_ring<TT, 1, true>

@@ -37,9 +37,6 @@ hipError_t ZS_CAT(launch_tick_g, ZS_G)(int fused, int waves, unsigned grid, size
     if (fused)
         hipLaunchKernelGGL(k_step<G>, dim3(grid + a.n_reset), dim3(64), lds, s, d, a.n_reset, a.actions, a.rew, a.done,
                            a.trunc, a.listed, a.reset_out, a.rlist, a.rcount, a.cur_list, a.cur_count, a.err, a.obs);
-    else if (waves == 5 && a.early)
-        hipLaunchKernelGGL((k_tick<G, 5, true>), dim3(grid), dim3(64), lds, s, d, a.actions, a.rew, a.done, a.trunc,
-                           a.listed, a.reset_out, a.rlist, a.rcount, a.obs, a.env0, a.env1);
     else if (waves == 5)
         hipLaunchKernelGGL((k_tick<G, 5>), dim3(grid), dim3(64), lds, s, d, a.actions, a.rew, a.done, a.trunc, a.listed,
                            a.reset_out, a.rlist, a.rcount, a.obs, a.env0, a.env1);

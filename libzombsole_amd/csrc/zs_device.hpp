@@ -99,7 +99,6 @@ struct Dev {
     int lists_cap;   // static spawn-list entries staged in LDS per workgroup (0 = read from global)
     int rlists_cap;  // the same for the reset work (k_reset has its own LDS budget; = lists_cap when fused)
     int fobs;        // observations are written by the step launch itself (tick and reset work)
-    int fobs_pipe;   // ... by the tick's k_obs_pipe walk (zs_tick.hpp fobs_pipe): observations per env, else 0
     int defer_respawn;  // zombie respawn left to k_respawn (wave per env) instead of the tick's leader
     int par_exec;       // the env's lanes execute the shuffled actions (zs_tick.hpp grp_execute), else its leader
     ObsLayout obsl;  // one env's observation image (zs_obs.hpp)

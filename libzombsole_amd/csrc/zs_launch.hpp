@@ -26,7 +26,6 @@ struct TickArgs {
     const int* cur_list;  // k_step: the pending list this step drains
     const int* cur_count;
     int* err;
-    int early;           // k_tick: the RNG window's first 4G words loaded with the first load round (EARLY)
 };
 
 #define ZS_TICK_DECL(G)                                                                                          \
@@ -42,76 +41,8 @@ ZS_TICK_DECL(32)
 ZS_TICK_DECL(64)
 #undef ZS_TICK_DECL
 
-// k_fstep (zs_fstep.hpp): the step as one launch with tick, encoder and writer waves per workgroup.
-// Role shapes (tick, encoder, writer waves) per instance; FsShape picks one by name.
-#define FS_MAX_UNITS 512  // tick units per workgroup (ready flags in LDS)
-struct FsShape {
-    int nt, nen, nw;
-};
-
-// LDS of a k_fstep workgroup: the padded-table encoder's static tables, nen encoder regions, `us` ring
-// slots, nt tick regions (each the tick's image of one unit, or the reset image of one env), the dirty
-// masks of the workgroup's envs (published by the tick waves), then the ring protocol words, the units'
-// ready flags and the unit counter.
-struct FsLayout {
-    int nt, nen;
-    int off_enc, enc_bytes;
-    int off_slots, slot_bytes, us;
-    int off_tick, tick_bytes;
-    int off_dq;
-    int off_state, off_ready, off_ctr;
-    int bytes;
-};
-
-__host__ __device__ inline FsLayout fs_layout(FsShape sh, int stat_bytes, int enc_bytes, int slot_bytes, int us,
-                                              int tick_bytes, int envs_per_wg) {
-    FsLayout L;
-    L.nt = sh.nt;
-    L.nen = sh.nen;
-    int o = ((stat_bytes + 15) / 16) * 16;
-    L.off_enc = o;
-    L.enc_bytes = ((enc_bytes + 15) / 16) * 16;
-    o += sh.nen * L.enc_bytes;
-    L.off_slots = o;
-    L.slot_bytes = ((slot_bytes + 15) / 16) * 16;
-    L.us = us;
-    o += us * L.slot_bytes;
-    L.off_tick = o;
-    L.tick_bytes = ((tick_bytes + 15) / 16) * 16;
-    o += sh.nt * L.tick_bytes;
-    L.off_dq = o;
-    o += ((8 * envs_per_wg + 15) / 16) * 16;
-    L.off_state = o;
-    o += 16 * 4;
-    L.off_ready = o;
-    o += FS_MAX_UNITS * 4;
-    L.off_ctr = o;
-    o += 16;
-    L.bytes = o;
-    return L;
-}
-
-struct FsArgs {
-    const int32_t* actions;
-    double* rew;
-    uint8_t* done;
-    uint8_t* trunc;
-    uint8_t* listed;
-    uint8_t* reset_out;
-    int* rlist;        // the pending-reset list this step appends to (the next step's resets)
-    int* rcount;
-    int* err;
-    void* obs;
-    int* done_ctr;     // workgroups finished (the last one does the step's tail, then zeroes it)
-    FsLayout L;
-};
-
-// the instances of k.fstep.hip: shape `sh` for (G, dtype, observations per env); hipErrorNotSupported when none
-hipError_t launch_fstep(int G, int dtype, int nobs, FsShape sh, unsigned grid, hipStream_t s, const Dev& d, const FsArgs& a);
-hipError_t fstep_attr(int G, int dtype, int nobs, FsShape sh, int bytes);
-
 // observation kernels
-enum { OBSK_OBS = 0, OBSK_GATHER, OBSK_PIPE, OBSK_LDS, OBSK_PATCH, OBSK_RING, OBSK_BRING };
+enum { OBSK_OBS = 0, OBSK_GATHER, OBSK_PIPE, OBSK_PATCH, OBSK_RING, OBSK_BRING };
 struct ObsLaunch {
     int kind;         // OBSK_*
     int nobs;         // 1, 2 or 4 (k_obs: any)
@@ -124,7 +55,7 @@ struct ObsLaunch {
     ObsLayout L;
     int env0, env1;
     int stat;         // k_obs: static words staged; k_obs_gather: static words from LDS tables
-    int us;           // k_obs_bring: unit slots of the ring
+    int us;           // k_obs_pbring: unit slots of the ring
 };
 #define ZS_OBS_DECL(T)                                                              \
     hipError_t launch_obs_##T(const ObsLaunch& o, hipStream_t s, const Dev& d); \

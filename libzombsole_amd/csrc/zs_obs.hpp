@@ -651,15 +651,16 @@ __global__ void __launch_bounds__(256, ZS_OBS_PIPE_WAVES) k_obs_pipe(Dev d, T* o
 }
 
 // ---------------------------------------------------------------------------
-// k_obs_lds: k_obs_pipe's persistent walk and register prefetch, but each observation block
-// (3 x 441 values, channels encoding) is first computed into a wave-private LDS slot, laid out at
-// the destination's 16-B phase, and then streamed out as 16-B stores: every full 16-B chunk of the
-// block is one aligned global_store_dwordx4 (half the store instructions of per-cell int64 stores,
-// an eighth of int16 ones) and the stream carries no lookups between its stores; the partial chunks
-// at the block's two ends are element stores.  tools/probe/storebw.hip: this store shape 6.0 TB/s.
-// The slot holds the values in the narrowest lossless type (obs_stage_t: int32 for int64 output —
-// every channel value is an int32: codes, lives, weapon codes), widened by the flush, so an int64
-// block stages in 5.3 KB instead of 10.6 KB and four workgroups (16 waves) fit a CU.
+// LDS-staged 16-B stores (k_obs_patch, k_obs_ring, k_obs_pbring): each observation block (3 x 441
+// values, channels encoding) is first computed into an LDS slot, laid out at the destination's 16-B
+// phase, and then streamed out as 16-B stores: every full 16-B chunk of the block is one aligned
+// global_store_dwordx4 (half the store instructions of per-cell int64 stores, an eighth of int16 ones)
+// and the stream carries no lookups between its stores; the partial chunks at the block's two ends are
+// element stores.  tools/probe/storebw.hip: this store shape 6.0 TB/s.  The slot holds the values in the
+// narrowest lossless type (obs_stage_t: int32 for int64 output — every channel value is an int32: codes,
+// lives, weapon codes), widened by the flush, so an int64 block stages in 5.3 KB instead of 10.6 KB.
+// (Round 6 removed k_obs_lds, k_obs_pipe's walk over this flush without writer waves: the ring and the
+// padded-table kernel replaced it wherever it was the pick.)
 // ---------------------------------------------------------------------------
 template <typename T> struct obs_stage { typedef T type; };
 template <> struct obs_stage<int64_t> { typedef int32_t type; };
@@ -881,81 +882,8 @@ __global__ void __launch_bounds__(256) k_obs_gather(Dev d, T* out, const uint8_t
     }
 }
 
-template <typename T, int NOBS>
-__global__ void __launch_bounds__(256, ZS_OBS_PIPE_WAVES) k_obs_lds(Dev d, T* out, ObsLayout L, int env0, int env1) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) step_tail(d);  // a zs_step's tail (Dev::tail_*)
-    extern __shared__ __align__(16) uint8_t smem[];
-    typedef typename obs_stage<T>::type S;
-    constexpr int WW = 21, PLANE = WW * WW, TS = (int)sizeof(T);
-    constexpr int SLOT = obs_stage_slot_bytes(TS);
-    // the wave index (hence the env and every block address) is wave-uniform: scalar registers, and
-    // the buffer resources of the flush need no waterfall loop
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const int stat_words = 4 * d.DW;
-    lv4u* st4 = (lv4u*)smem;
-    obs_stage_static4(d, st4, threadIdx.x, blockDim.x);
-    __syncthreads();
-    // every wave strides over [env0, env1) by the launch's wave count, XCD-contiguous blocks of envs per
-    // round (walking one region of envs per XCD instead measured no faster with the encoding on)
-    const int waves = gridDim.x * 4;
-    int e = env0 + xcd_remap(blockIdx.x, gridDim.x) * 4 + wave;
-    if (e >= env1) return;
-    lu8* img = (lu8*)(smem + stat_words * 4 + wave * (L.bytes + SLOT));
-    lu8* slot = img + L.bytes;  // 16-B aligned: the static tables, L.bytes and SLOT are multiples of 16
-    const li32* pos = (const li32*)(img + L.off_pos);
-    const int code_s = lane < d.A ? d.agent_codes[lane < d.A ? lane : 0] : (lane < d.A + d.P ? ZS_THING_PLAYER : ZS_THING_ZOMBIE);
-    auto build = [&](const ObsPrefetch& f) { obs_build_compact(d, L, img, f, code_s, lane); };
-    // Two envs of prefetch in flight: the loads of env e + 2 * waves are issued before the stores of
-    // env e and consumed after those of env e + waves, so a load has two envs' store streams to
-    // return in.  Between the loads and the wait for them everything is straight-line (agents
-    // unrolled, flush stores unconditional), so that wait leaves the stores in flight.
-    auto process = [&](int e) {
-        wave_sync();
-        obs_window_compact<NOBS>(d, L, img, lane);
-        wave_sync();
-#pragma unroll
-        for (int a = 0; a < NOBS; a++) {
-            const int32_t ap = pos[a];
-            const int ox = unpack_x(ap) - WW / 2, oy = unpack_y(ap) - WW / 2;
-            const lu8* wm = img + a * PLANE;
-            T* o = out + ((size_t)e * NOBS + a) * 3 * PLANE;
-            ZS_LDS S* ot = (ZS_LDS S*)slot + (int)((uintptr_t)o & 15) / TS;
-            if (!(ZS_OBS_DIAG & 16))  // diagnostic builds: 16 skips the encoding, 8 the stores
-                obs_encode_block<S>(d, L, st4, img, wm, ox, oy, ot, lane);
-            wave_sync();
-            if (!(ZS_OBS_DIAG & 8)) obs_stage_flush(slot, o, lane);
-            wave_sync();
-        }
-    };
-    ObsPrefetch fa, fb;
-    {
-        const int e1 = min(e + waves, env1 - 1);
-        obs_prefetch(d, e, min(e + 2 * waves, env1 - 1), OBS_OWN_ROWS, fa);
-        obs_prefetch(d, e1, min(e1 + 2 * waves, env1 - 1), obs_dirty(d, e1), fb);
-    }
-    build(fa);
-    for (;;) {
-        {
-            const int en = min(e + 2 * waves, env1 - 1);
-            obs_prefetch(d, en, min(en + 2 * waves, env1 - 1), fa.dirty_ahead, fa);
-        }
-        process(e);
-        e += waves;
-        if (e >= env1) break;
-        build(fb);
-        {
-            const int en = min(e + 2 * waves, env1 - 1);
-            obs_prefetch(d, en, min(en + 2 * waves, env1 - 1), fb.dirty_ahead, fb);
-        }
-        process(e);
-        e += waves;
-        if (e >= env1) break;
-        build(fa);
-    }
-}
-
 // ---------------------------------------------------------------------------
-// k_obs_patch: k_obs_lds's walk, prefetch and 16-B flush, with a cheaper encoder.  A window cell's
+// k_obs_patch: k_obs_pipe's walk and two-env prefetch with the LDS-staged 16-B flush and a cheaper encoder.  A window cell's
 // value is first taken from a padded static table of the map (one LDS read: the code and life the
 // cell shows when no thing stands on it, every obstacle is present at its MAX_LIFE and no body lies
 // there; out-of-bounds cells are Wall(200) entries of the padding), then the few cells whose value
@@ -1262,7 +1190,7 @@ __global__ void __launch_bounds__(64 * PATCH_WPG, ZS_OBS_PIPE_WAVES) k_obs_patch
 }
 
 // ---------------------------------------------------------------------------
-// k_obs_ring: k_obs_lds with the encoding and the store stream on different waves.  A workgroup of
+// k_obs_ring: the LDS-staged flush with the encoding and the store stream on different waves.  A workgroup of
 // RING_ENC encoder waves and RING_WRT writer waves walks envs b, b + G, ... (b = its XCD-contiguous
 // index, G = the grid); encoder waves build an env's image from prefetched registers and encode every
 // agent's block side by side into a ring slot of LDS (at the env's 16-B phase), writer waves stream
@@ -1446,16 +1374,16 @@ __global__ void __launch_bounds__(64 * (RING_ENC + RING_WRT), 1) k_obs_ring(Dev 
 }
 
 // ---------------------------------------------------------------------------
-// k_obs_bring: k_obs_ring's encoder / writer split on maps whose obstacle HP and dead-body rows are
+// k_obs_pbring: k_obs_ring's encoder / writer split on maps whose obstacle HP and dead-body rows are
 // too large for the register prefetch (city128: 3689 obstacles, 512 dead-body words), with
 // k_obs_gather's window-only fetches in the encoders.  An encoder wave takes an env in three load
 // rounds: its entity table and dirty masks; its dead-body and obstacle-present words (a clean chunk
 // from the shared zero / all-present rows) and the HP of its window cells' obstacles (a clean chunk from
 // hp_init; the cells' static words from the workgroup's LDS tables, obs_stage_static4), the rounds
-// software-pipelined so that an item's loads run while the previous one is encoded.  It encodes every agent's block into a ring slot (int32 staging for
-// int64 output), and BRING_WRT writer waves stream the units out as 16-B stores, as in k_obs_ring.
-// Unit slots: as many as fit beside the tables and the encoder images (us, at most 8 / PAIR; 4 for
-// city128's 42-KB int64 envs).
+// software-pipelined so that an item's loads run while the previous one is encoded.  It encodes every
+// agent's block into a ring slot (int32 staging for int64 output), and BRING_WRT writer waves stream the
+// units out as 16-B stores, as in k_obs_ring.  Unit slots: as many as fit beside the tables and the
+// encoder regions (us, at most 8 / PAIR; 5 for city128's 42-KB int64 envs).
 // ---------------------------------------------------------------------------
 // measured at C4 on one MI355X (2 runs each, profiles/r04_ab_c4_*.log): 9 / 3 159.5-159.9 us, 8 / 4 164.5,
 // 8 / 3 170, 5 / 3 184-202, 12 / 3 (4 slots) 201; with the 63-lane cell walk 9 / 3 158.3-159.7, 10 / 2
@@ -1471,217 +1399,20 @@ __global__ void __launch_bounds__(64 * (RING_ENC + RING_WRT), 1) k_obs_ring(Dev 
 #endif
 #define BRING_D 8  // dead-body words per lane (DW <= 512)
 #define BRING_O 2  // obstacle-present words per lane (OW <= 128, O <= 4096)
-__host__ __device__ constexpr int bring_fixed_bytes(int DW, int img_bytes) { return 16 * DW + BRING_ENC * img_bytes + 128; }
 __host__ __device__ constexpr int bring_unit_bytes(int tsize, int nobs) {
     return obs_stage_slot_bytes(tsize, nobs * ring_pair(tsize, nobs));
 }
-// unit slots within `budget` bytes of LDS (below 2: the kernel does not apply)
-__host__ __device__ constexpr int bring_slots(int DW, int img_bytes, int tsize, int nobs, int budget) {
-    return (budget - bring_fixed_bytes(DW, img_bytes)) / bring_unit_bytes(tsize, nobs) < 8 / ring_pair(tsize, nobs)
-               ? (budget - bring_fixed_bytes(DW, img_bytes)) / bring_unit_bytes(tsize, nobs)
-               : 8 / ring_pair(tsize, nobs);
-}
 __device__ __forceinline__ uint32_t chunk_of(uint32_t x, uint32_t m32) { return m32 ? __umulhi(x, m32) : x; }
 
-template <typename T, int NOBS>
-__global__ void __launch_bounds__(64 * (BRING_ENC + BRING_WRT), 1) k_obs_bring(Dev d, T* out, ObsLayout L, int env0, int env1,
-                                                                                int us) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) step_tail(d);  // a zs_step's tail (Dev::tail_*)
-    extern __shared__ __align__(16) uint8_t smem[];
-    typedef typename obs_stage<T>::type S;
-    constexpr int WW = 21, PLANE = WW * WW, PER = PLANE / 63, TS = (int)sizeof(T);
-    static_assert(PLANE % 63 == 0, "63 lanes x PER rows of three");
-    constexpr int PAIR = ring_pair(TS, NOBS), SLOT = obs_stage_slot_bytes(TS, NOBS * PAIR), BLK = NOBS * 3 * PLANE;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    lv4u* st4 = (lv4u*)smem;
-    lu8* slots = (lu8*)(smem + 16 * d.DW + BRING_ENC * L.bytes);
-    ZS_LDS int* state = (ZS_LDS int*)(slots + us * SLOT);  // state[PAIR * slot + h], at most 8 words
-    if (threadIdx.x < 8) state[threadIdx.x] = 0;
-    obs_stage_static4(d, st4, threadIdx.x, blockDim.x);
-    __syncthreads();
-    const int G = gridDim.x, n_units = (env1 - env0 + PAIR - 1) / PAIR;
-    const XcdDeal deal(blockIdx.x, G, n_units, BRING_WRT);
-    const int ucount = deal.ucount;
-    const int count = ucount ? PAIR * (ucount - 1) + min(PAIR, env1 - env0 - PAIR * deal.unit(ucount - 1)) : 0;
-    auto unit_env = [&](int u) { return env0 + PAIR * deal.unit(u); };
-    if (wave >= BRING_ENC) {  // writer
-        for (int u = wave - BRING_ENC; u < ucount; u += BRING_WRT) {
-            const int q = u % us, e = unit_env(u);
-            const bool whole = PAIR * u + PAIR <= count;
-            for (int h = 0; h < PAIR; h++)
-                if (PAIR * u + h < count) ring_wait(&state[PAIR * q + h], 2 * u + 1);
-            if (whole) obs_stage_flush<T, NOBS * PAIR, BRING_THR>(slots + q * SLOT, out + (size_t)e * BLK, lane);
-            else obs_stage_flush<T, NOBS, BRING_THR>(slots + q * SLOT, out + (size_t)e * BLK, lane);
-            for (int h = 0; h < PAIR; h++) ring_state_store(&state[PAIR * q + h], 2 * u + 2);
-        }
-        return;
-    }
-    // encoder
-    lu8* img = (lu8*)(smem + 16 * d.DW + wave * L.bytes);
-    li32* ipos = (li32*)(img + L.off_pos);
-    li32* ilife = (li32*)(img + L.off_life);
-    li32* icw = (li32*)(img + L.off_cw);
-    lu32* idead = (lu32*)(img + L.off_dead);
-    lu32* iopres = (lu32*)(img + L.off_opres);
-    const int code_s = lane < d.A ? d.agent_codes[lane < d.A ? lane : 0] : (lane < d.A + d.P ? ZS_THING_PLAYER : ZS_THING_ZOMBIE);
-    const int W = d.W, H = d.H, sl = lane < d.E ? lane : d.E - 1;
-    // a lane's window cells: lane + 63 i, row lr + 3 i, column lq (lane 63 repeats lane 0's next cell)
-    const int lr = lane / WW, lq = lane - lr * WW;
-    auto item_env = [&](int t) { return unit_env(t / PAIR) + t % PAIR; };
-    if (wave >= count) return;
-    // Three load rounds per item, software-pipelined over two register sets: while item t is encoded,
-    // the second and third rounds of item t + BRING_ENC and the first of item t + 2 BRING_ENC are in
-    // flight (items past the wave's last re-read its first env).
-    struct R1 {  // entity slot `lane`, dirty masks
-        int32_t p, l, w, r;
-        uint32_t hd, dd;
-    };
-    struct R23 {  // dead-body and present words; the HP of the window cells' obstacles
-        uint32_t dv[BRING_D], ov[BRING_O];
-        int32_t hv[NOBS][PER];
-    };
-    auto envc = [&](int t) { return item_env(t < count ? t : wave); };
-    auto round1 = [&](int t, R1& r) {
-        const int e = envc(t);
-        r.p = d.pos[EIX(d, sl, e)];
-        r.l = d.life[EIX(d, sl, e)];
-        r.w = d.weapon[EIX(d, sl, e)];
-        r.r = d.present[EIX(d, sl, e)];
-        r.hd = d.hp_dirty[e];
-        r.dd = d.dead_dirty[e];
-    };
-    // every load unconditional, addresses clamped; a window cell's obstacle index from the LDS tables
-    // (the cell's rank among the map's obstacle cells, 0 where none: discarded by the encoding)
-    auto round23 = [&](int t, const R1& r, R23& q) {
-        const int e = envc(t);
-        const uint32_t* dr = d.dead + (size_t)e * d.DW;
-#pragma unroll
-        for (int i = 0; i < BRING_D; i++) {
-            const int w = min(lane + 64 * i, d.DW - 1);
-            q.dv[i] = (((r.dd >> chunk_of((uint32_t)w, d.dead_chunk_m32)) & 1u) ? dr : d.dead_zero)[w];
-        }
-        const uint32_t* orow = r.hd ? d.obst_present + (size_t)e * d.OW : d.opres_full;
-#pragma unroll
-        for (int i = 0; i < BRING_O; i++) q.ov[i] = orow[min(lane + 64 * i, max(d.OW - 1, 0))];
-        const int32_t* hrow = d.obst_hp + (size_t)e * d.O;
-#pragma unroll
-        for (int a = 0; a < NOBS; a++) {
-            const int32_t ap = __builtin_amdgcn_readlane(r.p, a);
-            const int ox = unpack_x(ap) - WW / 2, oy = unpack_y(ap) - WW / 2;
-            const bool xin = (unsigned)(ox + lq) < (unsigned)W;
-            const int c0 = (oy + lr) * W + ox + lq;
-#pragma unroll
-            for (int i = 0; i < PER; i++) {
-                const int y = oy + lr + 3 * i;
-                const bool inb = xin && (unsigned)y < (unsigned)H;
-                const int c = inb ? c0 + 3 * i * W : 0;
-                const uint32_t bit = 1u << (c & 31);
-                const zs_v4u sw = st4[c >> 5];
-                const int o = (sw.x & bit) ? (int)(sw.w + __popc(sw.x & (bit - 1u))) : 0;
-                q.hv[a][i] = (((r.hd >> chunk_of((uint32_t)o, d.hp_chunk_m32)) & 1u) ? hrow : d.hp_init)[o];
-            }
-        }
-    };
-    // the image of an item: entity table, dead-body and present words, window maps
-    auto build = [&](const R1& r, const R23& q) {
-        for (int w = lane; w < L.win / 4; w += 64) ((lu32*)img)[w] = 0u;
-        if (lane < d.E) {
-            ipos[lane] = r.p;
-            ilife[lane] = r.l;
-            icw[lane] = code_s | (r.w << 8) | (r.r << 16);
-        }
-#pragma unroll
-        for (int i = 0; i < BRING_D; i++)
-            if (lane + 64 * i < d.DW) idead[lane + 64 * i] = q.dv[i];
-#pragma unroll
-        for (int i = 0; i < BRING_O; i++)
-            if (lane + 64 * i < d.OW) iopres[lane + 64 * i] = q.ov[i];
-        wave_sync();
-        if (lane < d.E && r.r) {  // every present entity's slot + 1 in each agent's window
-            const int x = unpack_x(r.p), y = unpack_y(r.p);
-#pragma unroll
-            for (int a = 0; a < NOBS; a++) {
-                const int32_t ap = ipos[a];
-                const int dx = x - (unpack_x(ap) - WW / 2), dy = y - (unpack_y(ap) - WW / 2);
-                if (dx >= 0 && dy >= 0 && dx < WW && dy < WW) img[a * PLANE + dy * WW + dx] = (uint8_t)(lane + 1);
-            }
-        }
-    };
-    // every agent's block of item t into its unit's slot
-    auto encode = [&](int t, const R23& q) {
-        const int u = t / PAIR, h = t % PAIR, e = item_env(t);
-        const int qs = u % us;
-        if (u >= us) ring_wait(&state[PAIR * qs + h], 2 * (u - us) + 2);
-        wave_sync();
-        ZS_LDS S* ot0 = (ZS_LDS S*)(slots + qs * SLOT) + (int)((uintptr_t)(out + (size_t)(e - h) * BLK) & 15) / TS + h * BLK;
-#pragma unroll
-        for (int a = 0; a < NOBS; a++) {
-            const int32_t ap = ipos[a];
-            const int ox = unpack_x(ap) - WW / 2, oy = unpack_y(ap) - WW / 2;
-            const lu8* wm = img + a * PLANE;
-            ZS_LDS S* ot = ot0 + a * 3 * PLANE;
-            const bool xin = (unsigned)(ox + lq) < (unsigned)W;
-            const int c0 = (oy + lr) * W + ox + lq;
-#pragma unroll
-            for (int i = 0; i < PER; i++) {
-                const int cell = lane + 63 * i, cc = i < PER - 1 ? cell : min(cell, PLANE - 1);
-                const int y = oy + lr + 3 * i;
-                const bool inb = xin && (unsigned)y < (unsigned)H;
-                const int c = inb ? c0 + 3 * i * W : 0;
-                const uint32_t bit = 1u << (c & 31);
-                const int sb = wm[cc];
-                const int v = icw[sb ? sb - 1 : 0], elife = ilife[sb ? sb - 1 : 0];
-                const zs_v4u sw = st4[c >> 5];
-                const uint32_t isob = (sw.x & bit) ? 1u : 0u;
-                const int oi = isob ? (int)(sw.w + __popc(sw.x & (bit - 1u))) : 0;
-                // unconditional read (oi 0 off an obstacle): a read under the test became a branch per cell
-                const bool obp = (isob & (iopres[oi >> 5] >> (oi & 31))) & 1u;
-                int code = (idead[c >> 5] & bit) ? ZS_THING_DEADBODY : (sw.z & bit) ? ZS_THING_OBJECTIVE : ZS_THING_NONE;
-                code = obp ? ((sw.y & bit) ? ZS_THING_BOX : ZS_THING_WALL) : code;
-                code = sb ? (v & 255) : code;
-                code = inb ? code : ZS_THING_WALL;
-                int life = sb ? elife : (obp ? q.hv[a][i] : 0);
-                life = inb ? life : 200;
-                const int weapon = (inb && sb) ? ((v >> 8) & 255) : 0;
-                if (cell < PLANE) {
-                    ot[cell] = (S)code;
-                    ot[PLANE + cell] = obs_val<S>(life);
-                    ot[2 * PLANE + cell] = (S)weapon;
-                }
-            }
-        }
-        ring_state_store(&state[PAIR * qs + h], 2 * u + 1);
-        wave_sync();  // the image is rebuilt for the next item
-    };
-    R1 ra, rb;
-    R23 qa, qb;
-    int t = wave;
-    round1(t, ra);
-    round1(t + BRING_ENC, rb);
-    round23(t, ra, qa);
-    // item t from set a while set b's later rounds run, then the roles swap
-    auto step = [&](int t, R1& rx, R23& qx, R1& ry, R23& qy) {
-        build(rx, qx);
-        round23(t + BRING_ENC, ry, qy);
-        round1(t + 2 * BRING_ENC, rx);
-        encode(t, qx);
-    };
-    for (; t < count; t += 2 * BRING_ENC) {
-        step(t, ra, qa, rb, qb);
-        if (t + BRING_ENC < count) step(t + BRING_ENC, rb, qb, ra, qa);
-    }
-}
-
 // ---------------------------------------------------------------------------
-// k_obs_pbring: k_obs_bring with the things written over the window afterwards instead of looked up per
-// cell.  k_obs_bring builds, per env, a map of every agent's window holding the slot of the thing on each
-// cell and reads it (and the thing's code, weapon and life) for every cell; here a cell costs its static
-// word (obstacle, Box, objective bits and obstacle rank: the LDS tables of obs_stage_static4), the present
-// bit of its obstacle, its dead-body bit and, for an obstacle, the HP its load round fetched
-// (gym/observation.py:57-90: present obstacle > dead body > objective > empty), and then each present thing's
-// lane (slot s on lane s) writes its code, life and weapon into every window it falls in (a thing takes
-// precedence over everything on its cell).  The encoder's LDS region holds only the dead-body and present
-// words.  Load rounds, ring and writers as k_obs_bring.
+// The encoding (round 5): a window cell costs its static word (obstacle, Box, objective bits and obstacle
+// rank: the LDS tables of obs_stage_static4), the present bit of its obstacle, its dead-body bit and, for
+// an obstacle, the HP its load round fetched (gym/observation.py:57-90: present obstacle > dead body >
+// objective > empty), and then each present thing's lane (slot s on lane s) writes its code, life and
+// weapon into every window it falls in (a thing takes precedence over everything on its cell).  The
+// encoder's LDS region holds only the dead-body and present words.  (Round 6 removed k_obs_bring, the
+// first form, which built per env a map of the thing on every window cell and looked it up per cell:
+// 157.7 against 151.1 us at C4, profiles/r05f_ab_pbring.log.)
 // ---------------------------------------------------------------------------
 __host__ __device__ constexpr int pbring_enc_bytes(int DW, int OW) { return ((DW * 4 + 15) / 16) * 16 + ((OW * 4 + 15) / 16) * 16; }
 __host__ __device__ constexpr int pbring_fixed_bytes(int DW, int OW) { return 16 * DW + BRING_ENC * pbring_enc_bytes(DW, OW) + 128; }

@@ -1446,116 +1446,6 @@ __device__ __forceinline__ void misc_store(const Dev& d, int f, int e, int v) {
     else *misc_word(d, f, e) = v;
 }
 
-// ---------------------------------------------------------------------------
-// Observations written by the step launch itself (Dev::fobs_pipe, zs_launch.fobs), for the registered
-// shape k_obs_pipe serves (surroundings of width 21, static tables, staged HP, window map): the tick
-// wave, right after its stage-out, runs k_obs_pipe's walk over its own stepping envs.  The entity
-// tables come from the tick's LDS, the dead-body / present / HP words are loaded one env ahead (a clean
-// chunk from the shared rows), the compact image and the static tables alias the dead tick region, and
-// the cells go out as per-cell stores (obs_cell_lds, obs_store).  The step's stores then start as each
-// workgroup finishes its tick instead of after the slowest one, and the separate observation launch
-// (its dispatch, first load round and drain) is gone.
-// ---------------------------------------------------------------------------
-template <typename T>
-__device__ __forceinline__ void fobs_pipe_env(const Dev& d, const ObsLayout& L, const lv4u* st4, const lu8* img, T* out,
-                                              int e, int nobs, int lane) {
-    constexpr int WW = 21, PLANE = WW * WW, PER = (PLANE + 63) / 64;
-    const li32* pos = (const li32*)(img + L.off_pos);
-    const bool ch = d.obs_enc == ZS_ENC_CHANNELS;
-    const int C = ch ? 3 : 1;
-#pragma unroll 1
-    for (int a = 0; a < nobs; a++) {
-        const int32_t ap = pos[a];
-        const int ox = unpack_x(ap) - WW / 2, oy = unpack_y(ap) - WW / 2;
-        const lu8* wm = img + a * PLANE;
-        T* o = out + ((size_t)e * nobs + a) * C * PLANE;
-#pragma unroll
-        for (int i = 0; i < PER; i++) {
-            const int cell = lane + 64 * i;
-            const int cc = cell < PLANE ? cell : PLANE - 1;
-            const int r = cc / WW, q = cc - r * WW;
-            int code, lf, weapon;
-            obs_cell_lds(d, L, st4, img, wm, cc, ox + q, oy + r, code, lf, weapon);
-            if (cell < PLANE) obs_store(o, PLANE, cell, ch, code, lf, weapon);
-        }
-    }
-}
-
-template <int NE>
-__device__ __forceinline__ void fobs_pipe(const Dev& d, const Grp& c, uint8_t* region, unsigned long long stepmask,
-                                          int G, int base, void* obs_out) {
-    constexpr int WW = 21, PLANE = WW * WW;
-    const int lane = threadIdx.x & 63;
-    const ObsLayout& L = d.obsl;
-    lv4u* st4 = (lv4u*)region;
-    lu8* img = (lu8*)(region + 16 * d.DW);
-    const int nobs = d.fobs_pipe;
-    const int code_s = lane < d.A ? (d.obs_enc == ZS_ENC_CHANNELS ? d.agent_codes[lane < d.A ? lane : 0] : ZS_THING_AGENT)
-                                  : (lane < d.A + d.P ? ZS_THING_PLAYER : ZS_THING_ZOMBIE);
-    obs_stage_static4(d, st4, lane, 64);
-    // Every word this launch wrote (the tick's HP stores, its dead-body and dirty-mask atomics) is read
-    // with device-scope loads, which bypass the CU's L1: a line the tick loaded earlier may be there.
-    auto ld = [](const void* p) { return __hip_atomic_load((const uint32_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
-    // the envs' dirty masks (lane g: env base + g; a lane past the stepping envs reads env base)
-    const int gl = lane < NE && ((stepmask >> (lane * G)) & 1ull) ? lane : 0;
-    const uint32_t hdl = ld(d.hp_dirty + base + gl), ddl = ld(d.dead_dirty + base + gl);
-    // obs_prefetch_env's dead-body / present / HP words of env e (the entity slots come from LDS)
-    auto prefetch = [&](int g, ObsPrefetch& f) {
-        const int e = base + g;
-        const uint32_t hd = (uint32_t)__builtin_amdgcn_readlane((int)hdl, g), dd = (uint32_t)__builtin_amdgcn_readlane((int)ddl, g);
-        const uint32_t* dr = d.dead + (size_t)e * d.DW;
-#pragma unroll
-        for (int i = 0; i < OBS_PF_D; i++) {
-            const int w = min(lane + 64 * i, d.DW - 1);
-            f.dead[i] = ld((((dd >> ((w * d.dead_chunk_m) >> 20)) & 1u) ? dr : d.dead_zero) + w);
-        }
-        f.opres = ld((hd ? d.obst_present + (size_t)e * d.OW : d.opres_full) + min(lane, max(d.OW - 1, 0)));
-        const int32_t* hr = d.obst_hp + (size_t)e * d.O;
-#pragma unroll
-        for (int i = 0; i < OBS_PF_H; i++) {
-            const int o = min(lane + 64 * i, d.O - 1);
-            f.hp[i] = (int32_t)ld((((hd >> ((o * d.hp_chunk_m) >> 20)) & 1u) ? hr : d.hp_init) + o);
-        }
-    };
-    int g2 = stepmask ? (__ffsll((long long)stepmask) - 1) / G : NE;
-    ObsPrefetch f;
-    if (g2 < NE) prefetch(g2, f);
-    while (g2 < NE) {
-        // this env's entity slots from the tick's LDS tables (lane s: slot s), then its image
-        const int s = lane < d.E ? lane : 0;
-        f.pos = c.lpos[s * NE + g2];
-        f.life = c.llife[s * NE + g2];
-        f.wp = c.lweap[s * NE + g2];
-        f.pr = c.lpres[s * NE + g2];
-        obs_build_compact(d, L, img, f, code_s, lane);
-        // the next stepping env's words, issued ahead of this env's stores
-        const unsigned long long rest = stepmask & ~((2ull << (g2 * G)) - 1ull);
-        const int gn = rest ? (__ffsll((long long)rest) - 1) / G : NE;
-        if (gn < NE) prefetch(gn, f);
-        wave_sync();
-        {  // window maps: every present entity's slot + 1 in each agent's window
-            const li32* pos = (const li32*)(img + L.off_pos);
-            const lv2i* ent = (const lv2i*)(img + L.off_life);
-            if (lane < d.E && ((ent[lane].x >> 16) & 1)) {
-                const int32_t p = pos[lane];
-                const int x = unpack_x(p), y = unpack_y(p);
-                for (int a = 0; a < nobs; a++) {
-                    const int32_t ap = pos[a];
-                    const int dx = x - (unpack_x(ap) - WW / 2), dy = y - (unpack_y(ap) - WW / 2);
-                    if (dx >= 0 && dy >= 0 && dx < WW && dy < WW) img[a * PLANE + dy * WW + dx] = (uint8_t)(lane + 1);
-                }
-            }
-        }
-        wave_sync();
-        const int e = base + g2;
-        if (d.obs_dtype == ZS_DTYPE_I64) fobs_pipe_env(d, L, st4, img, (int64_t*)obs_out, e, nobs, lane);
-        else if (d.obs_dtype == ZS_DTYPE_I32) fobs_pipe_env(d, L, st4, img, (int32_t*)obs_out, e, nobs, lane);
-        else fobs_pipe_env(d, L, st4, img, (int16_t*)obs_out, e, nobs, lane);
-        wave_sync();
-        g2 = gn;
-    }
-}
-
 // word v into every env's copy of LDS row w (IX layout: row w of env g at w * NE + g), one store
 template <int NE>
 __device__ __forceinline__ void bcast_row(lu32* base, int w, uint32_t v) {
@@ -1576,8 +1466,7 @@ __device__ __forceinline__ void bcast_row(lu32* base, int w, uint32_t v) {
 // EARLY (the one-round fused launch, whose register budget has room): the RNG window's first 4G words
 // are loaded in registers right after the first load round and reach LDS only after the decisions, so
 // their round trip (it needs the stream state) overlaps the decisions instead of the stage-in
-// smem: this wave's LDS image (tick_layout); pend (optional): the ballot of the envs this call found
-// pending a reset (bit g * G for env base + g), which the caller's reset work rebuilds (k_fstep)
+// smem: this wave's LDS image (tick_layout)
 #ifndef ZS_TICK_LAUNDER
 #define ZS_TICK_LAUNDER 1
 #endif
@@ -1585,8 +1474,7 @@ __device__ __forceinline__ void bcast_row(lu32* base, int w, uint32_t v) {
 template <int G, bool EARLY = false>
 __device__ __forceinline__ void tick_wg(const Dev& d0, int wg, const int32_t* actions, double* rew, uint8_t* done_out,
                                         uint8_t* trunc_out, uint8_t* listed_out, uint8_t* reset_out, int* reset_list,
-                                        int* reset_count, void* obs_out, int env0, int env1, lu8* smem,
-                                        unsigned long long* pend = nullptr) {
+                                        int* reset_count, void* obs_out, int env0, int env1, lu8* smem) {
     // The Dev fields are read through a pointer re-derived from the kernarg segment at each phase (ZS_TICK_LAUNDER):
     // read through the kernel's by-value argument, the compiler loads them all up front and keeps them in SGPRs
     // for the whole tick (458 SGPR spills into VGPR lanes at G = 8, each use a v_readlane).
@@ -1885,7 +1773,6 @@ __device__ __forceinline__ void tick_wg(const Dev& d0, int wg, const int32_t* ac
     wave_sync();
     STAMP(2);
     ZS_RELOAD_DEV();
-    if (pend) *pend = __ballot(active && leader && !stepping);
     if (active && leader && !stepping) {  // this call is the env's reset; outputs as after env.reset()
         int nr = dp->reward_mode == ZS_REWARD_SINGLE ? 1 : A;
         for (int a = 0; a < nr; a++) rew[(size_t)e * nr + a] = 0.0;
@@ -1997,9 +1884,7 @@ __device__ __forceinline__ void tick_wg(const Dev& d0, int wg, const int32_t* ac
     ZS_RELOAD_DEV();
     // observations of the envs ticked here (envs reset by this call get theirs from the reset work):
     // the whole wave encodes one env at a time, its image aliasing the dead tick region
-    if (dp->fobs && obs_out && dp->fobs_pipe) {
-        fobs_pipe<NE>(*dp, c, (uint8_t*)(smem + L.off_region), __ballot(stepping && leader), G, base, obs_out);
-    } else if (dp->fobs && obs_out) {
+    if (dp->fobs && obs_out) {
         const unsigned long long stepmask = __ballot(stepping && leader);  // bit g * G per stepping env
         lu8* img = (lu8*)(smem + L.off_region);
         lu32* st = dp->obs_stat ? (lu32*)(smem + L.off_region + dp->obsl.bytes) : nullptr;

@@ -135,12 +135,12 @@ PATHS = {
     "obs_k_obs": {"fobs": -1, "obs_pipe": -1, "obs_gather": -1},  # one-env-per-wave k_obs
     "obs_gather": {"fobs": -1, "obs_pipe": -1, "obs_ring": -1},  # window-only fetches (k_obs_gather)
     "obs_gather_scell": {"fobs": -1, "obs_pipe": -1, "obs_ring": -1, "obs_gather_stat": -1},  # ... global static words
-    "obs_bring": {"fobs": -1, "obs_pipe": -1},  # window-only encoders + writer waves (k_obs_bring)
-    "obs_pipe_cells": {"obs_lds": -1},          # k_obs_pipe's per-cell stores instead of k_obs_lds
-    "obs_lds": {"obs_lds": 1},                 # the LDS-staged store stream at any env count (k_obs_patch)
-    "obs_lds_select": {"obs_lds": 1, "obs_patch": -1},  # ... k_obs_lds's per-cell select chain
+    "obs_pbring": {"fobs": -1, "obs_pipe": -1},  # window-only encoders + writer waves (k_obs_pbring)
+    "obs_pipe_cells": {"obs_lds": -1},          # k_obs_pipe's per-cell stores instead of the staged flush
+    "obs_lds": {"obs_lds": 1},                 # the LDS-staged store kernels at any env count
+    "obs_lds_select": {"obs_lds": 1, "obs_patch": -1},  # ... without the padded-table encoder
     "obs_ring": {"obs_lds": 1, "obs_ring": 1},  # encoder / writer waves through an LDS ring
-    "obs_ring_select": {"obs_lds": 1, "obs_ring": 1, "obs_ring_patch": -1},  # ... k_obs_lds's encoders
+    "obs_ring_select": {"obs_lds": 1, "obs_ring": 1, "obs_ring_patch": -1},  # ... select-chain encoders
     "obs_scan": {"obs_win": -1},                # per-cell entity scan instead of the window map
     "obs_scan_in_step": {"obs_win": -1, "fobs": 1},
     "obs_scell": {"obs_stat": -1},              # per-cell static words instead of LDS bitmaps
@@ -211,11 +211,13 @@ def test_step_graph(path):
                16, 30, check_state_every=15, graph=True, launch=GRAPH[path])
 
 
-@pytest.mark.parametrize("patch", [-1, 1])
-def test_store_stream_every_phase(patch):
-    """k_obs_patch / k_obs_lds write each observation block from an LDS slot kept at the destination's
-    16-B phase: int16 blocks of 4 agents (2646 B: every even phase), int32 single-agent blocks (5292 B)."""
-    lo = {"obs_lds": 1, "obs_patch": patch}
+@pytest.mark.parametrize("kernel", ["patch", "ring_select"])
+def test_store_stream_every_phase(kernel):
+    """k_obs_patch and k_obs_ring (here with its select-chain encoders) write each observation block from an
+    LDS slot kept at the destination's 16-B phase: int16 blocks of 4 agents (2646 B: every even phase), int32
+    single-agent blocks (5292 B)."""
+    lo = {"patch": {"obs_lds": 1, "obs_patch": 1, "obs_ring": -1},
+          "ring_select": {"obs_lds": 1, "obs_ring": 1, "obs_ring_patch": -1}}[kernel]
     run_parity(lambda n: _abi.multi_env_config(n, "extermination", [], "bridge64", ["0", "1", "2", "3"],
                                                initial_zombies=20, obs_dtype=_abi.DTYPE_I16, max_episode_steps=200),
                64, 60, check_state_every=30, launch=lo)
@@ -225,15 +227,15 @@ def test_store_stream_every_phase(patch):
                64, 60, n_discrete=6, check_state_every=30, launch=lo)
 
 
-CITY128_OBS = {"pbring": {}, "bring": {"obs_ring_patch": -1}, "gather": {"obs_ring": -1},
+CITY128_OBS = {"pbring": {}, "gather": {"obs_ring": -1},
                "gather_scell": {"obs_ring": -1, "obs_gather_stat": -1}}
 
 
 @pytest.mark.parametrize("path", sorted(CITY128_OBS))
 def test_city128_obs_paths(path):
     """C4's observation kernels: k_obs_pbring (default: window-only encoders, the things written over the
-    windows, writer waves), k_obs_bring (per-cell window maps), k_obs_gather with static words from the
-    LDS tables or one global load per window cell."""
+    windows, writer waves), k_obs_gather with static words from the LDS tables or one global load per window
+    cell."""
     run_parity(lambda n: _abi.multi_env_config(n, "safehouse", [], "city128", ["0", "1", "2", "3"],
                                                initial_zombies=50, minimum_zombies=50),
                24, 30, check_state_every=15, launch=CITY128_OBS[path])

@@ -116,7 +116,7 @@ def run_full(make_builder, n, steps, nd=7, seed0=0, graph=True, twice=0, min_res
 
 
 def test_c3_65536_graph():
-    """The headline (BASELINE metric, C3 at N=1): 65 536 envs, k_obs_lds walking 32 envs per wave."""
+    """The headline (BASELINE metric, C3 at N=1): 65 536 envs, k_tick, the side-stream reset, k_obs_ring."""
     run_full(c3, 65536, 40)
 
 
@@ -152,8 +152,8 @@ def test_c2_4096_graph():
 
 
 def test_c2_4096_one_obs_workgroup_per_cu():
-    """obs_wgs = 1: the persistent observation kernel (k_obs_lds, the int64 ring off) at 1 workgroup
-    per CU walks 4 envs per wave at 4 096."""
+    """obs_wgs = 1: the persistent observation kernel (k_obs_patch, the int64 ring off) at 1 workgroup
+    per CU walks several envs per wave at 4 096."""
     run_full(c3, 4096, 40, seed0=99, launch={"obs_wgs": 1, "obs_lds": 1, "obs_ring": -1})
 
 
@@ -175,7 +175,7 @@ def test_c5_odd_int16_ring_pairs():
 
 
 def test_c2_4096_ring_select_encoders():
-    """k_obs_ring with k_obs_lds's select-chain encoders instead of the padded-table ones."""
+    """k_obs_ring with its select-chain encoders instead of the padded-table ones (its fallback)."""
     run_full(c3, 4096, 40, seed0=4321, launch={"obs_lds": 1, "obs_ring": 1, "obs_ring_patch": -1})
 
 
@@ -207,7 +207,7 @@ def test_c5_65536_int16_truncation_waves():
 
 
 def test_c4_16384_graph():
-    """C4: city128 safehouse, 4 agents + 50 zombies (minimum 50): k_obs_bring (window-only encoders and
+    """C4: city128 safehouse, 4 agents + 50 zombies (minimum 50): k_obs_pbring (window-only encoders and
     writer waves), k_respawn after zombie deaths and safehouse / all-dead autoresets, at full size."""
     def respawned(eng):
         assert eng.describe()["obs_kernel"] == "k_obs_pbring"
@@ -216,13 +216,6 @@ def test_c4_16384_graph():
         assert zd > 0, "no zombie died in the sampled envs: k_respawn untested"
         assert eng.describe()["respawn"] == "k_respawn"
     run_full(c4, 16384, 80, min_resets=1, after=respawned)
-
-
-def test_c4_16384_graph_bring():
-    """C4 through k_obs_bring (per-cell window maps of the things) at full size, respawns and autoresets."""
-    def bring(eng):
-        assert eng.describe()["obs_kernel"] == "k_obs_bring"
-    run_full(c4, 16384, 60, seed0=11, min_resets=1, launch={"obs_ring_patch": -1}, after=bring)
 
 
 def test_c4_4096_gather():
@@ -259,21 +252,6 @@ def test_c2_4096_multistep_graph_odd():
     run_full(lambda n: c3(n, max_steps=10), 4096, 45, seed0=7 * 4096, graph_steps=3, min_resets=1)
 
 
-def test_c3_8192_shard_graph_obs_in_step():
-    """The 8 192-env shard with the observations written by the step launch (zs_launch.fobs: the ticks run
-    k_obs_pipe's walk over their own envs, zs_tick.hpp fobs_pipe; the reset work writes its envs')."""
-    def in_step(eng):
-        assert eng.describe()["obs_kernel"] == "step launch"
-    run_full(c3, 8192, 60, seed0=2 * 8192, launch={"fobs": 1}, after=in_step)
-
-
-def test_c5_8192_int16_obs_in_step():
-    """C5's shard (int16, 4 agents) with the observations written by the step launch; TimeLimit 16, so the
-    reset work (which then writes its envs' observations too) runs every 16 steps."""
-    r = run_full(lambda n: c5(n, max_steps=16), 8192, 40, seed0=5 * 8192, launch={"fobs": 1}, min_resets=2 * 8192)
-    assert r >= 2 * 8192
-
-
 def test_c3_8192_shard_serial_exec():
     """The same shard with the leader's serial execution (zs_launch.par_exec = -1)."""
     run_full(c3, 8192, 40, seed0=2 * 8192, launch={"par_exec": -1})
@@ -308,68 +286,3 @@ def test_c4_16384_multistep_graph_respawn():
     run_full(lambda n: c4(n, max_steps=15), 16384, 48, graph_steps=8, min_resets=2 * 16384, after=check)
 
 
-def _fstep(eng):
-    desc = eng.describe()
-    assert desc["step_kernel"] == "k_fstep" and desc["obs_kernel"] == "k_fstep", desc
-
-
-def test_c3_65536_fstep_graph():
-    """The headline size through the one-launch step (k_fstep: tick, encoder and writer waves in every
-    workgroup), TimeLimit 16: the tick waves rebuild the pending envs of 65 536-env autoreset waves."""
-    r = run_full(lambda n: c3(n, max_steps=16), 65536, 40, launch={"fstep": 1}, min_resets=2 * 65536, after=_fstep)
-    assert r >= 2 * 65536
-
-
-def test_c3_65536_fstep_eager_masked():
-    """k_fstep through eager launches after a masked reset of every third env."""
-    run_full(c3, 65536, 24, graph=False, twice=3, launch={"fstep": 1}, min_resets=0, after=_fstep)
-
-
-def test_c5_65536_fstep_graph():
-    """C5 (int16, 4 agents, env pairs per ring unit) through k_fstep, TimeLimit 12."""
-    run_full(lambda n: c5(n, max_steps=12), 65536, 30, launch={"fstep": 1}, min_resets=2 * 65536, after=_fstep)
-
-
-def test_c5_65535_fstep_odd():
-    """k_fstep over an odd env count (C5's shape: G = 16, int16 env pairs per ring unit): the last tick unit,
-    the last workgroup's range and its last ring unit (a single env) short."""
-    run_full(lambda n: c5(n, max_steps=10), 65535, 25, seed0=31, launch={"fstep": 1}, min_resets=1, after=_fstep)
-
-
-def test_c3_65533_fstep_odd():
-    """The same for C3's shape (G = 8, int64): 65 533 envs, the last tick unit holding five."""
-    run_full(lambda n: c3(n, max_steps=10), 65533, 25, seed0=77, launch={"fstep": 1}, min_resets=1, after=_fstep)
-
-
-def test_c3_65536_fstep_six_tick_waves():
-    """k_fstep's other role shape (six tick waves, seven encoders), TimeLimit 16."""
-    run_full(lambda n: c3(n, max_steps=16), 65536, 34, launch={"fstep": 1, "fs_tick": 6}, min_resets=2 * 65536,
-             after=_fstep)
-
-
-def test_c3_65536_tick_early():
-    """k_tick with the RNG window's first 4G words loaded in its first load round (zs_launch.tick_early),
-    TimeLimit 16."""
-    def early(eng):
-        desc = eng.describe()
-        assert desc["step_kernel"] == "k_tick" and desc["tick_waves"] == 5, desc
-    run_full(lambda n: c3(n, max_steps=16), 65536, 36, launch={"tick_early": 1}, min_resets=2 * 65536, after=early)
-
-
-def test_c5_65536_tick_early_five_waves():
-    """The same on C5's shape (G = 16, E = 24) at five waves per SIMD."""
-    run_full(lambda n: c5(n, max_steps=12), 65536, 28, launch={"tick_early": 1, "tick_waves": 5},
-             min_resets=2 * 65536)
-
-
-def test_c3_8192_fstep_one_round():
-    """The N=8 shard through k_fstep's one-round shape (eight tick waves, one unit each, the RNG window
-    loaded early, the unit's resets after its tick), TimeLimit 15."""
-    run_full(lambda n: c3(n, max_steps=15), 8192, 40, seed0=6 * 8192, launch={"fstep": 1, "fs_tick": 8},
-             min_resets=2 * 8192, after=_fstep)
-
-
-def test_c5_8192_fstep_one_round():
-    """C5's shard (int16, 4 agents) through the one-round shape, TimeLimit 12."""
-    run_full(lambda n: c5(n, max_steps=12), 8192, 30, seed0=5 * 8192, launch={"fstep": 1, "fs_tick": 8},
-             min_resets=2 * 8192, after=_fstep)

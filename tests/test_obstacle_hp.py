@@ -57,10 +57,10 @@ def _poke_all(eng, pokes):
 
 
 # observation kernels: the engine's pick for the size (int16: k_obs_ring, int32: k_obs_patch), the
-# store streams forced at 64 envs (int64 too: k_obs_patch, k_obs_ring), and k_obs_lds's select chain
+# store streams forced at 64 envs (int64 too: k_obs_patch, k_obs_ring), and k_obs_pipe's per-cell stores
 OBS_PATHS = {"default": {}, "patch": {"obs_lds": 1, "obs_ring": -1},
              "ring": {"obs_lds": 1, "obs_ring": 1},
-             "lds_select": {"obs_lds": 1, "obs_patch": -1, "obs_ring": -1}}
+             "pipe_cells": {"obs_lds": -1}}
 
 
 @pytest.mark.gpu
@@ -222,7 +222,7 @@ def test_raise_kind_only_in_debug_envs():
         eng.close()
 
 
-BIG_ENCODERS = {"k_obs_pbring": {}, "k_obs_bring": {"obs_ring_patch": -1}, "k_obs_gather": {"obs_ring": -1}}
+BIG_ENCODERS = {"k_obs_pbring": {}, "k_obs_gather": {"obs_ring": -1}}
 
 
 @pytest.mark.gpu
@@ -233,7 +233,7 @@ def test_big_map_encoders_on_poked_states(dtype, kernel):
     prefetch of the store-stream kernels) against the oracle's encoder (gym/observation.py:57-173) on poked
     states: dead bodies in every dead-body chunk (clean chunks read the shared zero row), damaged and
     cleaned-up obstacles in several HP chunks (clean chunks read hp_init), lives below the int16 range.
-    1536 envs: k_obs_bring's 256 workgroups walk six envs each, so its four ring slots are reused."""
+    1536 envs: k_obs_pbring's 256 workgroups walk six envs each, so its ring slots are reused."""
     from libzombsole_amd.engine import Engine
     from oracle.oracle import OracleEnv
     n = 1536
@@ -282,17 +282,20 @@ def test_big_map_encoders_on_poked_states(dtype, kernel):
     eng.close()
 
 
-ENCODERS = {"k_obs_patch": {"obs_lds": 1, "obs_ring": -1, "obs_patch": 1},
-            "k_obs_lds": {"obs_lds": 1, "obs_ring": -1, "obs_patch": -1},
-            "k_obs_ring": {"obs_lds": 1, "obs_ring": 1}}
+# name -> (launch overrides, the kernel they select)
+ENCODERS = {"k_obs_patch": ({"obs_lds": 1, "obs_ring": -1, "obs_patch": 1}, "k_obs_patch"),
+            "k_obs_pipe": ({"obs_lds": -1}, "k_obs_pipe"),
+            "k_obs_ring": ({"obs_lds": 1, "obs_ring": 1}, "k_obs_ring"),
+            "k_obs_ring_select": ({"obs_lds": 1, "obs_ring": 1, "obs_ring_patch": -1}, "k_obs_ring")}
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype,kernel", [(_abi.DTYPE_I16, k) for k in sorted(ENCODERS)] +
-                         [(_abi.DTYPE_I64, "k_obs_lds"), (_abi.DTYPE_I64, "k_obs_patch")])
+                         [(_abi.DTYPE_I64, "k_obs_pipe"), (_abi.DTYPE_I64, "k_obs_patch")])
 def test_observation_encoders_on_poked_states(dtype, kernel):
-    """The store-stream observation kernels (the padded-table encoder of k_obs_patch and k_obs_ring,
-    k_obs_lds's per-cell select chain) against the oracle's encoder (gym/observation.py:57-173) on the
+    """The store-stream observation kernels (the padded-table encoder of k_obs_patch and k_obs_ring, the
+    per-cell select chains of k_obs_pipe and of k_obs_ring's fallback encoders) against the oracle's encoder
+    (gym/observation.py:57-173) on the
     same poked states of bridge64 with 4 agents: 40 to 900 dead-body cells per env (more than
     PATCH_DEAD_CAP = 256 cells takes the per-word scan), bodies under map obstacles and under things,
     damaged and cleaned-up obstacles, lives below the int16 range (int16 saturates in both).  (k_obs_ring's
@@ -305,8 +308,8 @@ def test_observation_encoders_on_poked_states(dtype, kernel):
         return _abi.multi_env_config(k, "extermination", [], "bridge64", ["0", "1", "2", "3"], initial_zombies=20,
                                      obs_dtype=dtype)
 
-    eng = Engine(cfg(n).set_launch(ENCODERS[kernel]))
-    assert eng.describe()["obs_kernel"] == kernel
+    eng = Engine(cfg(n).set_launch(ENCODERS[kernel][0]))
+    assert eng.describe()["obs_kernel"] == ENCODERS[kernel][1]
     eng.seed([900 + i for i in range(n)])
     eng.reset()
     rng = np.random.default_rng(11)
