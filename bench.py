@@ -25,7 +25,9 @@ import os
 import sys
 import time
 
-import libzombsole_amd  # noqa: F401  (HIP runtime settings, before the first HIP call)
+import libzombsole_amd  # noqa: E402
+
+libzombsole_amd.plain_graph_dispatch()  # HIP's plain dispatch for the step graphs, before the first HIP call
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)

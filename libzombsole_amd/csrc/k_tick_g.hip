@@ -13,6 +13,7 @@
 // autoreset, World rebuilt as in game.py:151-169), the others tick every other env (zs_tick.hpp).
 // An env is either pending (reset work only; the tick reports it as reset without touching its
 // state) or stepping (tick only), so the two roles never share an env.
+// Dev is the first argument: tick_wg / reset_env_wave reload it from kernarg offset 0 (zs_launder_dev)
 template <int G>
 __global__ void __launch_bounds__(64, ZS_FUSED_WAVES) k_step(Dev d, int n_reset, const int32_t* actions, double* rew,
                                              uint8_t* done_out, uint8_t* trunc_out, uint8_t* listed_out,

@@ -195,12 +195,19 @@ struct Dev {
 
 // the launch's Dev (its first kernel argument, at kernarg offset 0) through a pointer the compiler cannot
 // see through, so the fields read after it are loaded where they are used instead of held in SGPRs across
-// the whole kernel (tick_wg, reset_env_wave, k_obs_ring's encoders).  Only for kernels whose first argument
-// is the Dev.
-__device__ __forceinline__ const Dev* zs_launder_dev() {
+// the whole kernel (tick_wg, reset_env_wave, respawn_env_wave, k_obs_ring's encoders).
+// Contract: only for kernels whose FIRST argument is the Dev, unmodified (k_tick, k_step, k_reset, k_respawn,
+// k_obs_ring); d0 is that argument.  -DZS_CHECK_LAUNDER builds (host-compiled check, never the product)
+// compare the reloaded pointer's fields with d0 and trap on a mismatch.
+__device__ __forceinline__ const Dev* zs_launder_dev(const Dev& d0) {
     typedef const __attribute__((address_space(4))) Dev CDev;
     CDev* dp = (CDev*)__builtin_amdgcn_kernarg_segment_ptr();
     asm volatile("" : "+s"(dp));
+#ifdef ZS_CHECK_LAUNDER
+    if (dp->N != d0.N || dp->E != d0.E || dp->pos != d0.pos || dp->ring != d0.ring) __builtin_trap();
+#else
+    (void)d0;
+#endif
     return (const Dev*)dp;
 }
 

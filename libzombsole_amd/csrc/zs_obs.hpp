@@ -1254,6 +1254,7 @@ __host__ __device__ constexpr int ring_patch_lds_bytes(int static_bytes, int enc
 #ifndef ZS_RING_LAUNDER
 #define ZS_RING_LAUNDER 1
 #endif
+// Dev is the first argument (zs_launder_dev's contract: the encoders reload it from kernarg offset 0)
 template <typename T, int NOBS, bool PATCHED = false>
 __global__ void __launch_bounds__(64 * (RING_ENC + RING_WRT), 1) k_obs_ring(Dev d, T* out, ObsLayout L, int env0, int env1) {
     const Dev& d0 = d;
@@ -1319,7 +1320,7 @@ __global__ void __launch_bounds__(64 * (RING_ENC + RING_WRT), 1) k_obs_ring(Dev 
     // dq reloaded for the item two iterations after that
     auto encode = [&](int t, ObsPrefetch& f, zs_v2u& dq, int ahead) {
         // the Dev fields reloaded per item (ZS_RING_LAUNDER), not held in SGPRs across the wave's items
-        const Dev& d = ZS_RING_LAUNDER ? *zs_launder_dev() : d0;
+        const Dev& d = ZS_RING_LAUNDER ? *zs_launder_dev(d0) : d0;
         const int u = t / PAIR, h = t % PAIR, e = item_env(t);
         if (PATCHED) pe.build(d, f);
         else obs_build_compact(d, L, img, f, code_s, lane);

@@ -108,12 +108,12 @@ __device__ __forceinline__ uint32_t wave_rng_finish(WaveRng& r) {
 #define ZS_RESET_LAUNDER 1
 #endif
 #if ZS_RESET_LAUNDER
-#define ZS_RST_RELOAD() dp = zs_launder_dev()
+#define ZS_RST_RELOAD() dp = zs_launder_dev(d0)
 #else
 #define ZS_RST_RELOAD() (void)0
 #endif
 __device__ __forceinline__ void reset_env_wave(const Dev& d0, const ResetLds& L, int e, int list_mode, int* err_out) {
-    const Dev* dp = ZS_RESET_LAUNDER ? zs_launder_dev() : &d0;
+    const Dev* dp = ZS_RESET_LAUNDER ? zs_launder_dev(d0) : &d0;
     const int lane = threadIdx.x & 63, N = dp->N, E = dp->E, A = dp->A, P = dp->P;
     RST_DECL
     RST(0);
@@ -339,6 +339,7 @@ __device__ __forceinline__ void reset_role(const Dev& d, int list_mode, const in
 
 // the non-template kernels are compiled in k_reset.hip only
 #ifdef ZS_DEFINE_RESET_KERNELS
+// Dev is the first argument (zs_launder_dev's contract: reset_env_wave reloads it from kernarg offset 0)
 __global__ void __launch_bounds__(64, ZS_RESET_WAVES) k_reset(Dev d, int list_mode, const int* list, const int* count,
                                               const uint8_t* mask, int* err_out, void* obs_out) {
     reset_role(d, list_mode, list, count, mask, err_out, blockIdx.x, gridDim.x, obs_out);
@@ -353,7 +354,7 @@ __global__ void __launch_bounds__(64, ZS_RESET_WAVES) k_reset(Dev d, int list_mo
 // (core.py:40-66) as wave work (wave_spawn), new zombies appended to the dict order.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void respawn_env_wave(const Dev& d0, const ResetLds& L, int e) {
-    const Dev* dp = ZS_RESET_LAUNDER ? zs_launder_dev() : &d0;
+    const Dev* dp = ZS_RESET_LAUNDER ? zs_launder_dev(d0) : &d0;
     const int lane = threadIdx.x & 63, N = dp->N, E = dp->E, Z0 = dp->A + dp->P;
     RST_DECL
     RST(0);
@@ -480,6 +481,7 @@ __device__ __forceinline__ void respawn_env_wave(const Dev& d0, const ResetLds& 
 #ifndef ZS_RESPAWN_WAVES
 #define ZS_RESPAWN_WAVES 3
 #endif
+// Dev is the first argument (zs_launder_dev's contract: respawn_env_wave reloads it from kernarg offset 0)
 __global__ void __launch_bounds__(64, ZS_RESPAWN_WAVES) k_respawn(Dev d) {
     extern __shared__ __align__(16) uint8_t smem[];
     const int cnt = *d.resp_count, e0 = d.resp_list[blockIdx.x];  // one round trip (grid <= N)

@@ -1478,9 +1478,9 @@ __device__ __forceinline__ void tick_wg(const Dev& d0, int wg, const int32_t* ac
     // The Dev fields are read through a pointer re-derived from the kernarg segment at each phase (ZS_TICK_LAUNDER):
     // read through the kernel's by-value argument, the compiler loads them all up front and keeps them in SGPRs
     // for the whole tick (458 SGPR spills into VGPR lanes at G = 8, each use a v_readlane).
-    const Dev* dp = ZS_TICK_LAUNDER ? zs_launder_dev() : &d0;
+    const Dev* dp = ZS_TICK_LAUNDER ? zs_launder_dev(d0) : &d0;
 #if ZS_TICK_LAUNDER
-#define ZS_RELOAD_DEV() dp = zs_launder_dev()
+#define ZS_RELOAD_DEV() dp = zs_launder_dev(d0)
 #else
 #define ZS_RELOAD_DEV() (void)0
 #endif
@@ -1905,6 +1905,7 @@ __device__ __forceinline__ void tick_wg(const Dev& d0, int wg, const int32_t* ac
 #undef ZS_RELOAD_DEV
 }
 
+// Dev is the first argument: tick_wg reloads it from kernarg offset 0 (zs_launder_dev's contract)
 template <int G, int W = ZS_STEP_WAVES, bool EARLY = false>
 __global__ void __launch_bounds__(64, W) k_tick(Dev d, const int32_t* actions, double* rew, uint8_t* done_out,
                                              uint8_t* trunc_out, uint8_t* listed_out, uint8_t* reset_out,

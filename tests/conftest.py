@@ -8,7 +8,9 @@ for p in (ROOT, os.path.join(ROOT, "tests")):
     if p not in sys.path:
         sys.path.insert(0, p)
 
-import libzombsole_amd  # noqa: E402,F401  (its HIP runtime settings, before any test's first HIP call)
+import libzombsole_amd  # noqa: E402
+
+libzombsole_amd.plain_graph_dispatch()  # the graph dispatch the bench times, before any test's first HIP call
 
 
 def pytest_configure(config):

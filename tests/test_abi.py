@@ -51,3 +51,12 @@ def test_struct_layout_matches_header(tmp_path):
         assert got["%s sizeof" % name] == ctypes.sizeof(cls), name
         for f in cls._fields_:
             assert got["%s %s" % (name, f[0])] == getattr(cls, f[0]).offset, (name, f[0])
+
+
+def test_checked_launder_build_compiles(tmp_path):
+    """The kernels that reload their Dev from kernarg offset 0 (zs_launder_dev: k_reset, k_respawn here) build
+    with the contract check on (-DZS_CHECK_LAUNDER: the reloaded fields against the kernel's argument)."""
+    import subprocess
+    import __graft_entry__ as ge
+    subprocess.check_call([ge._hipcc()] + ge.HIPCC_FLAGS + ["-DZS_CHECK_LAUNDER", "-c", "-o", str(tmp_path / "k_reset.o"),
+                                                         os.path.join(ge.CSRC, "k_reset.hip")])

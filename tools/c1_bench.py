@@ -27,7 +27,9 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-import libzombsole_amd  # noqa: E402,F401
+import libzombsole_amd  # noqa: E402
+
+libzombsole_amd.plain_graph_dispatch()
 from libzombsole_amd import actions as A  # noqa: E402
 
 REFERENCE = {"multi": 973.0, "single": 1012.0}  # BASELINE.md §2, env-steps/s on one core
