@@ -1324,7 +1324,9 @@ __global__ void __launch_bounds__(64 * (RING_ENC + RING_WRT), 1) k_obs_ring(Dev 
         const int u = t / PAIR, h = t % PAIR, e = item_env(t);
         if (PATCHED) pe.build(d, f);
         else obs_build_compact(d, L, img, f, code_s, lane);
-        const int tn = t + ahead * RING_ENC, tq = t + (ahead + 2) * RING_ENC;
+        // this item's prefetch set next serves item t + ahead * RING_ENC, whose loads need the dirty masks of
+        // the item after that (t + 2 * ahead * RING_ENC)
+        const int tn = t + ahead * RING_ENC, tq = t + 2 * ahead * RING_ENC;
         if (ahead == 1) {
             if (tn < count) obs_prefetch(d, item_env(tn), tn + RING_ENC < count ? item_env(tn + RING_ENC) : item_env(tn), f.dirty_ahead, f);
         } else {
@@ -1365,6 +1367,21 @@ __global__ void __launch_bounds__(64 * (RING_ENC + RING_WRT), 1) k_obs_ring(Dev 
     for (; t < count; t += 2 * RING_ENC) {
         encode(t, fa, qa, 2);
         if (t + RING_ENC < count) encode(t + RING_ENC, fb, qb, 2);
+    }
+#elif ZS_RING_PF == 3
+    // three items of register prefetch
+    ObsPrefetch fa, fb, fc;
+    zs_v2u qa, qb, qc;
+    obs_prefetch_env(d, envc(t), OBS_OWN_ROWS, fa);
+    obs_prefetch_env(d, envc(t + RING_ENC), obs_dirty(d, envc(t + RING_ENC)), fb);
+    obs_prefetch_env(d, envc(t + 2 * RING_ENC), obs_dirty(d, envc(t + 2 * RING_ENC)), fc);
+    qa = obs_dirty(d, envc(t + 3 * RING_ENC));
+    qb = obs_dirty(d, envc(t + 4 * RING_ENC));
+    qc = obs_dirty(d, envc(t + 5 * RING_ENC));
+    for (; t < count; t += 3 * RING_ENC) {
+        encode(t, fa, qa, 3);
+        if (t + RING_ENC < count) encode(t + RING_ENC, fb, qb, 3);
+        if (t + 2 * RING_ENC < count) encode(t + 2 * RING_ENC, fc, qc, 3);
     }
 #else
     ObsPrefetch f;
