@@ -1364,19 +1364,13 @@ __device__ __forceinline__ void env_step_leader_b(const Dev& d, Grp& c, double* 
         if (listed_out)
             for (int a = 0; a < A; a++) listed_out[(size_t)c.e * A + a] = (uint8_t)MISC(c, MISC_N + A + a);
     } else {
-        for (int a = 0; a < A; a++) {
-            uint8_t was = (uint8_t)MISC(c, MISC_N + A + a);
-            if (listed_out) listed_out[(size_t)c.e * A + a] = was;
-            const double prev = (double)c.prevzd + (double)MISC(c, MISC_N + a) / 100.0;
-            const double cur = (double)c.zd + (double)LL(c, a) / 100.0;
-            double r = cur - prev;
-            if (!was) r = 0.0;
-            else if (LL(c, a) > 0) r = r + end_reward;
-            rew[(size_t)c.e * A + a] = r;
-            MISC(c, MISC_N + A + a) = LL(c, a) > 0;
-        }
+        // the per-agent deltas are formed by the agents' lanes after the leader's part (multi_rewards): the
+        // leader leaves the end reward and the reward tracker's old zombie-death count in the scratch rows
+        MISC(c, MISC_NMOVED) = ended ? (won ? 1 : 2) : (end_reward != 0.0 ? 2 : 0);
+        MISC(c, MISC_NORD) = c.prevzd;
     }
-    for (int a = 0; a < A; a++) MISC(c, MISC_N + a) = LL(c, a);
+    if (d.reward_mode == ZS_REWARD_SINGLE)
+        for (int a = 0; a < A; a++) MISC(c, MISC_N + a) = LL(c, a);
     c.prevzd = c.zd;
     c.epsteps++;
     if (d.max_steps > 0 && c.epsteps >= d.max_steps) tr = 1;
@@ -1384,6 +1378,29 @@ __device__ __forceinline__ void env_step_leader_b(const Dev& d, Grp& c, double* 
     trunc_out[c.e] = (uint8_t)tr;
     c.fin = ended || tr;
     SUB(4);
+}
+
+// MultiAgentRewards.update and the end-of-game rewards (gym/reward.py:77-98, gym/multiagent_env.py:143-162)
+// for the agents of a stepping env, one agent per lane of the env's group (agent a on lane a mod G), after
+// env_step_leader_b left the end reward (MISC_NMOVED: 0 none, 1 +10, 2 -10) and the tracker's previous
+// zombie-death count (MISC_NORD); the same float64 operations in the same order as the reference.  Also
+// env.agents for the next step (alive after this one) and the tracker's lives.
+__device__ __forceinline__ void multi_rewards(const Dev& d, const Grp& c, double* rew, uint8_t* listed_out) {
+    const int A = d.A, code = MISC(c, MISC_NMOVED), prevzd = MISC(c, MISC_NORD), zd = MISC(c, MISC_ZD);
+    const double end_reward = code == 1 ? 10.0 : (code == 2 ? -10.0 : 0.0);
+    for (int a = c.j; a < A; a += 64 / c.ne) {  // G = 64 / ne lanes per env
+        const uint8_t was = (uint8_t)MISC(c, MISC_N + A + a);
+        const int life = LL(c, a);
+        if (listed_out) listed_out[(size_t)c.e * A + a] = was;
+        const double prev = (double)prevzd + (double)MISC(c, MISC_N + a) / 100.0;
+        const double cur = (double)zd + (double)life / 100.0;
+        double r = cur - prev;
+        if (!was) r = 0.0;
+        else if (life > 0) r = r + end_reward;
+        rew[(size_t)c.e * A + a] = r;
+        MISC(c, MISC_N + A + a) = life > 0;
+        MISC(c, MISC_N + a) = life;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1862,6 +1879,9 @@ __device__ __forceinline__ void tick_wg(const Dev& d0, int wg, const int32_t* ac
         dp->rngst[e] = stf;
         lst[g] = stf;
     }
+    wave_sync();
+    // the multi-agent rewards by the agents' lanes (env_step_leader_b ran: the scratch row is its end-reward code)
+    if (stepping && dp->reward_mode == ZS_REWARD_MULTI && MISC(c, MISC_NMOVED) >= 0) multi_rewards(*dp, c, rew, listed_out);
     wave_sync();
     STAMP(4);
     ZS_RELOAD_DEV();
