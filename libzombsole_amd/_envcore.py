@@ -96,13 +96,25 @@ class EnvCore(object):
         try:
             eng.host_reset(self._rng_in(), rec)
         except Exception as err:
-            if type(err) is Exception:  # ZS_ENOSPACE (core.py:62-64): the draws were taken, as in the reference
-                random.setstate(HostRecord(eng, rec[0], self._lay, self._np_obs).rng_state())
-            raise
+            if type(err) is not Exception:
+                raise
+            # ZS_ENOSPACE: the draws were taken, as in the reference, which raises naming the first thing it
+            # could not place (core.py:58-64): players spawn first, then agents, on the same spawn cells
+            random.setstate(HostRecord(eng, rec[0], self._lay, self._np_obs).rng_state())
+            raise Exception("Not enough space to spawn %s" % self._unplaced()) from None
         r = self._record(rec)
         random.setstate(r.rng_state())
         self.game.new_episode(r.state_buf)
         return r
+
+    def _unplaced(self):
+        """The name of the first thing a reset cannot place (game.py:181-187, core.py:40-66): every spawn cell
+        is free at a reset (the map's obstacles stand on other cells; with no spawn cells listed, every cell
+        but an obstacle's), the players take them first, then the agents."""
+        m = self.game.map
+        free = len(m.player_spawns) if m.player_spawns else m.size[0] * m.size[1] - len(m.obstacles)
+        names = self.game.player_names
+        return names[free] if free < len(names) else "agent"
 
     def encode(self, action):
         """Agent.next_step's parse of one action dict: an engine triple, or the ActionError the reference's

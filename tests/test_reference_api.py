@@ -4,10 +4,14 @@ tests/test_multiagent_env.py of jvstinian/libzombsole), run against the drop-in 
 gymnasium is not installed in this image: `gym.make` is the local registry's make (same
 ids, kwargs and TimeLimit 1000) and `check_env` is replaced by the API checks it makes
 (spaces contain what reset/step return, the 5-tuple shape, reset after done)."""
+import json
+import os
 import random
 
 import numpy as np
 import pytest
+
+import golden_util as G
 
 from libzombsole_amd.gym.multiagent_env import MultiagentZombsoleEnv, MultiagentZombsoleEnvDiscreteAction
 from libzombsole_amd.gym_env import ZombsoleGymEnv, ZombsoleGymEnvDiscreteAction, make
@@ -280,3 +284,26 @@ def test_objects_held_across_reset_keep_their_values():
     new_things = list(env.game.world.things.values())
     assert all(all(v is not n for n in new_things) for v in old_zombies + old_agents)
     assert wall is env.game.map.things[0]
+
+
+SPAWN_FAILURES = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "spawn_failure.json")))
+
+
+@pytest.mark.parametrize("case", SPAWN_FAILURES, ids=lambda c: "%s-%d" % (c["case"], c["seed"]))
+def test_spawn_failure_message_and_stream(case):
+    """A world that cannot place every player / agent (game.py:151-187, core.py:40-66): the constructor raises
+    the reference's bare Exception naming the first thing it could not place, and the process-global `random`
+    stream has taken the spawn shuffles' draws (tests/golden/spawn_failure.json, recorded from the reference:
+    tests/golden/make_spawnfail_golden.py)."""
+    import hashlib
+    import random
+    import struct
+
+    from libzombsole_amd.gym.multiagent_env import MultiagentZombsoleEnv
+    from libzombsole_amd.gym_env import ZombsoleGymEnv
+    kw = dict(case["kwargs"], map_name=G.map_path("wall_hp"))
+    random.seed(case["seed"])
+    with pytest.raises(Exception) as ei:
+        (ZombsoleGymEnv if case["surface"] == "single" else MultiagentZombsoleEnv)(**kw)
+    assert type(ei.value) is Exception and str(ei.value) == case["message"]
+    assert hashlib.sha256(struct.pack("<625I", *random.getstate()[1])).hexdigest() == case["rng_sha"]
