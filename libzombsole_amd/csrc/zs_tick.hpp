@@ -1502,6 +1502,11 @@ __device__ __forceinline__ void tick_wg(const Dev& d0, int wg, const int32_t* ac
 #define ZS_RELOAD_DEV() (void)0
 #endif
     constexpr int NE = 64 / G;
+#ifndef ZS_DIAG_STOP
+#define ZS_DIAG_STOP 0  // diagnostic builds only: end the tick after phase k (1 stage-in ... 5 MT refill)
+#endif
+#define ZS_STOP_AFTER(k) \
+    if (ZS_DIAG_STOP == (k)) return
     const int lane = threadIdx.x & 63, g = lane / G, j = lane - g * G;
     const int base = env0 + wg * NE, e = base + g, N = dp->N, E = dp->E, A = dp->A;
     const bool active = e < env1;
@@ -1718,6 +1723,7 @@ __device__ __forceinline__ void tick_wg(const Dev& d0, int wg, const int32_t* ac
     wave_sync();
     STAMP(1);
     ZS_RELOAD_DEV();
+    ZS_STOP_AFTER(1);
     if (stepping) {
         // decisions (start-of-tick state), then the action list of get_actions (core.py:80-101) compacted from
         // them in dict order, when no decision was deferred to the leader (RNG-drawing) or raises:
@@ -1790,6 +1796,7 @@ __device__ __forceinline__ void tick_wg(const Dev& d0, int wg, const int32_t* ac
     wave_sync();
     STAMP(2);
     ZS_RELOAD_DEV();
+    ZS_STOP_AFTER(2);
     if (active && leader && !stepping) {  // this call is the env's reset; outputs as after env.reset()
         int nr = dp->reward_mode == ZS_REWARD_SINGLE ? 1 : A;
         for (int a = 0; a < nr; a++) rew[(size_t)e * nr + a] = 0.0;
@@ -1832,6 +1839,7 @@ __device__ __forceinline__ void tick_wg(const Dev& d0, int wg, const int32_t* ac
     wave_sync();
     STAMP(3);
     ZS_RELOAD_DEV();
+    ZS_STOP_AFTER(3);
     if (leader && stepping) {
         c.n_order = n_order;
         c.t = MISC(c, MISC_T) + 1;
@@ -1885,10 +1893,12 @@ __device__ __forceinline__ void tick_wg(const Dev& d0, int wg, const int32_t* ac
     wave_sync();
     STAMP(4);
     ZS_RELOAD_DEV();
+    ZS_STOP_AFTER(4);
     // the MT refill first: its loads do not wait behind the stage-out's stores (one vmcnt for both)
     coop_refill(*dp, base, min(NE, env1 - base), lst, (lu32*)(smem + L.off_bm));
     STAMP(5);
     ZS_RELOAD_DEV();
+    ZS_STOP_AFTER(5);
     if (stepping) {
         for (int s = j; s < E; s += G) {
             dp->pos[EIX(*dp, s, e)] = LP(c, s);
@@ -1923,6 +1933,7 @@ __device__ __forceinline__ void tick_wg(const Dev& d0, int wg, const int32_t* ac
     }
     STAMP(7);
 #undef ZS_RELOAD_DEV
+#undef ZS_STOP_AFTER
 }
 
 // Dev is the first argument: tick_wg reloads it from kernarg offset 0 (zs_launder_dev's contract)
