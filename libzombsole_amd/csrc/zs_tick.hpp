@@ -859,32 +859,27 @@ __device__ __forceinline__ void grp_shuffle(const Dev& d, Grp& c, int n, int& po
     grp_draws<G>(d, c, pos, n - 1, [&](int t) { return n - t; }, [&](int t, uint32_t v) { jt8[t] = (uint8_t)v; });
     wave_sync();
     GX(1);
-    // lane j follows the elements at positions j and j + G through the swaps (i = n - 1 - t, j_t), the
-    // draws read 16 at a time
-    int fin[2] = {-1, -1}, el[2] = {0, 0};
+    // the swaps (i = n - 1 - t with j_t), in order, by the env's leader lane on the LDS list.  The tick is
+    // VALU-bound where it matters (C3-C5: every instruction issues for the whole wave), and this chain is
+    // ~5 instructions a swap against ~16 for every lane following two elements through all the swaps (C5:
+    // the shuffle 803 VALU instructions per wave of 4 envs, profiles/r06v_pmc_stop.log); its LDS round trips
+    // run under the other waves' issue.
+    if (c.j == 0) {
+        const lu32* jw = (const lu32*)jt8;
+        for (int t0 = 0; t0 < n - 1; t0 += 4) {
+            const uint32_t q = jw[t0 >> 2];
 #pragma unroll
-    for (int h = 0; h < 2; h++) {
-        const int k = c.j + h * G;
-        if (k < n) {
-            el[h] = LPE(c, k);
-            fin[h] = k;
+            for (int b = 0; b < 4; b++) {
+                const int t = t0 + b;
+                if (t < n - 1) {
+                    const int i = n - 1 - t, jt = (int)((q >> (8 * b)) & 0xffu);
+                    const uint8_t x = LPE(c, i), y = LPE(c, jt);
+                    LPE(c, i) = y;
+                    LPE(c, jt) = x;
+                }
+            }
         }
     }
-    const lv4u* jv = (const lv4u*)jt8;
-    for (int t0 = 0; t0 < n - 1; t0 += 16) {
-        const zs_v4u q = jv[t0 >> 4];
-#pragma unroll
-        for (int b = 0; b < 16; b++) {
-            const int t = t0 + b, i = n - 1 - t, jt = (int)((q[b >> 2] >> (8 * (b & 3))) & 0xffu);
-            const bool live = t < n - 1;
-#pragma unroll
-            for (int h = 0; h < 2; h++) fin[h] = !live ? fin[h] : fin[h] == i ? jt : (fin[h] == jt ? i : fin[h]);
-        }
-    }
-    wave_sync();
-#pragma unroll
-    for (int h = 0; h < 2; h++)
-        if (fin[h] >= 0) LPE(c, fin[h]) = (uint8_t)el[h];
     wave_sync();
     GX(2);
 }
@@ -893,6 +888,9 @@ __device__ __forceinline__ void grp_shuffle(const Dev& d, Grp& c, int n, int& po
 // odirty is set when an obstacle was hit.  The lanes
 // exchange their actions through the env's two tables (t0, t1: one word per lane), read back four
 // words at a time.
+#ifndef ZS_DIAG_STOP
+#define ZS_DIAG_STOP 0  // diagnostic builds only (tick_wg): 7-10 end each chunk of grp_execute early
+#endif
 template <int G>
 __device__ __forceinline__ void grp_execute(const Dev& d, Grp& c, int n, int& pos, int& nmoved, int& odirty) {
     const int j = c.j;
@@ -951,6 +949,7 @@ __device__ __forceinline__ void grp_execute(const Dev& d, Grp& c, int n, int& po
         }
         wave_sync();
         GX(3);
+        if (ZS_DIAG_STOP == 7) continue;
         // earlier valid moves of the chunk that leave (vac) or enter (dep) this move's cell
         unsigned long long dep = 0ull, vac = 0ull;
         constexpr int UNR = G <= 16 ? G / 4 : 2;  // whole scans up to 16 lanes; wider groups by halves of 8
@@ -974,6 +973,7 @@ __device__ __forceinline__ void grp_execute(const Dev& d, Grp& c, int n, int& po
             }
         }
         GX(4);
+        if (ZS_DIAG_STOP == 8) continue;
         bool res = !mv || dep == 0ull;
         bool suc = mv && dep == 0ull && !occ0;
         unsigned long long R = gballot<G>(c, res), S = gballot<G>(c, suc);
@@ -1003,6 +1003,7 @@ __device__ __forceinline__ void grp_execute(const Dev& d, Grp& c, int n, int& po
             }
         }
         GX(5);
+        if (ZS_DIAG_STOP == 9) continue;
         const unsigned long long IR = gballot<G>(c, inr);
         const int r = __popcll(IR & below);
         wave_sync();  // the scans' table reads before the bounds overwrite t1
@@ -1011,6 +1012,7 @@ __device__ __forceinline__ void grp_execute(const Dev& d, Grp& c, int n, int& po
         grp_draws<G>(d, c, pos, __popcll(IR), [&](int t) { return (int)t1[t]; }, [&](int t, uint32_t v) { t1[t] = (int)v; });
         wave_sync();
         GX(6);
+        if (ZS_DIAG_STOP == 10) continue;
         // every hit on a target in execution order; the last hitter stores the result
         const int hv = inr ? (kind == K_ATTACK ? -(lo + t1[r]) : lo + t1[r]) : 0;
         wave_sync();
@@ -1503,7 +1505,7 @@ __device__ __forceinline__ void tick_wg(const Dev& d0, int wg, const int32_t* ac
 #endif
     constexpr int NE = 64 / G;
 #ifndef ZS_DIAG_STOP
-#define ZS_DIAG_STOP 0  // diagnostic builds only: end the tick after phase k (1 stage-in ... 5 MT refill)
+#define ZS_DIAG_STOP 0  // diagnostic builds only: end the tick after phase k (1 stage-in ... 5 MT refill; 6-10 inside the execution)
 #endif
 #define ZS_STOP_AFTER(k) \
     if (ZS_DIAG_STOP == (k)) return
@@ -1820,7 +1822,7 @@ __device__ __forceinline__ void tick_wg(const Dev& d0, int wg, const int32_t* ac
         if (nact >= 0 && nact <= 2 * G) {
             int pos = 0, odirty = 0;
             grp_shuffle<G>(*dp, c, nact, pos);
-            grp_execute<G>(*dp, c, nact, pos, nm0, odirty);
+            if (ZS_DIAG_STOP != 6) grp_execute<G>(*dp, c, nact, pos, nm0, odirty);
             if (dp->alog) {  // the executed actions in execution order (drop-in views)
                 int32_t* al = dp->alog + (size_t)e * dp->E * 2;
                 for (int k = j; k < nact; k += G) {
@@ -1840,6 +1842,7 @@ __device__ __forceinline__ void tick_wg(const Dev& d0, int wg, const int32_t* ac
     STAMP(3);
     ZS_RELOAD_DEV();
     ZS_STOP_AFTER(3);
+    if (ZS_DIAG_STOP >= 6) return;  // the execution's own stop points (6: the shuffle only, 7-10 in grp_execute)
     if (leader && stepping) {
         c.n_order = n_order;
         c.t = MISC(c, MISC_T) + 1;
