@@ -824,7 +824,11 @@ __device__ __forceinline__ void grp_reload(const Dev& d, Grp& c, int& pos) {
 template <int G, class Bound, class Put>
 __device__ __forceinline__ void grp_draws(const Dev& d, Grp& c, int& pos, int count, Bound bound, Put put) {
     const int j = c.j;
-    const unsigned long long below = (1ull << j) - 1ull;
+    // the wave's own ballots with per-lane masks of the group (gm) and of its lanes below this one: the fixed
+    // point's loop test compares whole-wave masks (scalar), with no per-lane shift of every ballot; a group at
+    // its fixed point is unchanged by the iterations the other groups still need
+    const unsigned long long gm = G == 64 ? ~0ull : ((1ull << G) - 1ull) << (c.g * G);
+    const unsigned long long below = gm & ((1ull << (c.g * G + j)) - 1ull);
     int done = 0;
     while (done < count) {
         if (pos >= c.wlen) grp_reload<G>(d, c, pos);
@@ -839,12 +843,12 @@ __device__ __forceinline__ void grp_draws(const Dev& d, Grp& c, int& pos, int co
             lv = avail && t < count;
             b = lv ? bound(t) : 1;
             rj = lv && (w >> (__clz(b))) >= (uint32_t)b;  // getrandbits(bit_length(b)) = w >> (32 - bit_length(b))
-            rej = gballot<G>(c, rj);
+            rej = __ballot(rj);
         } while (rej != prev);
-        const unsigned long long live = gballot<G>(c, lv);
+        const unsigned long long live = __ballot(lv) & gm;
         if (lv && !rj) put(t, w >> __clz(b));
-        done += __popcll(live) - __popcll(rej);
-        pos += 64 - __clzll((long long)live);
+        done += __popcll(live) - __popcll(rej & gm);
+        pos += 64 - __clzll((long long)live) - c.g * G;
     }
 }
 
@@ -1023,6 +1027,23 @@ __device__ __forceinline__ void grp_execute(const Dev& d, Grp& c, int n, int& po
         if (inr) life = tgt >= 0 ? LL(c, tgt) : ohp;
         bool last = inr;
         uint32_t ovf = 0u;  // an obstacle's life after one of the hits left the int16 / int32 range
+        const bool ohit = __ballot(inr && tgt < 0) != 0ull;  // some obstacle is hit in the wave's chunks
+        if (!ohit) {
+            // entity targets only (the common chunk): a life stays within a few hundred of 0, so no hit
+            // saturates (the same values as the loop below, fewer instructions)
+#pragma unroll UNR
+            for (int k0 = 0; k0 < mw; k0 += 4) {
+                const zs_v4i tv = t0v[k0 >> 2], hvv = t1v[k0 >> 2];
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const int k = k0 + u, hk = hvv[u];
+                    const bool same = inr && tv[u] == tgt;
+                    const int nl = hk < 0 ? life + hk : min(life + hk, ml);
+                    life = (same && k <= j) ? nl : life;
+                    last = last && !(same && k > j);
+                }
+            }
+        } else {
 #pragma unroll UNR
         for (int k0 = 0; k0 < mw; k0 += 4) {
             const zs_v4i tv = t0v[k0 >> 2], hvv = t1v[k0 >> 2];
@@ -1043,6 +1064,7 @@ __device__ __forceinline__ void grp_execute(const Dev& d, Grp& c, int n, int& po
                 last = last && !(inr && tv[u] == tgt && k > j);
             }
         }
+        }
         if (last) {
             if (tgt >= 0) {
                 LL(c, tgt) = (int)life;
@@ -1057,7 +1079,7 @@ __device__ __forceinline__ void grp_execute(const Dev& d, Grp& c, int n, int& po
                 else atomicAnd(wp, ~(1u << (oi & 31)));
             }
         }
-        if (gballot<G>(c, inr && tgt < 0)) odirty = 1;
+        if (ohit && gballot<G>(c, inr && tgt < 0)) odirty = 1;
         // commit the chunk's moves: cells freed before cells taken (a cell is left at most once and
         // taken at most once per tick, in that order), positions, movers in execution order
         if (suc) bm_clr(c, py * d.W + px);
