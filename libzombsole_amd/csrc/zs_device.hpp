@@ -340,6 +340,14 @@ __device__ __forceinline__ int d2(int x1, int y1, int x2, int y2) {
     return dx * dx + dy * dy;
 }
 
+// d2 of two packed positions (pack_xy) whose coordinate differences fit int16 (two cells of a map): one
+// packed int16 subtract and one int16 dot product
+typedef short zs_v2s __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ int d2p(int32_t a, int32_t b) {
+    const zs_v2s v = __builtin_bit_cast(zs_v2s, a) - __builtin_bit_cast(zs_v2s, b);
+    return __builtin_amdgcn_sdot2(v, v, 0, false);
+}
+
 __device__ __forceinline__ int64_t floordiv100(int64_t a) {  // Python a // 100
     int64_t q = a / 100;
     if ((a % 100) != 0 && a < 0) q -= 1;

@@ -334,6 +334,18 @@ __device__ __forceinline__ void set_target_life(const Dev& d, Grp& c, int tgt, i
 // closest(...) over present slots [s0, s1) \ {excl}: the first minimum in dict order (branch-free body:
 // the slots' LDS reads issue back to back)
 __device__ __forceinline__ int closest_in(const Dev& d, const Grp& c, int fx, int fy, int s0, int s1, int excl) {
+    if ((d.W - 1) * (d.W - 1) + (d.H - 1) * (d.H - 1) < 65536) {
+        // every d^2 of the map fits 16 bits: the minimum of one key (d^2, dict rank, slot) per slot (ranks and
+        // slots < 256), the same first minimum in dict order in half the instructions
+        const int32_t f = pack_xy(fx, fy);
+        uint32_t best = 0xffffffffu;
+#pragma unroll 4
+        for (int s = s0; s < s1; s++) {
+            const uint32_t key = ((uint32_t)d2p(LP(c, s), f) << 16) | ((uint32_t)LR(c, s) << 8) | (uint32_t)s;
+            best = (LPR(c, s) && s != excl) ? min(best, key) : best;
+        }
+        return best == 0xffffffffu ? -1 : (int)(best & 0xffu);
+    }
     int best = -1, bd = 0, br = 0;
 #pragma unroll 4
     for (int s = s0; s < s1; s++) {
