@@ -515,10 +515,13 @@ __device__ __forceinline__ void decide_zombie(const Dev& d, Grp& c, int s, bool 
         for (int k = 0; k < 4; k++) dd[k] = d2(hx, hy, x + c_adj_dx[k], y + c_adj_dy[k]);
 #pragma unroll 4
         for (int t = 0; t < d.E; t++) {
-            const int pt = LP(c, t);
-            const int ddx = unpack_x(pt) - x, ddy = unpack_y(pt) - y;
-            const bool on = LPR(c, t) && ddx * ddx + ddy * ddy == 1;  // an adjacent_positions cell
-            em |= on ? (ddy == 1 ? 1 : ddy == -1 ? 2 : ddx == 1 ? 4 : 8) : 0;
+            // the packed offset v = (dx, dy) of thing t: on an adjacent_positions cell when dx^2 + dy^2 == 1;
+            // which one from v's bits: (0,1) 0x00010000, (0,-1) 0xffff0000, (1,0) 0x1, (-1,0) 0xffff give
+            // (v >> 15 & 3) + (v >> 31) = 2, 3, 0, 1, and ^ 2 the neighbour order 0..3
+            const zs_v2s v = __builtin_bit_cast(zs_v2s, LP(c, t)) - __builtin_bit_cast(zs_v2s, p);
+            const uint32_t w = __builtin_bit_cast(uint32_t, v);
+            const bool on = LPR(c, t) && __builtin_amdgcn_sdot2(v, v, 0, false) == 1;
+            em |= on ? 1 << ((((w >> 15) & 3u) + (w >> 31)) ^ 2u) : 0;
         }
         int used = 0;
         for (int r = 0; r < 4; r++) {
