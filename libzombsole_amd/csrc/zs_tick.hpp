@@ -951,8 +951,8 @@ __device__ __forceinline__ void grp_execute(const Dev& d, Grp& c, int n, int& po
             mv = in_bounds(d, tx, ty) && d2(px, py, tx, ty) <= 1;
             dcell = ty * d.W + tx;
         }
-        t0[j] = mv ? tgt : -1;  // valid moves' destinations (packed, >= 0) and sources
-        t1[j] = p;
+        t0[j] = mv ? tgt : -1;  // valid moves' destinations (packed, >= 0) and sources (-2: not a valid move)
+        t1[j] = mv ? p : -2;
         if (act) LR(c, s) = (uint8_t)j;  // the chunk position of each actor (dict ranks are dead by now)
         const bool occ0 = mv && bm_test(c, dcell);
         const bool hits = kind == K_ATTACK || kind == K_HEAL;
@@ -969,19 +969,28 @@ __device__ __forceinline__ void grp_execute(const Dev& d, Grp& c, int n, int& po
         wave_sync();
         GX(3);
         if (ZS_DIAG_STOP == 7) continue;
-        // earlier valid moves of the chunk that leave (vac) or enter (dep) this move's cell
-        unsigned long long dep = 0ull, vac = 0ull;
+        // earlier valid moves of the chunk that leave (vac) or enter (dep) this move's cell.  A lane without a
+        // valid move wrote no cell (-1 / -2 match no destination), so the scan compares cells alone, four
+        // entries to a nibble, and the earlier-lanes and valid-move conditions apply once, to the masks
+        typedef typename std::conditional<G <= 32, uint32_t, unsigned long long>::type MaskT;
+        MaskT depm = 0, vacm = 0;
         constexpr int UNR = G <= 16 ? G / 4 : 2;  // whole scans up to 16 lanes; wider groups by halves of 8
 #pragma unroll UNR
         for (int k0 = 0; k0 < mw; k0 += 4) {
             const zs_v4i dv = t0v[k0 >> 2], sv = t1v[k0 >> 2];
+            uint32_t vn = 0u, dn = 0u;
 #pragma unroll
             for (int u = 0; u < 4; u++) {
-                const bool e = mv && k0 + u < j && dv[u] >= 0;
-                vac |= (unsigned long long)(e && sv[u] == tgt) << (k0 + u);
-                dep |= (unsigned long long)(e && (sv[u] == tgt || dv[u] == tgt)) << (k0 + u);
+                const bool a = sv[u] == tgt;
+                vn |= a ? 1u << u : 0u;
+                dn |= (a || dv[u] == tgt) ? 1u << u : 0u;
             }
+            vacm |= (MaskT)vn << k0;
+            depm |= (MaskT)dn << k0;
         }
+        const MaskT ltm = (MaskT)((1ull << j) - 1ull);
+        const unsigned long long vac = mv ? (unsigned long long)(vacm & ltm) : 0ull;
+        const unsigned long long dep = mv ? (unsigned long long)(depm & ltm) : 0ull;
         // the target's own move earlier in the chunk
         int tmv = -1, tdst = 0;
         if (et >= 0) {
@@ -1043,17 +1052,19 @@ __device__ __forceinline__ void grp_execute(const Dev& d, Grp& c, int n, int& po
         bool last = inr;
         uint32_t ovf = 0u;  // an obstacle's life after one of the hits left the int16 / int32 range
         const bool ohit = __ballot(inr && tgt < 0) != 0ull;  // some obstacle is hit in the wave's chunks
-        if (!ohit) {
-            // entity targets only (the common chunk): a life stays within a few hundred of 0, so no hit
-            // saturates (the same values as the loop below, fewer instructions)
+        if (!ohit && __ballot(inr && life > 100) == 0ull) {
+            // entity targets at most at MAX_LIFE (the common chunk; only a state poke sets more): no hit
+            // saturates, and min(life + hit, 100) is both an attack (hit < 0) and a capped heal.  A lane that
+            // hits nothing ends with last = false and an unused life, so the entries need no inr test; a
+            // no-hit entry's target (0x7fffffff) matches no lane's.  The same values as the loop below.
 #pragma unroll UNR
             for (int k0 = 0; k0 < mw; k0 += 4) {
                 const zs_v4i tv = t0v[k0 >> 2], hvv = t1v[k0 >> 2];
 #pragma unroll
                 for (int u = 0; u < 4; u++) {
-                    const int k = k0 + u, hk = hvv[u];
-                    const bool same = inr && tv[u] == tgt;
-                    const int nl = hk < 0 ? life + hk : min(life + hk, ml);
+                    const int k = k0 + u;
+                    const bool same = tv[u] == tgt;
+                    const int nl = min(life + hvv[u], 100);
                     life = (same && k <= j) ? nl : life;
                     last = last && !(same && k > j);
                 }
