@@ -14,12 +14,14 @@ if [ -z "$NO_TESTS" ]; then
       || { tail -30 "$OUT/pytest_gpu.log"; exit 1; }
   tail -1 "$OUT/pytest_gpu.log"
 fi
-timeout -k 10 300 python bench.py > "$OUT/bench_default.log" 2>&1 || { tail -5 "$OUT/bench_default.log"; exit 1; }
-tail -1 "$OUT/bench_default.log" | cut -c1-200
-for cfg in ${CFGS:-c3 c2 c4 c5 n8}; do
-    timeout -k 10 180 python bench.py $(args $cfg) --steps 200 --warmup 20 --no-cpu-baseline > "$OUT/bench_$cfg.log" 2>&1 \
-        || { tail -5 "$OUT/bench_$cfg.log"; exit 1; }
-done
+if [ -z "$NO_BENCH" ]; then
+  timeout -k 10 300 python bench.py > "$OUT/bench_default.log" 2>&1 || { tail -5 "$OUT/bench_default.log"; exit 1; }
+  tail -1 "$OUT/bench_default.log" | cut -c1-200
+  for cfg in ${CFGS:-c3 c2 c4 c5 n8}; do
+      timeout -k 10 180 python bench.py $(args $cfg) --steps 200 --warmup 20 --no-cpu-baseline > "$OUT/bench_$cfg.log" 2>&1 \
+          || { tail -5 "$OUT/bench_$cfg.log"; exit 1; }
+  done
+fi
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null || exit 2
 for cfg in ${PCFGS:-c3 c4 c5 n8}; do
     P=$PWD/$OUT/prof_$cfg
