@@ -1553,7 +1553,7 @@ __device__ __forceinline__ void tick_wg(const Dev& d0, int wg, const int32_t* ac
 #endif
     constexpr int NE = 64 / G;
 #ifndef ZS_DIAG_STOP
-#define ZS_DIAG_STOP 0  // diagnostic builds only: end the tick after phase k (1 stage-in ... 5 MT refill; 6-10 inside the execution)
+#define ZS_DIAG_STOP 0  // diagnostic builds only: end the tick after phase k (1 stage-in ... 5 MT refill; 6-10 inside the execution; 11-12 in the leader part)
 #endif
 #define ZS_STOP_AFTER(k) \
     if (ZS_DIAG_STOP == (k)) return
@@ -1890,7 +1890,7 @@ __device__ __forceinline__ void tick_wg(const Dev& d0, int wg, const int32_t* ac
     STAMP(3);
     ZS_RELOAD_DEV();
     ZS_STOP_AFTER(3);
-    if (ZS_DIAG_STOP >= 6) return;  // the execution's own stop points (6: the shuffle only, 7-10 in grp_execute)
+    if (ZS_DIAG_STOP >= 6 && ZS_DIAG_STOP <= 10) return;  // the execution's own stop points (6: the shuffle only, 7-10 in grp_execute)
     if (leader && stepping) {
         c.n_order = n_order;
         c.t = MISC(c, MISC_T) + 1;
@@ -1909,8 +1909,10 @@ __device__ __forceinline__ void tick_wg(const Dev& d0, int wg, const int32_t* ac
         }
     }
     wave_sync();
+    ZS_STOP_AFTER(11);  // diagnostic builds: 11 after the leader's first part, 12 after the group's cleanup
     env_cleanup_group<G>(*dp, c, stepping);
     wave_sync();
+    ZS_STOP_AFTER(12);
     if (leader && stepping) {
         if (MISC(c, MISC_NMOVED) >= 0) env_step_leader_b(*dp, c, rew, done_out, trunc_out, listed_out);
         if (c.fin && (dp->flags & ZS_FLAG_AUTORESET)) {
